@@ -1,0 +1,152 @@
+/*
+ * pcgpu.h — C ABI of the MI355X (gfx950) identity hot path of person_capture.
+ *
+ * This is the drop-in boundary that replaces the reference's inference runtimes
+ * (SURVEY.md §8b). Plain pointers and sizes only; no torch or HIP types appear in
+ * the signatures (streams are passed as void*). Every function returns an int
+ * status (PC_OK == 0); the message of the last failure on a context is available
+ * from pc_last_error(). Device pointers ("d_") are HIP device allocations on the
+ * context's device; host pointers ("h_") are ordinary CPU memory.
+ *
+ * Which reference interface each entry point replaces (file:line in the reference
+ * snapshot xmarre/person_capture):
+ *
+ *   pc_ctx_create / pc_ctx_destroy     ORT InferenceSession(..., providers=[TRT, CUDA, CPU]) setup
+ *                                      person_capture/face_embedder.py:557-703, 848-953
+ *   pc_net_create                      model load: SCRFD ONNX session (face_embedder.py:1102-1147),
+ *                                      ArcFace ONNX session (face_embedder.py:891-953),
+ *                                      YOLO(path) (detectors.py:84-269)
+ *   pc_net_run                         session.run / run_with_iobinding (face_embedder.py:1331-1343, 1369)
+ *   pc_letterbox                       [ext] insightface SCRFD.detect letterbox + cv2.dnn.blobFromImage
+ *                                      (called at face_embedder.py:2185)
+ *   pc_scrfd_detect                    [ext] SCRFD.detect(img, input_size=(D, D)) -> (det Nx5, kpss Nx5x2)
+ *                                      (face_embedder.py:2176-2187)
+ *   pc_warp_affine                     cv2.warpAffine(face, M, (112,112), INTER_LINEAR, BORDER_REFLECT)
+ *                                      (face_embedder.py:1465-1473)
+ *   pc_face_quality                    FaceEmbedder._face_quality (face_embedder.py:1274-1276)
+ *   pc_arcface_embed                   FaceEmbedder._arcface_encode (face_embedder.py:1290-1389)
+ *   pc_embed_finalize                  flip-sum + L2 (face_embedder.py:1383-1389)
+ *   pc_bank_match                      Processor._fd_min (gui_app.py:660-674), batched
+ *   pc_rotate_pad                      cv2.rotate + cv2.copyMakeBorder(BORDER_REPLICATE)
+ *                                      (face_embedder.py:2165-2169, 2292-2294, 2394)
+ *   pc_resize_area                     cv2.resize(..., INTER_AREA) (gui_app.py:1505-1507)
+ */
+#ifndef PCGPU_H
+#define PCGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PC_ABI_VERSION 1
+
+#define PC_OK 0
+#define PC_ERR_ARG 1
+#define PC_ERR_HIP 2
+#define PC_ERR_STATE 3
+#define PC_ERR_FORMAT 4
+#define PC_ERR_CAPACITY 5
+
+/* arithmetic of a network: f16 storage + f32 accumulation (throughput), or
+ * exact f32 (parity runs against the CPU oracle). */
+#define PC_PREC_F16 0
+#define PC_PREC_F32 1
+
+typedef struct pc_ctx pc_ctx;
+typedef struct pc_net pc_net;
+
+/* One letterbox job (SCRFD input): BGR u8 frame on device -> resized into the
+ * top-left of a DxD canvas. scale_x/scale_y are 1/(new/old) as cv::resize uses. */
+typedef struct pc_letterbox_desc {
+  const uint8_t* d_src;
+  int32_t H, W, row_stride;
+  int32_t new_w, new_h;
+  double scale_x, scale_y;
+  int32_t simd_end; /* byte index of each row where OpenCV's SIMD vertical pass stops */
+  int32_t pad_;
+} pc_letterbox_desc;
+
+/* One warpAffine job: crop (top-left pointer + size) -> out_w x out_h x 3 u8.
+ * M is the dst->src affine map (cv::warpAffine's internal inverse). */
+typedef struct pc_warp_desc {
+  const uint8_t* d_src;
+  int32_t row_stride;
+  int32_t w, h;
+  int32_t pad0_;
+  double M[6];
+  uint8_t* d_dst;
+  int32_t out_w, out_h;
+  int32_t border; /* 2 = BORDER_REFLECT, 4 = BORDER_REFLECT_101 */
+  int32_t pad1_;
+} pc_warp_desc;
+
+/* One INTER_AREA coefficient: source index, destination index, weight. */
+typedef struct pc_area_tab {
+  int32_t si;
+  int32_t di;
+  float alpha;
+} pc_area_tab;
+
+int pc_abi_version(void);
+
+/* ---- context ---- */
+int pc_ctx_create(int device_id, pc_ctx** out);
+int pc_ctx_destroy(pc_ctx* ctx);
+const char* pc_last_error(const pc_ctx* ctx);
+int pc_ctx_set_stream(pc_ctx* ctx, void* hip_stream); /* NULL = context-owned stream */
+void* pc_ctx_stream(pc_ctx* ctx);
+int pc_ctx_sync(pc_ctx* ctx);
+int pc_device_alloc(pc_ctx* ctx, size_t bytes, void** d_out);
+int pc_device_free(pc_ctx* ctx, void* d_ptr);
+int pc_copy_h2d(pc_ctx* ctx, void* d_dst, const void* h_src, size_t bytes); /* stream-ordered */
+int pc_copy_d2h(pc_ctx* ctx, void* h_dst, const void* d_src, size_t bytes); /* stream-ordered */
+int pc_copy_d2d(pc_ctx* ctx, void* d_dst, const void* d_src, size_t bytes);
+int pc_memset(pc_ctx* ctx, void* d_dst, int value, size_t bytes);
+
+/* ---- networks (serialized program produced by person_capture_amd.netdef) ---- */
+int pc_net_create(pc_ctx* ctx, const void* h_program, size_t program_bytes, int precision, int max_batch,
+                  pc_net** out);
+int pc_net_destroy(pc_net* net);
+/* d_input: NHWC, dims as pc_net_input_dims; activation dtype of the net's precision */
+int pc_net_run(pc_net* net, const void* d_input, int batch);
+int pc_net_input_dims(pc_net* net, int32_t* h_dims4 /* H, W, C, pixel stride */);
+int pc_net_output(pc_net* net, int index, void** d_ptr, int32_t* h_dims5 /* H, W, C, pixel stride, is_f32 */);
+int pc_net_num_outputs(pc_net* net);
+/* algorithmic FLOPs per image (2*MAC over all conv layers) and kernel launches per run */
+int pc_net_stats(pc_net* net, double* h_flops_per_image, int32_t* h_launches);
+/* capture pc_net_run(batch) into a HIP graph and replay it on later runs of the same batch */
+int pc_net_set_graph(pc_net* net, int enable);
+
+/* ---- image kernels ---- */
+int pc_letterbox(pc_ctx* ctx, int precision, const pc_letterbox_desc* h_descs, int n, int D, void* d_out);
+int pc_warp_affine(pc_ctx* ctx, const pc_warp_desc* h_descs, int n);
+int pc_face_quality(pc_ctx* ctx, const uint8_t* d_chips, int n, int side, double* d_out);
+int pc_arcface_prep(pc_ctx* ctx, int precision, const uint8_t* d_chips, int n, int side, int flip, void* d_out);
+int pc_rotate_pad(pc_ctx* ctx, const uint8_t* d_src, int H, int W, int row_stride, int deg, int pad, uint8_t* d_dst);
+int pc_resize_area(pc_ctx* ctx, const uint8_t* d_src, int row_stride, const pc_area_tab* h_xtab,
+                   const int32_t* h_xstart, int n_x, const pc_area_tab* h_ytab, const int32_t* h_ystart, int n_y,
+                   uint8_t* d_dst, int OH, int OW);
+
+/* ---- detection ---- */
+/* Runs letterbox -> SCRFD net -> decode(score >= det_thresh) -> NMS(nms_thresh) for n frames.
+ * Outputs (device): d_dets [n][max_det][5], d_kps [n][max_det][10], d_count [n] (number kept,
+ * may exceed max_det: then only the first max_det rows are written), d_ncand [n] candidates
+ * above threshold (capacity 8192 per frame; more is PC_ERR_CAPACITY on the next call). */
+int pc_scrfd_detect(pc_net* net, const pc_letterbox_desc* h_descs, int n, int D, float det_thresh,
+                    float nms_thresh, const float* h_det_scale, int max_det, float* d_dets, float* d_kps,
+                    int32_t* d_count, int32_t* d_ncand);
+
+/* ---- embedding / match ---- */
+int pc_embed_finalize(pc_ctx* ctx, const float* d_e, int ld, int n, int dim, int flip, float* d_out);
+/* chips: [n][side][side][3] BGR u8 (side == net input side). d_feat: [n][dim] unit f32 */
+int pc_arcface_embed(pc_net* net, const uint8_t* d_chips, int n, int flip, float* d_feat);
+int pc_bank_match(pc_ctx* ctx, const float* d_q, int n, const float* d_bank, int b, int dim, float* d_fd,
+                  int32_t* d_idx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PCGPU_H */

@@ -1,0 +1,113 @@
+"""ctypes binding of libpcgpu.so (the C ABI in include/pcgpu.h).
+
+Loaded the way the reference loads its native preview DLL
+(person_capture/hdr_preview.py:19-102): explicit argtypes/restype, opaque
+context pointers. There is no fallback: if the library is missing or fails to
+load, every GPU entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+LIB_PATH = Path(__file__).resolve().parent / "lib" / "libpcgpu.so"
+
+PC_OK = 0
+PC_PREC_F16 = 0
+PC_PREC_F32 = 1
+
+_lib = None
+
+
+class LetterboxDesc(C.Structure):
+    _fields_ = [("d_src", C.c_void_p), ("H", C.c_int32), ("W", C.c_int32), ("row_stride", C.c_int32),
+                ("new_w", C.c_int32), ("new_h", C.c_int32), ("scale_x", C.c_double), ("scale_y", C.c_double),
+                ("simd_end", C.c_int32), ("pad_", C.c_int32)]
+
+
+class WarpDesc(C.Structure):
+    _fields_ = [("d_src", C.c_void_p), ("row_stride", C.c_int32), ("w", C.c_int32), ("h", C.c_int32),
+                ("pad0_", C.c_int32), ("M", C.c_double * 6), ("d_dst", C.c_void_p), ("out_w", C.c_int32),
+                ("out_h", C.c_int32), ("border", C.c_int32), ("pad1_", C.c_int32)]
+
+
+class AreaTab(C.Structure):
+    _fields_ = [("si", C.c_int32), ("di", C.c_int32), ("alpha", C.c_float)]
+
+
+assert C.sizeof(LetterboxDesc) == 56 and C.sizeof(WarpDesc) == 96 and C.sizeof(AreaTab) == 12
+
+_P = C.c_void_p
+_I = C.c_int
+_SZ = C.c_size_t
+_F = C.c_float
+
+SIGNATURES = {
+    "pc_abi_version": ([], _I),
+    "pc_ctx_create": ([_I, C.POINTER(_P)], _I),
+    "pc_ctx_destroy": ([_P], _I),
+    "pc_last_error": ([_P], C.c_char_p),
+    "pc_ctx_set_stream": ([_P, _P], _I),
+    "pc_ctx_stream": ([_P], _P),
+    "pc_ctx_sync": ([_P], _I),
+    "pc_device_alloc": ([_P, _SZ, C.POINTER(_P)], _I),
+    "pc_device_free": ([_P, _P], _I),
+    "pc_copy_h2d": ([_P, _P, _P, _SZ], _I),
+    "pc_copy_d2h": ([_P, _P, _P, _SZ], _I),
+    "pc_copy_d2d": ([_P, _P, _P, _SZ], _I),
+    "pc_memset": ([_P, _P, _I, _SZ], _I),
+    "pc_net_create": ([_P, _P, _SZ, _I, _I, C.POINTER(_P)], _I),
+    "pc_net_destroy": ([_P], _I),
+    "pc_net_run": ([_P, _P, _I], _I),
+    "pc_net_input_dims": ([_P, C.POINTER(C.c_int32)], _I),
+    "pc_net_output": ([_P, _I, C.POINTER(_P), C.POINTER(C.c_int32)], _I),
+    "pc_net_num_outputs": ([_P], _I),
+    "pc_net_stats": ([_P, C.POINTER(C.c_double), C.POINTER(C.c_int32)], _I),
+    "pc_net_set_graph": ([_P, _I], _I),
+    "pc_letterbox": ([_P, _I, C.POINTER(LetterboxDesc), _I, _I, _P], _I),
+    "pc_warp_affine": ([_P, C.POINTER(WarpDesc), _I], _I),
+    "pc_face_quality": ([_P, _P, _I, _I, _P], _I),
+    "pc_arcface_prep": ([_P, _I, _P, _I, _I, _I, _P], _I),
+    "pc_rotate_pad": ([_P, _P, _I, _I, _I, _I, _I, _P], _I),
+    "pc_resize_area": ([_P, _P, _I, C.POINTER(AreaTab), C.POINTER(C.c_int32), _I, C.POINTER(AreaTab),
+                        C.POINTER(C.c_int32), _I, _P, _I, _I], _I),
+    "pc_scrfd_detect": ([_P, C.POINTER(LetterboxDesc), _I, _I, _F, _F, C.POINTER(_F), _I, _P, _P, _P, _P], _I),
+    "pc_embed_finalize": ([_P, _P, _I, _I, _I, _I, _P], _I),
+    "pc_arcface_embed": ([_P, _P, _I, _I, _P], _I),
+    "pc_bank_match": ([_P, _P, _I, _P, _I, _I, _P, _P], _I),
+}
+
+
+def load(path: os.PathLike = LIB_PATH) -> C.CDLL:
+    """Load libpcgpu.so (raises if absent: the GPU path has no CPU fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    p = Path(path)
+    if not p.is_file():
+        raise RuntimeError(f"pcgpu native library not built: {p} (run __graft_entry__.build() or make -C "
+                           f"person_capture_amd/csrc)")
+    try:
+        # the torch-ROCm HIP runtime (same soname) must be the one this library binds to
+        import torch  # noqa: F401
+    except Exception:
+        pass
+    lib = C.CDLL(str(p))
+    for name, (args, res) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    if lib.pc_abi_version() != 1:
+        raise RuntimeError("pcgpu ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def check(rc: int, ctx=None, what: str = "") -> None:
+    if rc != PC_OK:
+        msg = ""
+        if ctx is not None and _lib is not None:
+            m = _lib.pc_last_error(ctx)
+            msg = m.decode() if m else ""
+        raise RuntimeError(f"pcgpu {what} failed (status {rc}): {msg}")

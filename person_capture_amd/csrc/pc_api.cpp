@@ -1,0 +1,688 @@
+// C-ABI layer (include/pcgpu.h): contexts, the network executor and the
+// domain entry points of the identity hot path. Compiled by hipcc for gfx950.
+//
+// A network arrives as a serialized "program" (person_capture_amd/netdef.py):
+// buffers, NHWC tensor views, float arrays and a flat op list (CONV / STEM /
+// MAXPOOL). The executor resolves views to device pointers for the run's batch,
+// picks a conv tile per layer and launches the kernels of pc_conv.hip in order on
+// the context stream; optionally the whole run is captured into a HIP graph.
+#include <hip/hip_runtime.h>
+#include <string.h>
+#include <stdio.h>
+#include <string>
+#include <vector>
+#include <map>
+#include <algorithm>
+#include "../../include/pcgpu.h"
+#include "pc_common.h"
+
+namespace pc {
+hipError_t conv_launch(int f32, int rowb, int bc, int bp, const ConvParams& p, hipStream_t s);
+hipError_t splitk_reduce_launch(int f32, const float* part, int splitk, int M, int npad, int cout, const float* bias,
+                                const float* slope, int act, void* y, int ycs, int out_f32, hipStream_t s);
+hipError_t stem_launch(int f32, const StemParams& p, hipStream_t s);
+hipError_t maxpool_launch(int f32, const PoolParams& p, hipStream_t s);
+struct LetterboxDesc;
+struct WarpDesc;
+struct AreaTab;
+hipError_t letterbox_launch(int f32, const LetterboxDesc* d_descs, int N, int D, void* out, hipStream_t s);
+hipError_t warp_launch(const WarpDesc* d_descs, int N, int max_pixels, hipStream_t s);
+hipError_t quality_launch(const uint8_t* chips, int N, int side, double* out, hipStream_t s);
+hipError_t arcprep_launch(int f32, const uint8_t* chips, int N, int side, int flip, void* out, hipStream_t s);
+hipError_t rotate_pad_launch(const uint8_t* src, int H, int W, int row_stride, int deg, int pad, uint8_t* dst, int OH,
+                             int OW, hipStream_t s);
+hipError_t resize_area_launch(const uint8_t* src, int row_stride, const AreaTab* xtab, const int* xstart,
+                              const AreaTab* ytab, const int* ystart, uint8_t* dst, int OH, int OW, hipStream_t s);
+hipError_t embed_finalize_launch(const float* e, int ld, int n, int dim, int flip, float* out, hipStream_t s);
+hipError_t bank_match_launch(const float* q, int n, const float* bank, int B, int dim, float* fd, int* idx,
+                             hipStream_t s);
+struct DecodeLevel {
+  const float* out;
+  int H, W, cs, stride;
+  int loc_offset;
+  int anchor_offset;
+};
+struct DecodeParams {
+  DecodeLevel lv[3];
+  int nlv;
+  int total_loc;
+  float thresh;
+  const float* det_scale;
+  float* cand;
+  int* count;
+  int cap;
+};
+hipError_t scrfd_decode_launch(const DecodeParams& p, int N, hipStream_t s);
+hipError_t scrfd_nms_launch(const float* cand, const int* count, int cap, float nms_thresh, int max_det, float* dets,
+                            float* kps, int* nkeep, int N, hipStream_t s);
+}  // namespace pc
+
+using namespace pc;
+
+static_assert(sizeof(pc_letterbox_desc) == 56, "letterbox desc layout");
+static_assert(sizeof(pc_warp_desc) == 96, "warp desc layout");
+static_assert(sizeof(pc_area_tab) == 12, "area tab layout");
+
+struct pc_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipStream_t own_stream = nullptr;
+  std::string err;
+  void* zero = nullptr;
+  // staging ring for small per-call descriptor arrays (pinned host -> device)
+  char* stage_h = nullptr;
+  char* stage_d = nullptr;
+  size_t stage_cap = 0, stage_off = 0;
+  // detection scratch
+  float* cand = nullptr;
+  int* cand_count = nullptr;
+  float* det_scale = nullptr;
+  size_t cand_images = 0;
+};
+
+static int fail(pc_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+#define HIPCHK(ctx, expr)                                                                     \
+  do {                                                                                        \
+    hipError_t _e = (expr);                                                                   \
+    if (_e != hipSuccess)                                                                     \
+      return fail((ctx), PC_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));      \
+  } while (0)
+
+static int stage_copy(pc_ctx* c, const void* h, size_t nbytes, void** d_out) {
+  const size_t bytes = (nbytes + 255) & ~size_t(255);
+  if (bytes > c->stage_cap) return fail(c, PC_ERR_CAPACITY, "staging ring too small");
+  if (c->stage_off + bytes > c->stage_cap) {
+    // wrap: everything previously staged must have been consumed
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->stage_off = 0;
+  }
+  memcpy(c->stage_h + c->stage_off, h, nbytes);
+  HIPCHK(c, hipMemcpyAsync(c->stage_d + c->stage_off, c->stage_h + c->stage_off, nbytes, hipMemcpyHostToDevice,
+                           c->stream));
+  *d_out = c->stage_d + c->stage_off;
+  c->stage_off += bytes;
+  return PC_OK;
+}
+
+extern "C" int pc_abi_version(void) { return PC_ABI_VERSION; }
+
+extern "C" int pc_ctx_create(int device_id, pc_ctx** out) {
+  if (!out) return PC_ERR_ARG;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return PC_ERR_HIP;
+  if (device_id < 0 || device_id >= ndev) return PC_ERR_ARG;
+  pc_ctx* c = new pc_ctx();
+  c->device = device_id;
+  if (hipSetDevice(device_id) != hipSuccess) { delete c; return PC_ERR_HIP; }
+  if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) { delete c; return PC_ERR_HIP; }
+  c->stream = c->own_stream;
+  if (hipMalloc(&c->zero, 4096) != hipSuccess || hipMemset(c->zero, 0, 4096) != hipSuccess) { delete c; return PC_ERR_HIP; }
+  c->stage_cap = 8u << 20;
+  if (hipHostMalloc((void**)&c->stage_h, c->stage_cap, hipHostMallocDefault) != hipSuccess ||
+      hipMalloc((void**)&c->stage_d, c->stage_cap) != hipSuccess) {
+    delete c;
+    return PC_ERR_HIP;
+  }
+  *out = c;
+  return PC_OK;
+}
+
+extern "C" int pc_ctx_destroy(pc_ctx* c) {
+  if (!c) return PC_OK;
+  hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  if (c->zero) hipFree(c->zero);
+  if (c->stage_h) hipHostFree(c->stage_h);
+  if (c->stage_d) hipFree(c->stage_d);
+  if (c->cand) hipFree(c->cand);
+  if (c->cand_count) hipFree(c->cand_count);
+  if (c->det_scale) hipFree(c->det_scale);
+  if (c->own_stream) hipStreamDestroy(c->own_stream);
+  delete c;
+  return PC_OK;
+}
+
+extern "C" const char* pc_last_error(const pc_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+extern "C" int pc_ctx_set_stream(pc_ctx* c, void* s) {
+  if (!c) return PC_ERR_ARG;
+  c->stream = s ? (hipStream_t)s : c->own_stream;
+  return PC_OK;
+}
+extern "C" void* pc_ctx_stream(pc_ctx* c) { return c ? (void*)c->stream : nullptr; }
+extern "C" int pc_ctx_sync(pc_ctx* c) {
+  if (!c) return PC_ERR_ARG;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return PC_OK;
+}
+extern "C" int pc_device_alloc(pc_ctx* c, size_t bytes, void** d) {
+  if (!c || !d) return PC_ERR_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipMalloc(d, bytes ? bytes : 16));
+  return PC_OK;
+}
+extern "C" int pc_device_free(pc_ctx* c, void* d) {
+  if (!c) return PC_ERR_ARG;
+  if (d) HIPCHK(c, hipFree(d));
+  return PC_OK;
+}
+extern "C" int pc_copy_h2d(pc_ctx* c, void* d, const void* h, size_t n) {
+  if (!c) return PC_ERR_ARG;
+  if (n) HIPCHK(c, hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, c->stream));
+  return PC_OK;
+}
+extern "C" int pc_copy_d2h(pc_ctx* c, void* h, const void* d, size_t n) {
+  if (!c) return PC_ERR_ARG;
+  if (n) HIPCHK(c, hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, c->stream));
+  return PC_OK;
+}
+extern "C" int pc_copy_d2d(pc_ctx* c, void* d, const void* s, size_t n) {
+  if (!c) return PC_ERR_ARG;
+  if (n) HIPCHK(c, hipMemcpyAsync(d, s, n, hipMemcpyDeviceToDevice, c->stream));
+  return PC_OK;
+}
+extern "C" int pc_memset(pc_ctx* c, void* d, int v, size_t n) {
+  if (!c) return PC_ERR_ARG;
+  if (n) HIPCHK(c, hipMemsetAsync(d, v, n, c->stream));
+  return PC_OK;
+}
+
+// ===========================================================================
+// network executor
+// ===========================================================================
+enum { OP_CONV = 1, OP_STEM = 2, OP_MAXPOOL = 3 };
+
+struct NetBuf { long long elems; int is_f32; void* d = nullptr; };
+struct NetTensor { int buf, H, W, C, cs, coff, is_f32; };
+struct NetOp { int w[32]; };
+struct ConvPlan { int rowb, bc, bp, splitk; long long M_per_image; };
+
+struct pc_net {
+  pc_ctx* ctx = nullptr;
+  int f32 = 0;
+  int max_batch = 0;
+  int in_tensor = 0;
+  std::vector<NetBuf> bufs;
+  std::vector<NetTensor> tens;
+  std::vector<NetOp> ops;
+  std::vector<int> outs;
+  std::vector<void*> arrays;  // device copies (conv weights in act dtype, others f32)
+  std::vector<long long> array_count;
+  std::vector<ConvPlan> plans;
+  float* partial = nullptr;
+  size_t partial_bytes = 0;
+  double flops_per_image = 0.0;
+  int launches = 0;
+  const void* cur_input = nullptr;
+  // graph replay
+  int use_graph = 0;
+  std::map<std::pair<int, const void*>, hipGraphExec_t> graphs;
+  // arcface scratch
+  void* prep = nullptr;
+  size_t prep_bytes = 0;
+};
+
+static inline int esize(const pc_net* n, int is_f32) { return (is_f32 || n->f32) ? 4 : 2; }
+
+static void* tensor_ptr(pc_net* n, int t) {
+  const NetTensor& T = n->tens[t];
+  if (T.buf < 0) return (void*)((const char*)n->cur_input + (size_t)T.coff * esize(n, T.is_f32));
+  return (char*)n->bufs[T.buf].d + (size_t)T.coff * esize(n, T.is_f32);
+}
+
+static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl) {
+  const int* w = op.w;
+  const int out = w[1], nseg = w[2], npad = w[14];
+  const int esz = n->f32 ? 4 : 2;
+  int rowb = 128;
+  for (int s = 0; s < nseg; ++s) {
+    const NetTensor& X = n->tens[w[3 + 5 * s]];
+    if ((X.C * esz) % 128) rowb = 64;
+    if ((X.C * esz) % 64) return fail(n->ctx, PC_ERR_FORMAT, "conv input channels not a multiple of the K tile");
+  }
+  int bc = 0;
+  for (int cand : {128, 96, 64, 32})
+    if (npad % cand == 0) { bc = cand; break; }
+  if (!bc) return fail(n->ctx, PC_ERR_FORMAT, "conv npad must be a multiple of 32");
+  const NetTensor& Y = n->tens[out];
+  const long long Mimg = (long long)Y.H * Y.W;
+  const long long M = Mimg * n->max_batch;
+  int bp;
+  if (bc == 128) bp = (M / 128) * (npad / 128) >= 512 ? 128 : 64;
+  else if (bc == 96) bp = 128;
+  else bp = (M / 256) * (npad / bc) >= 512 ? 256 : 128;
+  pl.rowb = rowb; pl.bc = bc; pl.bp = bp; pl.M_per_image = Mimg;
+  pl.splitk = w[24] > 1 ? w[24] : 1;
+  if (Y.C > npad) return fail(n->ctx, PC_ERR_FORMAT, "conv output tensor wider than npad");
+  return PC_OK;
+}
+
+extern "C" int pc_net_create(pc_ctx* c, const void* prog, size_t nbytes, int precision, int max_batch, pc_net** out) {
+  if (!c || !prog || !out || max_batch <= 0) return fail(c, PC_ERR_ARG, "pc_net_create: bad arguments");
+  *out = nullptr;
+  const int32_t* P = (const int32_t*)prog;
+  const size_t nw = nbytes / 4;
+  if (nw < 8 || P[0] != 0x544E4350 || P[1] != 1) return fail(c, PC_ERR_FORMAT, "bad program magic/version");
+  HIPCHK(c, hipSetDevice(c->device));
+  pc_net* n = new pc_net();
+  n->ctx = c;
+  n->f32 = precision == PC_PREC_F32;
+  n->max_batch = max_batch;
+  const int nbuf = P[2], nten = P[3], narr = P[4], nop = P[5], nout = P[6];
+  n->in_tensor = P[7];
+  size_t pos = 8;
+  auto need = [&](size_t k) { return pos + k <= nw; };
+  if (!need((size_t)nbuf * 4 + (size_t)nten * 8 + (size_t)narr * 4 + nout + (size_t)nop * 32)) {
+    delete n;
+    return fail(c, PC_ERR_FORMAT, "truncated program");
+  }
+  for (int i = 0; i < nbuf; ++i, pos += 4) {
+    NetBuf b;
+    b.elems = (long long)(uint32_t)P[pos] | ((long long)P[pos + 1] << 32);
+    b.is_f32 = P[pos + 2];
+    n->bufs.push_back(b);
+  }
+  for (int i = 0; i < nten; ++i, pos += 8) {
+    NetTensor t{P[pos], P[pos + 1], P[pos + 2], P[pos + 3], P[pos + 4], P[pos + 5], P[pos + 6]};
+    n->tens.push_back(t);
+  }
+  std::vector<std::pair<long long, long long>> arr;
+  for (int i = 0; i < narr; ++i, pos += 4) {
+    long long off = (long long)(uint32_t)P[pos] | ((long long)P[pos + 1] << 32);
+    long long cnt = (long long)(uint32_t)P[pos + 2] | ((long long)P[pos + 3] << 32);
+    arr.push_back({off, cnt});
+  }
+  for (int i = 0; i < nout; ++i) n->outs.push_back(P[pos++]);
+  for (int i = 0; i < nop; ++i, pos += 32) {
+    NetOp op;
+    memcpy(op.w, P + pos, 32 * 4);
+    n->ops.push_back(op);
+  }
+  const float* data = (const float*)(P + pos);
+  const size_t ndata = nw - pos;
+  // which arrays are conv weights (uploaded in the activation dtype)
+  std::vector<int> is_w(narr, 0);
+  for (auto& op : n->ops)
+    if (op.w[0] == OP_CONV && op.w[13] >= 0) is_w[op.w[13]] = 1;
+  n->arrays.assign(narr, nullptr);
+  n->array_count.assign(narr, 0);
+  int rc = PC_OK;
+  for (int i = 0; i < narr && rc == PC_OK; ++i) {
+    const long long off = arr[i].first, cnt = arr[i].second;
+    if (off < 0 || cnt < 0 || (size_t)(off + cnt) > ndata) { rc = fail(c, PC_ERR_FORMAT, "array out of range"); break; }
+    n->array_count[i] = cnt;
+    if (is_w[i] && !n->f32) {
+      std::vector<_Float16> h(cnt);
+      for (long long k = 0; k < cnt; ++k) h[k] = (_Float16)data[off + k];
+      if (hipMalloc(&n->arrays[i], cnt * 2 + 16) != hipSuccess ||
+          hipMemcpy(n->arrays[i], h.data(), cnt * 2, hipMemcpyHostToDevice) != hipSuccess)
+        rc = fail(c, PC_ERR_HIP, "weight upload failed");
+    } else {
+      if (hipMalloc(&n->arrays[i], cnt * 4 + 16) != hipSuccess ||
+          hipMemcpy(n->arrays[i], data + off, cnt * 4, hipMemcpyHostToDevice) != hipSuccess)
+        rc = fail(c, PC_ERR_HIP, "array upload failed");
+    }
+  }
+  for (size_t i = 0; i < n->bufs.size() && rc == PC_OK; ++i) {
+    NetBuf& b = n->bufs[i];
+    const size_t bytes = (size_t)b.elems * max_batch * ((b.is_f32 || n->f32) ? 4 : 2) + 256;
+    if (hipMalloc(&b.d, bytes) != hipSuccess) rc = fail(c, PC_ERR_HIP, "activation buffer allocation failed");
+    else hipMemset(b.d, 0, bytes);  // channel padding lanes must read as zero
+  }
+  // plans + split-K workspace + stats
+  n->plans.resize(n->ops.size());
+  size_t part = 0;
+  for (size_t i = 0; i < n->ops.size() && rc == PC_OK; ++i) {
+    const NetOp& op = n->ops[i];
+    if (op.w[0] == OP_CONV) {
+      rc = plan_conv(n, op, n->plans[i]);
+      if (rc) break;
+      const ConvPlan& pl = n->plans[i];
+      if (pl.splitk > 1) part = std::max(part, (size_t)((long long)pl.splitk * pl.M_per_image * max_batch * op.w[14] * 4));
+      const NetTensor& Y = n->tens[op.w[1]];
+      double macs = 0.0;
+      for (int s = 0; s < op.w[2]; ++s) {
+        const NetTensor& X = n->tens[op.w[3 + 5 * s]];
+        (void)X;
+        // algorithmic MACs: real output channels x real taps x input channels (padded lanes excluded by the
+        // program: w[25+s] carries the true input channel count)
+        const int cin_true = op.w[25 + s] > 0 ? op.w[25 + s] : X.C;
+        macs += (double)Y.H * Y.W * op.w[16] * op.w[4 + 5 * s] * op.w[5 + 5 * s] * cin_true;
+      }
+      n->flops_per_image += 2.0 * macs;
+      n->launches += pl.splitk > 1 ? 2 : 1;
+    } else if (op.w[0] == OP_STEM) {
+      const NetTensor& Y = n->tens[op.w[1]];
+      const int cin_true = op.w[13] > 0 ? op.w[13] : 3;
+      n->flops_per_image += 2.0 * Y.H * Y.W * op.w[8] * op.w[3] * op.w[4] * cin_true;
+      n->launches += 1;
+    } else if (op.w[0] == OP_MAXPOOL) {
+      n->launches += 1;
+    } else {
+      rc = fail(c, PC_ERR_FORMAT, "unknown op type");
+    }
+  }
+  if (rc == PC_OK && part) {
+    if (hipMalloc((void**)&n->partial, part) != hipSuccess) rc = fail(c, PC_ERR_HIP, "split-K workspace");
+    n->partial_bytes = part;
+  }
+  if (rc != PC_OK) {
+    pc_net_destroy(n);
+    return rc;
+  }
+  *out = n;
+  return PC_OK;
+}
+
+extern "C" int pc_net_destroy(pc_net* n) {
+  if (!n) return PC_OK;
+  hipSetDevice(n->ctx->device);
+  hipStreamSynchronize(n->ctx->stream);
+  for (auto& kv : n->graphs) hipGraphExecDestroy(kv.second);
+  for (void* a : n->arrays) if (a) hipFree(a);
+  for (auto& b : n->bufs) if (b.d) hipFree(b.d);
+  if (n->partial) hipFree(n->partial);
+  if (n->prep) hipFree(n->prep);
+  delete n;
+  return PC_OK;
+}
+
+static int run_ops(pc_net* n, int N) {
+  pc_ctx* c = n->ctx;
+  hipStream_t s = c->stream;
+  for (size_t i = 0; i < n->ops.size(); ++i) {
+    const int* w = n->ops[i].w;
+    if (w[0] == OP_CONV) {
+      const ConvPlan& pl = n->plans[i];
+      ConvParams p;
+      memset(&p, 0, sizeof(p));
+      const NetTensor& Y = n->tens[w[1]];
+      p.nseg = w[2];
+      const int bke = pl.rowb / (n->f32 ? 4 : 2);
+      int kt = 0;
+      for (int sg = 0; sg < p.nseg; ++sg) {
+        const NetTensor& X = n->tens[w[3 + 5 * sg]];
+        ConvSeg& S = p.seg[sg];
+        S.x = tensor_ptr(n, w[3 + 5 * sg]);
+        S.H = X.H; S.W = X.W; S.C = X.C; S.cs = X.cs;
+        S.KH = w[4 + 5 * sg]; S.KW = w[5 + 5 * sg]; S.stride = w[6 + 5 * sg]; S.pad = w[7 + 5 * sg];
+        S.cblk = X.C / bke;
+        S.kt = S.KH * S.KW * S.cblk;
+        kt += S.kt;
+      }
+      p.w = n->arrays[w[13]];
+      p.ktot = w[15];
+      p.N = N; p.OH = Y.H; p.OW = Y.W; p.M = N * Y.H * Y.W;
+      p.npad = w[14];
+      p.cout = w[16];
+      p.cwrite = std::min(Y.C, p.npad);
+      p.y = tensor_ptr(n, w[1]);
+      p.ycs = Y.cs;
+      p.out_f32 = Y.is_f32 && !n->f32 ? 1 : (n->f32 ? 1 : 0);
+      p.bias = w[17] >= 0 ? (const float*)n->arrays[w[17]] : nullptr;
+      p.bias_mode = w[17] >= 0 ? w[18] : 0;
+      p.slope = w[19] >= 0 ? (const float*)n->arrays[w[19]] : nullptr;
+      p.act = w[20];
+      p.res = w[21] >= 0 ? tensor_ptr(n, w[21]) : nullptr;
+      p.res_mode = w[21] >= 0 ? w[22] : 0;
+      if (w[21] >= 0) {
+        const NetTensor& R = n->tens[w[21]];
+        p.rcs = R.cs; p.rH = R.H; p.rW = R.W;
+      }
+      p.act_after_res = w[23];
+      p.kt_total = kt;
+      p.splitk = pl.splitk;
+      p.partial = n->partial;
+      p.zero = c->zero;
+      HIPCHK(c, conv_launch(n->f32, pl.rowb, pl.bc, pl.bp, p, s));
+      if (pl.splitk > 1) {
+        HIPCHK(c, splitk_reduce_launch(n->f32, n->partial, pl.splitk, p.M, p.npad, p.cout, p.bias, p.slope, p.act,
+                                       p.y, p.ycs, p.out_f32, s));
+      }
+    } else if (w[0] == OP_STEM) {
+      StemParams p;
+      memset(&p, 0, sizeof(p));
+      const NetTensor& X = n->tens[w[2]];
+      const NetTensor& Y = n->tens[w[1]];
+      p.x = tensor_ptr(n, w[2]);
+      p.N = N; p.H = X.H; p.W = X.W; p.cin = X.C; p.xcs = X.cs;
+      p.OH = Y.H; p.OW = Y.W; p.KH = w[3]; p.KW = w[4]; p.stride = w[5]; p.pad = w[6];
+      p.w = (const float*)n->arrays[w[7]];
+      p.cout = w[8];
+      p.bias = (const float*)n->arrays[w[9]];
+      p.slope = w[10] >= 0 ? (const float*)n->arrays[w[10]] : nullptr;
+      p.act = w[11];
+      p.ycs = Y.cs;
+      p.cpad = w[12];
+      p.y = tensor_ptr(n, w[1]);
+      HIPCHK(c, stem_launch(n->f32, p, s));
+    } else if (w[0] == OP_MAXPOOL) {
+      PoolParams p;
+      const NetTensor& X = n->tens[w[2]];
+      const NetTensor& Y = n->tens[w[1]];
+      p.x = tensor_ptr(n, w[2]); p.N = N; p.H = X.H; p.W = X.W; p.C = X.C; p.xcs = X.cs;
+      p.y = tensor_ptr(n, w[1]); p.OH = Y.H; p.OW = Y.W; p.ycs = Y.cs;
+      p.k = w[3]; p.stride = w[4]; p.pad = w[5];
+      HIPCHK(c, maxpool_launch(n->f32, p, s));
+    }
+  }
+  return PC_OK;
+}
+
+extern "C" int pc_net_run(pc_net* n, const void* d_in, int N) {
+  if (!n || !d_in) return PC_ERR_ARG;
+  pc_ctx* c = n->ctx;
+  if (N <= 0 || N > n->max_batch) return fail(c, PC_ERR_ARG, "batch out of range");
+  n->cur_input = d_in;
+  if (!n->use_graph) return run_ops(n, N);
+  auto key = std::make_pair(N, d_in);
+  auto it = n->graphs.find(key);
+  if (it == n->graphs.end()) {
+    hipGraph_t g;
+    HIPCHK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    int rc = run_ops(n, N);
+    hipError_t e = hipStreamEndCapture(c->stream, &g);
+    if (rc != PC_OK) return rc;
+    if (e != hipSuccess) return fail(c, PC_ERR_HIP, std::string("graph capture: ") + hipGetErrorString(e));
+    hipGraphExec_t ge;
+    e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+    hipGraphDestroy(g);
+    if (e != hipSuccess) return fail(c, PC_ERR_HIP, std::string("graph instantiate: ") + hipGetErrorString(e));
+    it = n->graphs.emplace(key, ge).first;
+  }
+  HIPCHK(c, hipGraphLaunch(it->second, c->stream));
+  return PC_OK;
+}
+
+extern "C" int pc_net_set_graph(pc_net* n, int enable) {
+  if (!n) return PC_ERR_ARG;
+  n->use_graph = enable ? 1 : 0;
+  return PC_OK;
+}
+
+extern "C" int pc_net_input_dims(pc_net* n, int32_t* d) {
+  if (!n || !d) return PC_ERR_ARG;
+  const NetTensor& T = n->tens[n->in_tensor];
+  d[0] = T.H; d[1] = T.W; d[2] = T.C; d[3] = T.cs;
+  return PC_OK;
+}
+extern "C" int pc_net_num_outputs(pc_net* n) { return n ? (int)n->outs.size() : -1; }
+extern "C" int pc_net_output(pc_net* n, int idx, void** d_ptr, int32_t* dims) {
+  if (!n || idx < 0 || idx >= (int)n->outs.size()) return PC_ERR_ARG;
+  const int t = n->outs[idx];
+  const NetTensor& T = n->tens[t];
+  if (d_ptr) *d_ptr = tensor_ptr(n, t);
+  if (dims) { dims[0] = T.H; dims[1] = T.W; dims[2] = T.C; dims[3] = T.cs; dims[4] = (T.is_f32 || n->f32) ? 1 : 0; }
+  return PC_OK;
+}
+extern "C" int pc_net_stats(pc_net* n, double* flops, int32_t* launches) {
+  if (!n) return PC_ERR_ARG;
+  if (flops) *flops = n->flops_per_image;
+  if (launches) *launches = n->launches;
+  return PC_OK;
+}
+
+// ===========================================================================
+// image / detection / embedding entry points
+// ===========================================================================
+extern "C" int pc_letterbox(pc_ctx* c, int prec, const pc_letterbox_desc* h, int n, int D, void* d_out) {
+  if (!c || !h || n <= 0 || D <= 0 || !d_out) return fail(c, PC_ERR_ARG, "pc_letterbox: bad arguments");
+  void* dd;
+  int rc = stage_copy(c, h, sizeof(pc_letterbox_desc) * n, &dd);
+  if (rc) return rc;
+  HIPCHK(c, letterbox_launch(prec == PC_PREC_F32, (const LetterboxDesc*)dd, n, D, d_out, c->stream));
+  return PC_OK;
+}
+
+extern "C" int pc_warp_affine(pc_ctx* c, const pc_warp_desc* h, int n) {
+  if (!c || !h || n < 0) return fail(c, PC_ERR_ARG, "pc_warp_affine: bad arguments");
+  if (n == 0) return PC_OK;
+  int maxpix = 0;
+  for (int i = 0; i < n; ++i) maxpix = std::max(maxpix, h[i].out_w * h[i].out_h);
+  void* dd;
+  int rc = stage_copy(c, h, sizeof(pc_warp_desc) * n, &dd);
+  if (rc) return rc;
+  HIPCHK(c, warp_launch((const WarpDesc*)dd, n, maxpix, c->stream));
+  return PC_OK;
+}
+
+extern "C" int pc_face_quality(pc_ctx* c, const uint8_t* chips, int n, int side, double* out) {
+  if (!c || n < 0 || side <= 0 || side > 128) return fail(c, PC_ERR_ARG, "pc_face_quality: bad arguments");
+  if (n == 0) return PC_OK;
+  HIPCHK(c, quality_launch(chips, n, side, out, c->stream));
+  return PC_OK;
+}
+
+extern "C" int pc_arcface_prep(pc_ctx* c, int prec, const uint8_t* chips, int n, int side, int flip, void* out) {
+  if (!c || n < 0) return fail(c, PC_ERR_ARG, "pc_arcface_prep: bad arguments");
+  if (n == 0) return PC_OK;
+  HIPCHK(c, arcprep_launch(prec == PC_PREC_F32, chips, n, side, flip, out, c->stream));
+  return PC_OK;
+}
+
+extern "C" int pc_rotate_pad(pc_ctx* c, const uint8_t* src, int H, int W, int row_stride, int deg, int pad,
+                             uint8_t* dst) {
+  if (!c || !src || !dst || H <= 0 || W <= 0 || pad < 0 || (deg != 0 && deg != 90 && deg != 180 && deg != 270))
+    return fail(c, PC_ERR_ARG, "pc_rotate_pad: bad arguments");
+  const int RH = (deg == 90 || deg == 270) ? W : H;
+  const int RW = (deg == 90 || deg == 270) ? H : W;
+  HIPCHK(c, rotate_pad_launch(src, H, W, row_stride, deg, pad, dst, RH + 2 * pad, RW + 2 * pad, c->stream));
+  return PC_OK;
+}
+
+extern "C" int pc_resize_area(pc_ctx* c, const uint8_t* src, int row_stride, const pc_area_tab* xt,
+                              const int32_t* xs, int n_x, const pc_area_tab* yt, const int32_t* ys, int n_y,
+                              uint8_t* dst, int OH, int OW) {
+  if (!c || !src || !dst || !xt || !xs || !yt || !ys) return fail(c, PC_ERR_ARG, "pc_resize_area: bad arguments");
+  void *dxt, *dxs, *dyt, *dys;
+  int rc;
+  if ((rc = stage_copy(c, xt, sizeof(pc_area_tab) * n_x, &dxt))) return rc;
+  if ((rc = stage_copy(c, xs, sizeof(int32_t) * (OW + 1), &dxs))) return rc;
+  if ((rc = stage_copy(c, yt, sizeof(pc_area_tab) * n_y, &dyt))) return rc;
+  if ((rc = stage_copy(c, ys, sizeof(int32_t) * (OH + 1), &dys))) return rc;
+  HIPCHK(c, resize_area_launch(src, row_stride, (const AreaTab*)dxt, (const int*)dxs, (const AreaTab*)dyt,
+                               (const int*)dys, dst, OH, OW, c->stream));
+  return PC_OK;
+}
+
+extern "C" int pc_embed_finalize(pc_ctx* c, const float* e, int ld, int n, int dim, int flip, float* out) {
+  if (!c || n < 0) return fail(c, PC_ERR_ARG, "pc_embed_finalize: bad arguments");
+  if (n == 0) return PC_OK;
+  HIPCHK(c, embed_finalize_launch(e, ld, n, dim, flip, out, c->stream));
+  return PC_OK;
+}
+
+extern "C" int pc_bank_match(pc_ctx* c, const float* q, int n, const float* bank, int b, int dim, float* fd,
+                             int32_t* idx) {
+  if (!c || n < 0 || b < 0 || dim <= 0) return fail(c, PC_ERR_ARG, "pc_bank_match: bad arguments");
+  if (n == 0) return PC_OK;
+  HIPCHK(c, bank_match_launch(q, n, bank, b, dim, fd, idx, c->stream));
+  return PC_OK;
+}
+
+extern "C" int pc_arcface_embed(pc_net* net, const uint8_t* chips, int n, int flip, float* feat) {
+  if (!net || n < 0) return PC_ERR_ARG;
+  pc_ctx* c = net->ctx;
+  if (n == 0) return PC_OK;
+  const int rows = flip ? 2 * n : n;
+  if (rows > net->max_batch) return fail(c, PC_ERR_ARG, "pc_arcface_embed: 2n exceeds the net's max batch");
+  const NetTensor& I = net->tens[net->in_tensor];
+  if (I.C != 4 || I.H != I.W) return fail(c, PC_ERR_FORMAT, "arcface net input must be square NHWC4");
+  const size_t need = (size_t)net->max_batch * I.H * I.W * 4 * (net->f32 ? 4 : 2);
+  if (net->prep_bytes < need) {
+    if (net->prep) HIPCHK(c, hipFree(net->prep));
+    HIPCHK(c, hipMalloc(&net->prep, need));
+    net->prep_bytes = need;
+  }
+  HIPCHK(c, arcprep_launch(net->f32, chips, n, I.H, flip, net->prep, c->stream));
+  int rc = pc_net_run(net, net->prep, rows);
+  if (rc) return rc;
+  const NetTensor& O = net->tens[net->outs[0]];
+  const float* e = (const float*)tensor_ptr(net, net->outs[0]);
+  HIPCHK(c, embed_finalize_launch(e, O.cs, n, O.C, flip, feat, c->stream));
+  return PC_OK;
+}
+
+extern "C" int pc_scrfd_detect(pc_net* net, const pc_letterbox_desc* h, int n, int D, float det_thresh,
+                               float nms_thresh, const float* h_det_scale, int max_det, float* dets, float* kps,
+                               int32_t* count, int32_t* ncand) {
+  if (!net || !h || n <= 0 || !h_det_scale || max_det <= 0) return PC_ERR_ARG;
+  pc_ctx* c = net->ctx;
+  if (n > net->max_batch) return fail(c, PC_ERR_ARG, "pc_scrfd_detect: batch exceeds max batch");
+  if ((int)net->outs.size() != 3) return fail(c, PC_ERR_FORMAT, "SCRFD net must have 3 outputs");
+  const NetTensor& I = net->tens[net->in_tensor];
+  if (I.H != D || I.W != D) return fail(c, PC_ERR_ARG, "pc_scrfd_detect: D does not match the net input size");
+  const int cap = 8192;
+  if (c->cand_images < (size_t)n) {
+    if (c->cand) hipFree(c->cand);
+    if (c->cand_count) hipFree(c->cand_count);
+    if (c->det_scale) hipFree(c->det_scale);
+    HIPCHK(c, hipMalloc((void**)&c->cand, (size_t)n * cap * 16 * 4));
+    HIPCHK(c, hipMalloc((void**)&c->cand_count, (size_t)n * 4));
+    HIPCHK(c, hipMalloc((void**)&c->det_scale, (size_t)n * 4));
+    c->cand_images = n;
+  }
+  // letterbox into the net's own input staging area (reuse prep scratch)
+  const size_t need = (size_t)net->max_batch * D * D * 4 * (net->f32 ? 4 : 2);
+  if (net->prep_bytes < need) {
+    if (net->prep) HIPCHK(c, hipFree(net->prep));
+    HIPCHK(c, hipMalloc(&net->prep, need));
+    net->prep_bytes = need;
+  }
+  int rc = pc_letterbox(c, net->f32 ? PC_PREC_F32 : PC_PREC_F16, h, n, D, net->prep);
+  if (rc) return rc;
+  rc = pc_net_run(net, net->prep, n);
+  if (rc) return rc;
+  DecodeParams p;
+  memset(&p, 0, sizeof(p));
+  p.nlv = 3;
+  const int strides[3] = {8, 16, 32};
+  int loc = 0, anc = 0;
+  for (int l = 0; l < 3; ++l) {
+    const NetTensor& O = net->tens[net->outs[l]];
+    if (!(O.is_f32 || net->f32)) return fail(c, PC_ERR_FORMAT, "SCRFD head outputs must be f32");
+    p.lv[l].out = (const float*)tensor_ptr(net, net->outs[l]);
+    p.lv[l].H = O.H; p.lv[l].W = O.W; p.lv[l].cs = O.cs; p.lv[l].stride = strides[l];
+    p.lv[l].loc_offset = loc; p.lv[l].anchor_offset = anc;
+    loc += O.H * O.W;
+    anc += O.H * O.W * 2;
+  }
+  p.total_loc = loc;
+  p.thresh = det_thresh;
+  void* dscale;
+  if ((rc = stage_copy(c, h_det_scale, (size_t)n * 4, &dscale))) return rc;
+  HIPCHK(c, hipMemsetAsync(c->cand_count, 0, n * 4, c->stream));
+  p.det_scale = (const float*)dscale;
+  p.cand = c->cand;
+  p.count = c->cand_count;
+  p.cap = cap;
+  HIPCHK(c, scrfd_decode_launch(p, n, c->stream));
+  HIPCHK(c, scrfd_nms_launch(c->cand, c->cand_count, cap, nms_thresh, max_det, dets, kps, count, n, c->stream));
+  if (ncand) HIPCHK(c, hipMemcpyAsync(ncand, c->cand_count, n * 4, hipMemcpyDeviceToDevice, c->stream));
+  return PC_OK;
+}

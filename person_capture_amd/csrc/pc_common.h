@@ -1,0 +1,75 @@
+// Internal types shared by the gfx950 kernels and the C-ABI layer.
+// Everything here is device-agnostic plain data; the kernels live in pc_*.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pc {
+
+typedef _Float16 f16;
+typedef f16 f16x8 __attribute__((ext_vector_type(8)));
+typedef f16 f16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(1))) void* gptr_t;
+
+enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_PRELU = 2, ACT_SILU = 3 };
+enum BiasMode { BIAS_NONE = 0, BIAS_CHANNEL = 1, BIAS_BORDER9 = 2 };
+enum ResMode { RES_NONE = 0, RES_SAME = 1, RES_UP2 = 2 };
+
+// One K-segment of an implicit-GEMM convolution: a KHxKW window over an NHWC
+// tensor whose (padded) channel count C is a multiple of the K-tile width.
+struct ConvSeg {
+  const void* x;       // NHWC activations, pixel stride `cs` elements
+  int H, W, C, cs;     // input dims, padded channels, pixel stride
+  int KH, KW, stride, pad;
+  int kt;              // K tiles in this segment = KH*KW*(C/BKE)
+  int cblk;            // C / BKE
+};
+
+struct ConvParams {
+  ConvSeg seg[2];
+  int nseg;
+  const void* w;       // [npad][ktot] weights, BN/scale already folded
+  long long ktot;      // weight row stride in elements
+  int N, OH, OW, M;    // output batch/dims, M = N*OH*OW pixels
+  int npad;            // padded output channels (multiple of the channel tile)
+  int cout;            // valid output channels
+  int cwrite;          // channels written (>= cout; lanes in [cout, cwrite) are stored as 0)
+  void* y;             // output NHWC base (channel offset already applied)
+  int ycs;             // output pixel stride (elements)
+  int out_f32;         // 1: write float, 0: write activation dtype
+  const float* bias;   // BIAS_CHANNEL: [npad]; BIAS_BORDER9: [9][npad]
+  int bias_mode;
+  const float* slope;  // PReLU slopes [npad]
+  int act;
+  const void* res;     // residual NHWC (activation dtype)
+  int rcs, res_mode, rH, rW;
+  int act_after_res;   // 1: y = act(acc + b + res); 0: y = act(acc + b) + res
+  float* partial;      // split-K partials [splitk][M][npad]
+  int splitk;
+  int kt_total;
+  const void* zero;    // >= 256 zero bytes (padding taps read from here)
+};
+
+// Direct convolution for tiny input channel counts (network stems, Cin <= 4).
+struct StemParams {
+  const void* x;       // NHWC, pixel stride xcs
+  int N, H, W, cin, xcs;
+  int OH, OW, KH, KW, stride, pad;
+  const float* w;      // [cout][KH][KW][cin] (folded)
+  const float* bias;   // [cout]
+  const float* slope;  // [cout] or null
+  int act;
+  int cout, ycs;       // valid output channels, output pixel stride
+  void* y;
+  int cpad;            // channels written (>= cout, the tail is zero-filled)
+};
+
+struct PoolParams {
+  const void* x; int N, H, W, C, xcs;
+  void* y; int OH, OW, ycs;
+  int k, stride, pad;
+};
+
+}  // namespace pc

@@ -1,0 +1,470 @@
+// Implicit-GEMM convolution engine for gfx950 (CDNA4).
+//
+// One kernel template runs every dense conv of the identity hot path
+// (IResNet ArcFace trunk, SCRFD backbone/neck/heads, the embedding FC as a
+// KxK "valid" conv): out[pixel][cout] = sum_k X_im2col[pixel][k] * W[cout][k].
+//
+// Layout: activations NHWC with channels padded to the K-tile
+// width, weights [cout_pad][K] with K = segment-major, tap-major, channel-minor,
+// BN scales folded in. A workgroup (4 waves, 2x2) owns a BC(channels) x BP(pixels)
+// output tile; each K-tile is one conv tap x ROWB bytes of channels, so every
+// staged LDS row is one contiguous 64/128-byte run of a single pixel (im2col
+// gather) or of a single output channel (weights). Rows are moved HBM->LDS with
+// 16-byte global_load_lds (LDS-DMA, no VGPR round trip); padding taps point at a
+// zero page so the staging is branch-free. The LDS image is XOR-swizzled on the
+// source side so the ds_read_b128 fragment reads are bank-conflict free
+// (verified by brute force over the gfx950 16-lane groups).
+// MFMA: v_mfma_f32_16x16x32_f16 (fast path) or v_mfma_f32_16x16x4_f32 (exact
+// f32 parity path); fp32 accumulation; fused epilogue = bias (optionally the
+// 9-class border table of a folded pre-BN) + ReLU/PReLU/SiLU + residual (same
+// pixel or nearest-2x upsampled) in either order, or split-K fp32 partials.
+//
+// A second, optional K-segment lets a residual block's shortcut projection
+// (IResNet downsample 1x1/s2, ResNetV1e avg-down == 2x2/s2 conv) accumulate into
+// the same tile, so shortcut + main branch cost one launch and one output write.
+#include "pc_common.h"
+
+namespace pc {
+
+__device__ __forceinline__ float act_apply(float v, int act, float slope) {
+  if (act == ACT_RELU) return v > 0.f ? v : 0.f;
+  if (act == ACT_PRELU) return v > 0.f ? v : v * slope;
+  if (act == ACT_SILU) return v / (1.0f + __expf(-v));
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ void store4(T* dst, const float* v, int n);
+
+template <>
+__device__ __forceinline__ void store4<f16>(f16* dst, const float* v, int n) {
+  if (n >= 4) {
+    f16x4 h = {(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
+    *reinterpret_cast<f16x4*>(dst) = h;
+  } else {
+    for (int j = 0; j < n; ++j) dst[j] = (f16)v[j];
+  }
+}
+template <>
+__device__ __forceinline__ void store4<float>(float* dst, const float* v, int n) {
+  if (n >= 4) {
+    *reinterpret_cast<f32x4*>(dst) = f32x4{v[0], v[1], v[2], v[3]};
+  } else {
+    for (int j = 0; j < n; ++j) dst[j] = v[j];
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void load4(const T* src, float* v, int n) {
+  if constexpr (sizeof(T) == 2) {
+    if (n >= 4) {
+      f16x4 h = *reinterpret_cast<const f16x4*>(src);
+      v[0] = (float)h[0]; v[1] = (float)h[1]; v[2] = (float)h[2]; v[3] = (float)h[3];
+      return;
+    }
+  } else {
+    if (n >= 4) {
+      f32x4 h = *reinterpret_cast<const f32x4*>(src);
+      v[0] = h[0]; v[1] = h[1]; v[2] = h[2]; v[3] = h[3];
+      return;
+    }
+  }
+  for (int j = 0; j < n; ++j) v[j] = (float)src[j];
+}
+
+template <typename T, int BC, int BP, int ROWB>
+__global__ __launch_bounds__(256, 2) void conv_igemm(ConvParams p) {
+  constexpr int CHUNKS = ROWB / 16;       // 16-byte chunks per LDS row
+  constexpr int EPC = 16 / sizeof(T);     // elements per chunk
+  constexpr int BKE = ROWB / sizeof(T);   // K elements per tile
+  constexpr int ROWS = BC + BP;
+  constexpr int RPI = 1024 / ROWB;        // LDS rows written by one wave-instruction
+  constexpr int NTOT = ROWS / RPI;        // wave-instructions per tile
+  constexpr int NI = (NTOT + 3) / 4;      // per wave
+  constexpr int TC = BC / 32, TP = BP / 32;
+  constexpr int BUF = ROWS * ROWB;
+  static_assert(ROWS % RPI == 0, "tile rows");
+  static_assert(BC % 32 == 0 && BP % 32 == 0, "tile dims");
+
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int p0 = blockIdx.x * BP;
+  const int c0 = blockIdx.y * BC;
+  const int z = blockIdx.z;
+
+  // ---- split-K range ----
+  const int per = (p.kt_total + p.splitk - 1) / p.splitk;
+  const int kb = z * per;
+  const int ke = min(p.kt_total, kb + per);
+  const int nk = ke > kb ? ke - kb : 0;
+
+  // ---- K iterator state: (segment, tap, channel block) ----
+  int seg = 0, tap = 0, cb = 0;
+  {
+    int rem = kb;
+    if (p.nseg > 1 && rem >= p.seg[0].kt) { rem -= p.seg[0].kt; seg = 1; }
+    const int cbl = p.seg[seg].cblk;
+    tap = rem / cbl;
+    cb = rem - tap * cbl;
+  }
+
+  // ---- per-lane staging geometry ----
+  const int lrow = lane / CHUNKS;
+  const int pchunk = lane % CHUNKS;
+  int x_oh[NI], x_ow[NI], x_n[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int g = i * 4 + wave;
+    const int r = g * RPI + lrow;
+    x_n[i] = -1; x_oh[i] = 0; x_ow[i] = 0;
+    if (g < NTOT && r >= BC) {
+      const int pix = p0 + (r - BC);
+      if (pix < p.M) {
+        const int hw = p.OH * p.OW;
+        const int n = pix / hw;
+        const int rem = pix - n * hw;
+        x_n[i] = n;
+        x_oh[i] = rem / p.OW;
+        x_ow[i] = rem - x_oh[i] * p.OW;
+      }
+    }
+  }
+
+  const char* wbase = reinterpret_cast<const char*>(p.w);
+  const char* zero = reinterpret_cast<const char*>(p.zero);
+
+  auto stage = [&](int buf, int ktl, int sg, int tp_, int cb_) {
+    const ConvSeg& S = p.seg[sg];
+    const int th = tp_ / S.KW;
+    const int tw = tp_ - th * S.KW;
+    const char* xb = reinterpret_cast<const char*>(S.x);
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int g = i * 4 + wave;
+      if (g < NTOT) {
+        const int r = g * RPI + lrow;
+        const int lc = pchunk ^ ((r >> 1) & (CHUNKS - 1));
+        const char* src;
+        if (g * RPI < BC) {  // weight row (wave-uniform branch)
+          const long long n = c0 + r;
+          src = wbase + ((n * p.ktot + (long long)ktl * BKE) * sizeof(T)) + lc * 16;
+        } else {
+          const int ih = x_oh[i] * S.stride - S.pad + th;
+          const int iw = x_ow[i] * S.stride - S.pad + tw;
+          const bool ok = x_n[i] >= 0 && (unsigned)ih < (unsigned)S.H && (unsigned)iw < (unsigned)S.W;
+          const long long pixoff = ((long long)x_n[i] * S.H + ih) * S.W + iw;
+          src = ok ? xb + ((pixoff * S.cs + (long long)cb_ * BKE) * sizeof(T)) + lc * 16 : zero + lc * 16;
+        }
+        char* dst = smem + buf * BUF + g * 1024;
+        __builtin_amdgcn_global_load_lds((gptr_t)src, (lds_ptr_t)dst, 16, 0, 0);
+      }
+    }
+  };
+  auto advance = [&]() {
+    if (++cb == p.seg[seg].cblk) {
+      cb = 0;
+      if (++tap == p.seg[seg].KH * p.seg[seg].KW) { tap = 0; ++seg; }
+    }
+  };
+
+  f32x4 acc[TC][TP];
+#pragma unroll
+  for (int a = 0; a < TC; ++a)
+#pragma unroll
+    for (int b = 0; b < TP; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int buf) {
+    const char* base = smem + buf * BUF;
+    if constexpr (sizeof(T) == 2) {
+      constexpr int KSTEPS = BKE / 32;
+#pragma unroll
+      for (int ks = 0; ks < KSTEPS; ++ks) {
+        f16x8 fa[TC], fb[TP];
+        const int c = ks * 4 + (lane >> 4);
+#pragma unroll
+        for (int t = 0; t < TC; ++t) {
+          const int row = wr * (BC / 2) + t * 16 + (lane & 15);
+          fa[t] = *reinterpret_cast<const f16x8*>(base + row * ROWB + ((c ^ ((row >> 1) & (CHUNKS - 1))) << 4));
+        }
+#pragma unroll
+        for (int t = 0; t < TP; ++t) {
+          const int row = BC + wc * (BP / 2) + t * 16 + (lane & 15);
+          fb[t] = *reinterpret_cast<const f16x8*>(base + row * ROWB + ((c ^ ((row >> 1) & (CHUNKS - 1))) << 4));
+        }
+#pragma unroll
+        for (int a = 0; a < TC; ++a)
+#pragma unroll
+          for (int b = 0; b < TP; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[a], fb[b], acc[a][b], 0, 0, 0);
+      }
+    } else {
+      constexpr int KSTEPS = BKE / 4;
+#pragma unroll
+      for (int ks = 0; ks < KSTEPS; ++ks) {
+        float fa[TC], fb[TP];
+        const int woff = (lane >> 4) << 2;
+#pragma unroll
+        for (int t = 0; t < TC; ++t) {
+          const int row = wr * (BC / 2) + t * 16 + (lane & 15);
+          fa[t] = *reinterpret_cast<const float*>(base + row * ROWB + ((ks ^ ((row >> 1) & (CHUNKS - 1))) << 4) + woff);
+        }
+#pragma unroll
+        for (int t = 0; t < TP; ++t) {
+          const int row = BC + wc * (BP / 2) + t * 16 + (lane & 15);
+          fb[t] = *reinterpret_cast<const float*>(base + row * ROWB + ((ks ^ ((row >> 1) & (CHUNKS - 1))) << 4) + woff);
+        }
+#pragma unroll
+        for (int a = 0; a < TC; ++a)
+#pragma unroll
+          for (int b = 0; b < TP; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[a], fb[b], acc[a][b], 0, 0, 0);
+      }
+    }
+  };
+
+  // ---- main loop: 2-deep LDS ring, DMA of tile k+1 under the MFMAs of tile k ----
+  if (nk > 0) {
+    stage(0, kb, seg, tap, cb);
+    advance();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int it = 0; it < nk; ++it) {
+      const int cur = it & 1;
+      if (it + 1 < nk) {
+        stage(cur ^ 1, kb + it + 1, seg, tap, cb);
+        advance();
+      }
+      compute(cur);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue ----
+  const int chq = (lane >> 4) * 4;
+#pragma unroll
+  for (int b = 0; b < TP; ++b) {
+    const int pix = p0 + wc * (BP / 2) + b * 16 + (lane & 15);
+    if (pix >= p.M) continue;
+    if (p.splitk > 1) {
+#pragma unroll
+      for (int a = 0; a < TC; ++a) {
+        const int ch = c0 + wr * (BC / 2) + a * 16 + chq;
+        float* dst = p.partial + ((long long)z * p.M + pix) * p.npad + ch;
+        *reinterpret_cast<f32x4*>(dst) = acc[a][b];
+      }
+      continue;
+    }
+    int n = 0, oh = 0, ow = 0;
+    if (p.bias_mode == BIAS_BORDER9 || p.res_mode == RES_UP2) {
+      const int hw = p.OH * p.OW;
+      n = pix / hw;
+      const int rem = pix - n * hw;
+      oh = rem / p.OW;
+      ow = rem - oh * p.OW;
+    }
+    int bofs = 0;
+    if (p.bias_mode == BIAS_BORDER9) {
+      // class of this output pixel w.r.t. which taps of the (single) 3x3 segment fall
+      // into the zero padding of the folded pre-BN input
+      const ConvSeg& S = p.seg[0];
+      const int ih0 = oh * S.stride - S.pad, iw0 = ow * S.stride - S.pad;
+      const int rc = ih0 < 0 ? 0 : (ih0 + S.KH - 1 >= S.H ? 2 : 1);
+      const int cc = iw0 < 0 ? 0 : (iw0 + S.KW - 1 >= S.W ? 2 : 1);
+      bofs = (rc * 3 + cc) * p.npad;
+    }
+    long long rpix = pix;
+    if (p.res_mode == RES_UP2) rpix = ((long long)n * p.rH + (oh >> 1)) * p.rW + (ow >> 1);
+#pragma unroll
+    for (int a = 0; a < TC; ++a) {
+      const int ch = c0 + wr * (BC / 2) + a * 16 + chq;
+      if (ch >= p.cwrite) continue;
+      const int nv = min(4, p.cwrite - ch);
+      float v[4] = {acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]};
+      if (p.bias_mode != BIAS_NONE) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] += p.bias[bofs + ch + j];
+      }
+      float sl[4] = {0.f, 0.f, 0.f, 0.f};
+      if (p.act == ACT_PRELU) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sl[j] = p.slope[ch + j];
+      }
+      if (!p.act_after_res) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = act_apply(v[j], p.act, sl[j]);
+      }
+      if (p.res_mode != RES_NONE) {
+        float r[4] = {0.f, 0.f, 0.f, 0.f};
+        load4<T>(reinterpret_cast<const T*>(p.res) + rpix * p.rcs + ch, r, nv);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] += r[j];
+      }
+      if (p.act_after_res) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = act_apply(v[j], p.act, sl[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (ch + j >= p.cout) v[j] = 0.f;  // keep channel padding exactly zero
+      if (p.out_f32)
+        store4<float>(reinterpret_cast<float*>(p.y) + (long long)pix * p.ycs + ch, v, nv);
+      else
+        store4<T>(reinterpret_cast<T*>(p.y) + (long long)pix * p.ycs + ch, v, nv);
+    }
+  }
+}
+
+// Sum split-K partials, then the same bias/activation epilogue (no residual).
+template <typename T>
+__global__ void splitk_reduce(const float* __restrict__ part, int splitk, int M, int npad, int cout,
+                              const float* __restrict__ bias, const float* __restrict__ slope, int act,
+                              void* y, int ycs, int out_f32) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long total = (long long)M * cout;
+  if (i >= total) return;
+  const int pix = (int)(i / cout);
+  const int ch = (int)(i - (long long)pix * cout);
+  float s = 0.f;
+  for (int z = 0; z < splitk; ++z) s += part[((long long)z * M + pix) * npad + ch];
+  if (bias) s += bias[ch];
+  s = act_apply(s, act, slope ? slope[ch] : 0.f);
+  if (out_f32) reinterpret_cast<float*>(y)[(long long)pix * ycs + ch] = s;
+  else reinterpret_cast<T*>(y)[(long long)pix * ycs + ch] = (T)s;
+}
+
+// Direct 3x3 conv for stems: input NHWC with exactly 4 (padded) channels, one
+// thread per output pixel, the whole [cout][3][3][4] filter bank in LDS. The
+// 36-value input patch stays in registers (compile-time indexed).
+template <typename T>
+__global__ __launch_bounds__(256) void stem_conv3x3(StemParams p) {
+  __shared__ __attribute__((aligned(16))) float sw[64 * 36];
+  for (int i = threadIdx.x; i < p.cout * 36; i += blockDim.x) sw[i] = p.w[i];
+  __syncthreads();
+  const long long pix = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long M = (long long)p.N * p.OH * p.OW;
+  if (pix >= M) return;
+  const int hw = p.OH * p.OW;
+  const int n = (int)(pix / hw);
+  const int rem = (int)(pix - (long long)n * hw);
+  const int oh = rem / p.OW, ow = rem - (rem / p.OW) * p.OW;
+  float in[36];
+  const T* xb = reinterpret_cast<const T*>(p.x);
+#pragma unroll
+  for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      const int ih = oh * p.stride - p.pad + kh, iw = ow * p.stride - p.pad + kw;
+      const bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+      if (ok) load4<T>(xb + (((long long)n * p.H + ih) * p.W + iw) * p.xcs, v, 4);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) in[(kh * 3 + kw) * 4 + c] = v[c];
+    }
+  T* y = reinterpret_cast<T*>(p.y) + pix * p.ycs;
+  for (int co0 = 0; co0 < p.cpad; co0 += 4) {
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int co = co0 + j;
+      float s = 0.f;
+      if (co < p.cout) {
+        const float* wrow = sw + co * 36;
+#pragma unroll
+        for (int k = 0; k < 36; ++k) s = fmaf(in[k], wrow[k], s);
+        s += p.bias[co];
+        s = act_apply(s, p.act, p.slope ? p.slope[co] : 0.f);
+      }
+      v[j] = s;
+    }
+    store4<T>(y + co0, v, 4);
+  }
+}
+
+// NHWC max pool (padding = -inf, PyTorch semantics); one thread per pixel x 4 channels.
+template <typename T>
+__global__ void maxpool_nhwc(PoolParams p) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int cg = p.C / 4;
+  const long long total = (long long)p.N * p.OH * p.OW * cg;
+  if (i >= total) return;
+  const int g = (int)(i % cg);
+  const long long pix = i / cg;
+  const int hw = p.OH * p.OW;
+  const int n = (int)(pix / hw);
+  const int rem = (int)(pix - (long long)n * hw);
+  const int oh = rem / p.OW, ow = rem - (rem / p.OW) * p.OW;
+  float m[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  const T* xb = reinterpret_cast<const T*>(p.x);
+  for (int kh = 0; kh < p.k; ++kh)
+    for (int kw = 0; kw < p.k; ++kw) {
+      const int ih = oh * p.stride - p.pad + kh, iw = ow * p.stride - p.pad + kw;
+      if ((unsigned)ih >= (unsigned)p.H || (unsigned)iw >= (unsigned)p.W) continue;
+      float v[4];
+      load4<T>(xb + (((long long)n * p.H + ih) * p.W + iw) * p.xcs + g * 4, v, 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) m[j] = fmaxf(m[j], v[j]);
+    }
+  store4<T>(reinterpret_cast<T*>(p.y) + pix * p.ycs + g * 4, m, 4);
+}
+
+// ---------------------------------------------------------------------------
+// host-side launchers
+// ---------------------------------------------------------------------------
+template <typename T, int BC, int BP, int ROWB>
+static hipError_t launch_cfg(const ConvParams& p, hipStream_t s) {
+  dim3 grid((p.M + BP - 1) / BP, p.npad / BC, p.splitk);
+  hipLaunchKernelGGL((conv_igemm<T, BC, BP, ROWB>), grid, dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+template <typename T, int ROWB>
+static hipError_t launch_rowb(const ConvParams& p, int bc, int bp, hipStream_t s) {
+  if (bc == 128 && bp == 128) return launch_cfg<T, 128, 128, ROWB>(p, s);
+  if (bc == 128 && bp == 64) return launch_cfg<T, 128, 64, ROWB>(p, s);
+  if (bc == 64 && bp == 256) return launch_cfg<T, 64, 256, ROWB>(p, s);
+  if (bc == 64 && bp == 128) return launch_cfg<T, 64, 128, ROWB>(p, s);
+  if (bc == 96 && bp == 128) return launch_cfg<T, 96, 128, ROWB>(p, s);
+  if (bc == 32 && bp == 256) return launch_cfg<T, 32, 256, ROWB>(p, s);
+  if (bc == 32 && bp == 128) return launch_cfg<T, 32, 128, ROWB>(p, s);
+  return hipErrorInvalidValue;
+}
+
+hipError_t conv_launch(int f32, int rowb, int bc, int bp, const ConvParams& p, hipStream_t s) {
+  if (f32) return rowb == 128 ? launch_rowb<float, 128>(p, bc, bp, s) : launch_rowb<float, 64>(p, bc, bp, s);
+  return rowb == 128 ? launch_rowb<f16, 128>(p, bc, bp, s) : launch_rowb<f16, 64>(p, bc, bp, s);
+}
+
+hipError_t splitk_reduce_launch(int f32, const float* part, int splitk, int M, int npad, int cout,
+                                const float* bias, const float* slope, int act, void* y, int ycs,
+                                int out_f32, hipStream_t s) {
+  const long long total = (long long)M * cout;
+  dim3 grid((unsigned)((total + 255) / 256));
+  if (f32)
+    hipLaunchKernelGGL(splitk_reduce<float>, grid, dim3(256), 0, s, part, splitk, M, npad, cout, bias, slope, act, y, ycs, out_f32);
+  else
+    hipLaunchKernelGGL(splitk_reduce<f16>, grid, dim3(256), 0, s, part, splitk, M, npad, cout, bias, slope, act, y, ycs, out_f32);
+  return hipGetLastError();
+}
+
+hipError_t stem_launch(int f32, const StemParams& p, hipStream_t s) {
+  const long long M = (long long)p.N * p.OH * p.OW;
+  dim3 grid((unsigned)((M + 255) / 256));
+  if (p.KH != 3 || p.KW != 3 || p.cin != 4 || p.cout > 64 || p.cpad % 4) return hipErrorInvalidValue;
+  if (f32) hipLaunchKernelGGL(stem_conv3x3<float>, grid, dim3(256), 0, s, p);
+  else hipLaunchKernelGGL(stem_conv3x3<f16>, grid, dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t maxpool_launch(int f32, const PoolParams& p, hipStream_t s) {
+  const long long total = (long long)p.N * p.OH * p.OW * (p.C / 4);
+  dim3 grid((unsigned)((total + 255) / 256));
+  if (f32) hipLaunchKernelGGL(maxpool_nhwc<float>, grid, dim3(256), 0, s, p);
+  else hipLaunchKernelGGL(maxpool_nhwc<f16>, grid, dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+}  // namespace pc

@@ -1,0 +1,357 @@
+// Byte-exact image kernels of the identity hot path (gfx950).
+//
+// These restate, on device, the u8 image operations the reference performs on
+// the CPU through OpenCV 4.9 (opencv-python-headless==4.9.0.80, not vendored):
+//   * SCRFD letterbox + blob      [ext] insightface SCRFD.detect / cv2.resize INTER_LINEAR
+//                                 / cv2.dnn.blobFromImage(1/128, 127.5, swapRB)
+//   * 5-point similarity warp     face_embedder.py:1465-1473 (cv2.warpAffine INTER_LINEAR,
+//                                 BORDER_REFLECT on the face-box crop)
+//   * face quality                face_embedder.py:1274-1276 (BGR2GRAY + Laplacian(CV_64F).var())
+//   * ArcFace preprocessing       face_embedder.py:1281-1298 (BGR->RGB, x/127.5-1, h-flip TTA)
+//   * INTER_AREA downscale        gui_app.py:1505-1507 (pre-scan 4K -> 416 wide)
+// The fixed-point arithmetic follows OpenCV's published algorithm (11-bit
+// resize coefficients, 1/32-pixel warp tables with 15-bit weights, 14-bit gray
+// coefficients); oracle/cv_ops.c restates the same arithmetic on the CPU and the
+// parity tests require bit-exact agreement. Parity against OpenCV itself is
+// unpinned (OpenCV is not installed anywhere in this pipeline).
+//
+// All of these are HBM/gather-bound: one thread per output pixel, no MFMA.
+#include "pc_common.h"
+
+#pragma clang fp contract(off)
+
+namespace pc {
+
+// ---------------------------------------------------------------------------
+// SCRFD letterbox: resize (INTER_LINEAR, OpenCV u8 fixed point) into the top-left
+// of a zero DxD canvas, then blob (x - 127.5) / 128 with BGR->RGB, NHWC, 4 channels.
+// ---------------------------------------------------------------------------
+struct LetterboxDesc {
+  const uint8_t* src;
+  int H, W, row_stride;     // source frame (BGR u8), bytes per row
+  int new_w, new_h;         // resized size
+  double scale_x, scale_y;  // 1 / (new/old), as cv::resize computes them
+  int simd_end;             // byte index where OpenCV's SIMD vertical pass ends (row width*3 based)
+  int pad_;
+};
+
+__device__ __forceinline__ void lin_coef(int d, double scale, int src_len, int& s0, short& a0, short& a1) {
+  float f = (float)((d + 0.5) * scale - 0.5);
+  int s = (int)floorf(f);
+  f -= (float)s;
+  if (s < 0) { f = 0.f; s = 0; }
+  if (s >= src_len - 1) { f = 0.f; s = src_len - 1; }
+  s0 = s;
+  a0 = (short)__float2int_rn((1.f - f) * 2048.f);
+  a1 = (short)__float2int_rn(f * 2048.f);
+}
+
+template <typename T>
+__global__ void letterbox_blob(const LetterboxDesc* __restrict__ descs, int D, T* __restrict__ out) {
+  const int n = blockIdx.y;
+  const int pix = blockIdx.x * blockDim.x + threadIdx.x;
+  if (pix >= D * D) return;
+  const LetterboxDesc d = descs[n];
+  const int y = pix / D, x = pix - (pix / D) * D;
+  float v[3] = {0.f, 0.f, 0.f};  // BGR u8 values
+  if (x < d.new_w && y < d.new_h) {
+    int sx, sy;
+    short a0, a1, b0, b1;
+    lin_coef(x, d.scale_x, d.W, sx, a0, a1);
+    lin_coef(y, d.scale_y, d.H, sy, b0, b1);
+    const int sx1 = sx + 1 < d.W ? sx + 1 : sx;   // weight a1 is 0 whenever clamped
+    const int sy1 = sy + 1 < d.H ? sy + 1 : sy;
+    const uint8_t* r0 = d.src + (long long)sy * d.row_stride;
+    const uint8_t* r1 = d.src + (long long)sy1 * d.row_stride;
+    const bool simd = x * 3 < d.simd_end;  // which rounding OpenCV's vertical pass used for these bytes
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const int S0 = r0[sx * 3 + c] * a0 + r0[sx1 * 3 + c] * a1;
+      const int S1 = r1[sx * 3 + c] * a0 + r1[sx1 * 3 + c] * a1;
+      int val;
+      if (simd) {
+        const int t0 = ((S0 >> 4) * (int)b0) >> 16;
+        const int t1 = ((S1 >> 4) * (int)b1) >> 16;
+        val = (t0 + t1 + 2) >> 2;
+      } else {
+        val = (S0 * (int)b0 + S1 * (int)b1 + (1 << 21)) >> 22;
+      }
+      val = val < 0 ? 0 : (val > 255 ? 255 : val);
+      v[c] = (float)val;
+    }
+  }
+  // blobFromImage: (x - mean) * scalefactor, swapRB -> channel order R,G,B
+  T* o = out + ((long long)n * D * D + pix) * 4;
+  const float r = (v[2] - 127.5f) * 0.0078125f;
+  const float g = (v[1] - 127.5f) * 0.0078125f;
+  const float b = (v[0] - 127.5f) * 0.0078125f;
+  if constexpr (sizeof(T) == 2) {
+    f16x4 h = {(f16)r, (f16)g, (f16)b, (f16)0.f};
+    *reinterpret_cast<f16x4*>(o) = h;
+  } else {
+    *reinterpret_cast<f32x4*>(o) = f32x4{r, g, b, 0.f};
+  }
+}
+
+// ---------------------------------------------------------------------------
+// warpAffine INTER_LINEAR on a crop, u8 BGR, BORDER_REFLECT or BORDER_REFLECT_101.
+// M is the dst->src map (already inverted on the host exactly as cv::warpAffine does).
+// ---------------------------------------------------------------------------
+struct WarpDesc {
+  const uint8_t* src;   // top-left of the crop inside the frame
+  int row_stride;       // frame bytes per row
+  int w, h;             // crop size
+  double M[6];          // dst -> src
+  uint8_t* dst;         // out_h x out_w x 3, contiguous
+  int out_w, out_h;
+  int border;           // 2 = BORDER_REFLECT, 4 = BORDER_REFLECT_101
+  int pad_;
+};
+
+__device__ __forceinline__ int border_interp(int p, int len, int border) {
+  if ((unsigned)p < (unsigned)len) return p;
+  if (len == 1) return 0;
+  const int delta = border == 4 ? 1 : 0;
+  do {
+    if (p < 0) p = -p - 1 + delta;
+    else p = len - 1 - (p - len) - delta;
+  } while ((unsigned)p >= (unsigned)len);
+  return p;
+}
+
+__device__ __forceinline__ void bilinear_wtab(int fx, int fy, int w[4]) {
+  // OpenCV initInterTab2D(INTER_LINEAR, fixpt): float products of the 1-D
+  // linear taps, rounded to Q15, then the largest/smallest entry absorbs the
+  // rounding residue so the four weights sum to exactly 32768.
+  const float scale = 1.f / 32.f;
+  const float xs = fx * scale, ys = fy * scale;
+  const float tx[2] = {1.f - xs, xs};
+  const float ty[2] = {1.f - ys, ys};
+  int isum = 0;
+#pragma unroll
+  for (int k1 = 0; k1 < 2; ++k1)
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2) {
+      const float v = ty[k1] * tx[k2];
+      w[k1 * 2 + k2] = __float2int_rn(v * 32768.f);
+      isum += w[k1 * 2 + k2];
+    }
+  if (isum != 32768) {
+    const int diff = isum - 32768;
+    int mk = 0, Mk = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (w[k] < w[mk]) mk = k;
+      else if (w[k] > w[Mk]) Mk = k;
+    }
+    if (diff < 0) w[Mk] -= diff;
+    else w[mk] -= diff;
+  }
+}
+
+__global__ void warp_affine_u8(const WarpDesc* __restrict__ descs) {
+  const WarpDesc d = descs[blockIdx.y];
+  const int pix = blockIdx.x * blockDim.x + threadIdx.x;
+  if (pix >= d.out_w * d.out_h) return;
+  const int y = pix / d.out_w, x = pix - (pix / d.out_w) * d.out_w;
+  const int AB_BITS = 10, AB_SCALE = 1 << AB_BITS, INTER_BITS = 5;
+  const int round_delta = AB_SCALE / 32 / 2;
+  const int adelta = __double2int_rn(d.M[0] * x * AB_SCALE);
+  const int bdelta = __double2int_rn(d.M[3] * x * AB_SCALE);
+  const int X0 = __double2int_rn((d.M[1] * y + d.M[2]) * AB_SCALE) + round_delta;
+  const int Y0 = __double2int_rn((d.M[4] * y + d.M[5]) * AB_SCALE) + round_delta;
+  const int X = (X0 + adelta) >> (AB_BITS - INTER_BITS);
+  const int Y = (Y0 + bdelta) >> (AB_BITS - INTER_BITS);
+  int sx = X >> INTER_BITS, sy = Y >> INTER_BITS;
+  sx = sx < -32768 ? -32768 : (sx > 32767 ? 32767 : sx);
+  sy = sy < -32768 ? -32768 : (sy > 32767 ? 32767 : sy);
+  int wt[4];
+  bilinear_wtab(X & 31, Y & 31, wt);
+  const int x0 = border_interp(sx, d.w, d.border), x1 = border_interp(sx + 1, d.w, d.border);
+  const int y0 = border_interp(sy, d.h, d.border), y1 = border_interp(sy + 1, d.h, d.border);
+  const uint8_t* r0 = d.src + (long long)y0 * d.row_stride;
+  const uint8_t* r1 = d.src + (long long)y1 * d.row_stride;
+  uint8_t* o = d.dst + (long long)pix * 3;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    int v = r0[x0 * 3 + c] * wt[0] + r0[x1 * 3 + c] * wt[1] + r1[x0 * 3 + c] * wt[2] + r1[x1 * 3 + c] * wt[3];
+    v = (v + (1 << 14)) >> 15;
+    o[c] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// quality = var(Laplacian(BGR2GRAY(chip), CV_64F)), ksize=1, BORDER_REFLECT_101.
+// The Laplacian values are small integers, so sum and sum of squares are exact in
+// int64; var = (S2 - S1^2/N)/N in f64 (numpy's two-pass var agrees to ~1e-15).
+// One 256-thread workgroup per chip.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void face_quality(const uint8_t* __restrict__ chips, int side, double* __restrict__ out) {
+  __shared__ uint8_t g[128 * 128];
+  __shared__ long long red[2][4];
+  const uint8_t* c = chips + (long long)blockIdx.x * side * side * 3;
+  const int n = side * side;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int b = c[i * 3 + 0], gg = c[i * 3 + 1], r = c[i * 3 + 2];
+    g[i] = (uint8_t)((b * 1868 + gg * 9617 + r * 4899 + (1 << 13)) >> 14);
+  }
+  __syncthreads();
+  long long s1 = 0, s2 = 0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int y = i / side, x = i - (i / side) * side;
+    const int xm = border_interp(x - 1, side, 4), xp = border_interp(x + 1, side, 4);
+    const int ym = border_interp(y - 1, side, 4), yp = border_interp(y + 1, side, 4);
+    const int l = (int)g[y * side + xm] + (int)g[y * side + xp] + (int)g[ym * side + x] + (int)g[yp * side + x] - 4 * (int)g[i];
+    s1 += l;
+    s2 += (long long)l * l;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    s1 += __shfl_xor(s1, o);
+    s2 += __shfl_xor(s2, o);
+  }
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { red[0][wv] = s1; red[1][wv] = s2; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    long long t1 = 0, t2 = 0;
+    for (int k = 0; k < 4; ++k) { t1 += red[0][k]; t2 += red[1][k]; }
+    const double N = (double)n;
+    const double mean = (double)t1 / N;
+    // sum (l - mean)^2 = S2 - 2*mean*S1 + N*mean^2 = S2 - S1*mean (exact algebra)
+    out[blockIdx.x] = ((double)t2 - (double)t1 * mean) / N;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// ArcFace input: BGR u8 chip -> RGB, x/127.5 - 1 (f32 division as numpy does),
+// NHWC with 4 channels; optionally the horizontally flipped copy at n + N.
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ void arcface_prep(const uint8_t* __restrict__ chips, int N, int side, int flip, T* __restrict__ out) {
+  const int n = blockIdx.y;
+  const int pix = blockIdx.x * blockDim.x + threadIdx.x;
+  if (pix >= side * side) return;
+  const int y = pix / side, x = pix - (pix / side) * side;
+  const uint8_t* s = chips + ((long long)n * side * side + pix) * 3;
+  const float r = (float)s[2] / 127.5f - 1.0f;
+  const float g = (float)s[1] / 127.5f - 1.0f;
+  const float b = (float)s[0] / 127.5f - 1.0f;
+  T* o = out + ((long long)n * side * side + pix) * 4;
+  T* of = out + ((long long)(n + N) * side * side + y * side + (side - 1 - x)) * 4;
+  if constexpr (sizeof(T) == 2) {
+    f16x4 h = {(f16)r, (f16)g, (f16)b, (f16)0.f};
+    *reinterpret_cast<f16x4*>(o) = h;
+    if (flip) *reinterpret_cast<f16x4*>(of) = h;
+  } else {
+    const f32x4 h{r, g, b, 0.f};
+    *reinterpret_cast<f32x4*>(o) = h;
+    if (flip) *reinterpret_cast<f32x4*>(of) = h;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Rotation by 90/180/270 (cv2.rotate semantics) and replicate padding
+// (cv2.copyMakeBorder BORDER_REPLICATE) for SCRFD fallback passes
+// (face_embedder.py:2165-2169, 2292-2294, 2394).
+// ---------------------------------------------------------------------------
+__global__ void rotate_pad_u8(const uint8_t* __restrict__ src, int H, int W, int row_stride, int deg, int pad,
+                              uint8_t* __restrict__ dst, int OH, int OW) {
+  const long long pix = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (pix >= (long long)OH * OW) return;
+  const int y = (int)(pix / OW), x = (int)(pix - (pix / OW) * OW);
+  // coordinates in the rotated (unpadded) image, replicate-clamped
+  const int RH = (deg == 90 || deg == 270) ? W : H;
+  const int RW = (deg == 90 || deg == 270) ? H : W;
+  int ry = y - pad, rx = x - pad;
+  ry = ry < 0 ? 0 : (ry >= RH ? RH - 1 : ry);
+  rx = rx < 0 ? 0 : (rx >= RW ? RW - 1 : rx);
+  int sy, sx;
+  if (deg == 90) { sy = H - 1 - rx; sx = ry; }          // ROTATE_90_CLOCKWISE
+  else if (deg == 180) { sy = H - 1 - ry; sx = W - 1 - rx; }
+  else if (deg == 270) { sy = rx; sx = W - 1 - ry; }    // ROTATE_90_COUNTERCLOCKWISE
+  else { sy = ry; sx = rx; }
+  const uint8_t* s = src + (long long)sy * row_stride + sx * 3;
+  uint8_t* o = dst + pix * 3;
+  o[0] = s[0]; o[1] = s[1]; o[2] = s[2];
+}
+
+// ---------------------------------------------------------------------------
+// cv2.resize INTER_AREA for downscales (u8, 3 channels), OpenCV's generic
+// (non-integer scale) area path: float weights, accumulated per output pixel in
+// source order, saturate_cast<uchar> (round half to even) at the end.
+// Coefficient tables (xofs: src index, dst index, weight) are built on the host
+// exactly as cv::computeResizeAreaTab does and passed in.
+// ---------------------------------------------------------------------------
+struct AreaTab { int si; int di; float alpha; };
+
+__global__ void resize_area_u8(const uint8_t* __restrict__ src, int row_stride,
+                               const AreaTab* __restrict__ xtab, const int* __restrict__ xtab_start,
+                               const AreaTab* __restrict__ ytab, const int* __restrict__ ytab_start,
+                               uint8_t* __restrict__ dst, int OH, int OW) {
+  const int pix = blockIdx.x * blockDim.x + threadIdx.x;
+  if (pix >= OH * OW) return;
+  const int dy = pix / OW, dx = pix - (pix / OW) * OW;
+  float acc[3] = {0.f, 0.f, 0.f};
+  for (int j = ytab_start[dy]; j < ytab_start[dy + 1]; ++j) {
+    const AreaTab ty = ytab[j];
+    const uint8_t* row = src + (long long)ty.si * row_stride;
+    float rs[3] = {0.f, 0.f, 0.f};
+    for (int i = xtab_start[dx]; i < xtab_start[dx + 1]; ++i) {
+      const AreaTab tx = xtab[i];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) rs[c] += (float)row[tx.si * 3 + c] * tx.alpha;
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) acc[c] += rs[c] * ty.alpha;
+  }
+  uint8_t* o = dst + (long long)pix * 3;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    int v = __float2int_rn(acc[c]);
+    o[c] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+  }
+}
+
+// ---------------------------------------------------------------------------
+hipError_t letterbox_launch(int f32, const LetterboxDesc* d_descs, int N, int D, void* out, hipStream_t s) {
+  dim3 grid((D * D + 255) / 256, N);
+  if (f32) hipLaunchKernelGGL(letterbox_blob<float>, grid, dim3(256), 0, s, d_descs, D, (float*)out);
+  else hipLaunchKernelGGL(letterbox_blob<f16>, grid, dim3(256), 0, s, d_descs, D, (f16*)out);
+  return hipGetLastError();
+}
+
+hipError_t warp_launch(const WarpDesc* d_descs, int N, int max_pixels, hipStream_t s) {
+  dim3 grid((max_pixels + 255) / 256, N);
+  hipLaunchKernelGGL(warp_affine_u8, grid, dim3(256), 0, s, d_descs);
+  return hipGetLastError();
+}
+
+hipError_t quality_launch(const uint8_t* chips, int N, int side, double* out, hipStream_t s) {
+  if (side > 128) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(face_quality, dim3(N), dim3(256), 0, s, chips, side, out);
+  return hipGetLastError();
+}
+
+hipError_t arcprep_launch(int f32, const uint8_t* chips, int N, int side, int flip, void* out, hipStream_t s) {
+  dim3 grid((side * side + 255) / 256, N);
+  if (f32) hipLaunchKernelGGL(arcface_prep<float>, grid, dim3(256), 0, s, chips, N, side, flip, (float*)out);
+  else hipLaunchKernelGGL(arcface_prep<f16>, grid, dim3(256), 0, s, chips, N, side, flip, (f16*)out);
+  return hipGetLastError();
+}
+
+hipError_t rotate_pad_launch(const uint8_t* src, int H, int W, int row_stride, int deg, int pad, uint8_t* dst,
+                             int OH, int OW, hipStream_t s) {
+  const long long n = (long long)OH * OW;
+  hipLaunchKernelGGL(rotate_pad_u8, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, H, W, row_stride, deg,
+                     pad, dst, OH, OW);
+  return hipGetLastError();
+}
+
+hipError_t resize_area_launch(const uint8_t* src, int row_stride, const AreaTab* xtab, const int* xstart,
+                              const AreaTab* ytab, const int* ystart, uint8_t* dst, int OH, int OW, hipStream_t s) {
+  hipLaunchKernelGGL(resize_area_u8, dim3((OH * OW + 255) / 256), dim3(256), 0, s, src, row_stride, xtab, xstart, ytab,
+                     ystart, dst, OH, OW);
+  return hipGetLastError();
+}
+
+}  // namespace pc

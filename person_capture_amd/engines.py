@@ -1,0 +1,187 @@
+"""Device engines behind the facades: ArcFace embedder, SCRFD detector and the
+bank matcher, each a thin orchestration of C-ABI calls on one GpuContext."""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import models
+from ._lib import PC_PREC_F16, PC_PREC_F32, LetterboxDesc, check
+from .runtime import DeviceBuffer, GpuContext, Net
+
+
+class ArcFaceEngine:
+    """IResNet embedder: u8 BGR chips (device) -> unit f32 embeddings, flip-TTA fused
+    (FaceEmbedder._arcface_encode, face_embedder.py:1290-1389)."""
+
+    def __init__(self, ctx: GpuContext, params: models.Params, depth: int = 100, precision: int = PC_PREC_F16,
+                 max_batch: int = 256, graph: bool = False):
+        self.ctx = ctx
+        self.depth = depth
+        self.precision = precision
+        self.program = models.compile_iresnet(params, depth)
+        self.net = Net(ctx, self.program.serialize(), precision=precision, max_batch=max_batch)
+        self.dim = params["fc.weight"].shape[0]
+        self.max_batch = max_batch
+        if graph:
+            self.net.set_graph(True)
+
+    @property
+    def flops_per_forward(self) -> float:
+        return self.net.flops_per_image
+
+    def embed_device(self, d_chips: int, n: int, flip: bool, d_out: int) -> None:
+        """Enqueue: chips [n][112][112][3] u8 at d_chips -> d_out [n][dim] f32."""
+        rows = 2 * n if flip else n
+        if rows > self.max_batch:
+            raise ValueError(f"ArcFace batch {rows} exceeds max_batch {self.max_batch}")
+        check(self.ctx.lib.pc_arcface_embed(self.net.handle, C.c_void_p(int(d_chips)), int(n), 1 if flip else 0,
+                                            C.c_void_p(int(d_out))), self.ctx.handle, "arcface_embed")
+
+    def embed(self, chips_bgr: np.ndarray, flip: bool = True) -> np.ndarray:
+        """Host convenience: chips [n][112][112][3] u8 -> [n][dim] unit f32 (chunks by max_batch)."""
+        chips = np.ascontiguousarray(chips_bgr, dtype=np.uint8)
+        n = chips.shape[0]
+        if n == 0:
+            return np.zeros((0, self.dim), np.float32)
+        per = self.max_batch // 2 if flip else self.max_batch
+        outs = []
+        for s in range(0, n, per):
+            part = chips[s:s + per]
+            m = part.shape[0]
+            d_in = self.ctx.scratch("arc_chips", part.nbytes)
+            self.ctx.upload(part, d_in)
+            d_out = self.ctx.scratch("arc_feat", m * self.dim * 4)
+            self.embed_device(d_in.ptr, m, flip, d_out.ptr)
+            outs.append(self.ctx.download(d_out.ptr, (m, self.dim), np.float32))
+        return np.concatenate(outs, axis=0)
+
+
+class BankMatcher:
+    """Batched Processor._fd_min (gui_app.py:660-674) on device."""
+
+    def __init__(self, ctx: GpuContext):
+        self.ctx = ctx
+
+    def match_device(self, d_q: int, n: int, d_bank: int, b: int, dim: int, d_fd: int, d_idx: int) -> None:
+        check(self.ctx.lib.pc_bank_match(self.ctx.handle, C.c_void_p(int(d_q)), int(n), C.c_void_p(int(d_bank)),
+                                         int(b), int(dim), C.c_void_p(int(d_fd)), C.c_void_p(int(d_idx))),
+              self.ctx.handle, "bank_match")
+
+    def match(self, q: np.ndarray, bank: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+        q = np.ascontiguousarray(q, dtype=np.float32)
+        bank = np.ascontiguousarray(bank, dtype=np.float32).reshape(-1, q.shape[1]) if bank is not None and \
+            np.asarray(bank).size else np.zeros((0, q.shape[1]), np.float32)
+        n, dim = q.shape
+        if n == 0:
+            return np.zeros((0,), np.float32), np.zeros((0,), np.int32)
+        dq = self.ctx.scratch("bm_q", q.nbytes)
+        self.ctx.upload(q, dq)
+        db = self.ctx.scratch("bm_bank", max(bank.nbytes, 4))
+        if bank.size:
+            self.ctx.upload(bank, db)
+        dfd = self.ctx.scratch("bm_fd", n * 4)
+        didx = self.ctx.scratch("bm_idx", n * 4)
+        self.match_device(dq.ptr, n, db.ptr, bank.shape[0], dim, dfd.ptr, didx.ptr)
+        fd = self.ctx.download(dfd.ptr, (n,), np.float32)
+        idx = self.ctx.download(didx.ptr, (n,), np.int32)
+        return fd, idx
+
+
+def letterbox_geometry(H: int, W: int, D: int) -> Tuple[int, int, float]:
+    """[ext] insightface SCRFD.detect sizing: keep aspect, fit into DxD."""
+    im_ratio = float(H) / W
+    model_ratio = 1.0
+    if im_ratio > model_ratio:
+        new_h = D
+        new_w = int(new_h / im_ratio)
+    else:
+        new_w = D
+        new_h = int(new_w * im_ratio)
+    det_scale = float(new_h) / H
+    return new_w, new_h, det_scale
+
+
+def opencv_vresize_simd_end(width_bytes: int) -> int:
+    """Byte index where OpenCV's 128-bit VResizeLinearVec_32s8u stops for a u8 row of
+    width_bytes (16-byte loop, then 8-byte loop while x < width - 8); the remainder
+    uses the scalar FixedPtCast path with different rounding."""
+    x = (width_bytes // 16) * 16 if width_bytes >= 16 else 0
+    while x < width_bytes - 8:
+        x += 8
+    return x
+
+
+def make_letterbox_desc(d_src: int, H: int, W: int, row_stride: int, D: int) -> Tuple[LetterboxDesc, float]:
+    new_w, new_h, det_scale = letterbox_geometry(H, W, D)
+    d = LetterboxDesc()
+    d.d_src = int(d_src)
+    d.H, d.W, d.row_stride = H, W, row_stride
+    d.new_w, d.new_h = new_w, new_h
+    d.scale_x = 1.0 / (float(new_w) / W)
+    d.scale_y = 1.0 / (float(new_h) / H)
+    d.simd_end = opencv_vresize_simd_end(new_w * 3)
+    return d, det_scale
+
+
+class ScrfdEngine:
+    """SCRFD detector at one square input size D (letterbox + net + decode + NMS on device)."""
+
+    def __init__(self, ctx: GpuContext, params: models.Params, variant: str = "10g", D: int = 640,
+                 precision: int = PC_PREC_F16, max_batch: int = 64, max_det: int = 256):
+        self.ctx = ctx
+        self.D = D
+        self.variant = variant
+        self.precision = precision
+        self.program = models.compile_scrfd(params, variant, D)
+        self.net = Net(ctx, self.program.serialize(), precision=precision, max_batch=max_batch)
+        self.max_batch = max_batch
+        self.max_det = max_det
+
+    @property
+    def flops_per_image(self) -> float:
+        return self.net.flops_per_image
+
+    def detect_device(self, descs: Sequence[LetterboxDesc], det_scales: Sequence[float], thresh: float,
+                      nms_thresh: float = 0.4) -> Tuple[DeviceBuffer, DeviceBuffer, DeviceBuffer, DeviceBuffer]:
+        n = len(descs)
+        arr = (LetterboxDesc * n)(*descs)
+        sc = (C.c_float * n)(*[float(s) for s in det_scales])
+        dd = self.ctx.scratch(f"scrfd_dets{self.D}", n * self.max_det * 5 * 4)
+        dk = self.ctx.scratch(f"scrfd_kps{self.D}", n * self.max_det * 10 * 4)
+        dc = self.ctx.scratch(f"scrfd_cnt{self.D}", n * 4)
+        dn = self.ctx.scratch(f"scrfd_ncand{self.D}", n * 4)
+        check(self.ctx.lib.pc_scrfd_detect(self.net.handle, arr, n, self.D, C.c_float(thresh), C.c_float(nms_thresh),
+                                           sc, self.max_det, C.c_void_p(dd.ptr), C.c_void_p(dk.ptr),
+                                           C.c_void_p(dc.ptr), C.c_void_p(dn.ptr)), self.ctx.handle, "scrfd_detect")
+        return dd, dk, dc, dn
+
+    def read_results(self, bufs, n: int) -> List[Tuple[np.ndarray, np.ndarray]]:
+        dd, dk, dc, dn = bufs
+        cnt = self.ctx.download(dc.ptr, (n,), np.int32)
+        ncand = self.ctx.download(dn.ptr, (n,), np.int32)
+        if np.any(ncand > 8192):
+            raise RuntimeError("SCRFD candidate capacity (8192 per frame) exceeded; raise det_thresh")
+        dets = self.ctx.download(dd.ptr, (n, self.max_det, 5), np.float32)
+        kps = self.ctx.download(dk.ptr, (n, self.max_det, 10), np.float32)
+        out = []
+        for i in range(n):
+            k = min(int(cnt[i]), self.max_det)
+            out.append((dets[i, :k].copy(), kps[i, :k].reshape(k, 5, 2).copy()))
+        return out
+
+    def detect_frames(self, d_frames: Sequence[Tuple[int, int, int, int]], thresh: float,
+                      nms_thresh: float = 0.4) -> List[Tuple[np.ndarray, np.ndarray]]:
+        """d_frames: (device ptr, H, W, row_stride) per frame (BGR u8)."""
+        descs, scales = [], []
+        for (ptr, H, W, rs) in d_frames:
+            d, s = make_letterbox_desc(ptr, H, W, rs, self.D)
+            descs.append(d)
+            scales.append(s)
+        res = []
+        for s0 in range(0, len(descs), self.max_batch):
+            b = self.detect_device(descs[s0:s0 + self.max_batch], scales[s0:s0 + self.max_batch], thresh, nms_thresh)
+            res.extend(self.read_results(b, len(descs[s0:s0 + self.max_batch])))
+        return res

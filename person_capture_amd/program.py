@@ -1,0 +1,205 @@
+"""Serialized network programs for the gfx950 executor (pcgpu.h: pc_net_create).
+
+A program is the host-side description of one conv network after all
+inference-time algebra has been applied (BN folded into weights/biases, the
+IResNet pre-BN folded with a per-border-class bias table, ResNetV1e avg-down
+shortcuts rewritten as 2x2/s2 convs, PAFPN top-down/bottom-up adds expressed as
+residual epilogues or second K-segments). The device executor
+(csrc/pc_api.cpp) only sees CONV / STEM / MAXPOOL ops over NHWC tensor views.
+
+Binary format (little-endian int32 words, then float32 data):
+  magic 'PCNT', version 1, n_buf, n_tensor, n_array, n_op, n_out, input_tensor
+  buffers : n_buf   x [elems_per_image lo, hi, is_f32, 0]
+  tensors : n_tensor x [buf, H, W, C, cs, coff, is_f32, 0]
+  arrays  : n_array x [offset lo, hi, count lo, hi]   (in floats, into data)
+  outputs : n_out tensor ids
+  ops     : n_op x 32 words (layouts below, mirrored in pc_api.cpp)
+  data    : float32
+"""
+from __future__ import annotations
+
+import struct
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+OP_CONV, OP_STEM, OP_MAXPOOL = 1, 2, 3
+ACT_NONE, ACT_RELU, ACT_PRELU, ACT_SILU = 0, 1, 2, 3
+BIAS_NONE, BIAS_CHANNEL, BIAS_BORDER9 = 0, 1, 2
+RES_NONE, RES_SAME, RES_UP2 = 0, 1, 2
+
+
+def cpad(c: int, m: int = 32) -> int:
+    return (int(c) + m - 1) // m * m
+
+
+class Program:
+    """Builder for a pcgpu network program."""
+
+    def __init__(self) -> None:
+        self.vbufs: List[List[int]] = []          # [elems_per_image, is_f32]
+        self.tensors: List[List[int]] = []        # [vbuf, H, W, C, cs, coff, is_f32]
+        self.arrays: List[np.ndarray] = []
+        self.ops: List[List[int]] = []
+        self.outputs: List[int] = []
+        self.input: Optional[int] = None
+        self.flops_per_image = 0.0
+
+    # ---- tensors -------------------------------------------------------
+    def input_tensor(self, H: int, W: int, C: int) -> int:
+        t = len(self.tensors)
+        self.tensors.append([-1, H, W, C, C, 0, 0])
+        self.input = t
+        return t
+
+    def act(self, H: int, W: int, C: int, is_f32: int = 0) -> int:
+        vb = len(self.vbufs)
+        self.vbufs.append([H * W * C, is_f32])
+        t = len(self.tensors)
+        self.tensors.append([vb, H, W, C, C, 0, is_f32])
+        return t
+
+    def dims(self, t: int) -> Tuple[int, int, int]:
+        T = self.tensors[t]
+        return T[1], T[2], T[3]
+
+    def arr(self, a: np.ndarray) -> int:
+        self.arrays.append(np.ascontiguousarray(a, dtype=np.float32).reshape(-1))
+        return len(self.arrays) - 1
+
+    # ---- ops -----------------------------------------------------------
+    def conv(self, out: int, segs: Sequence[Tuple[int, int, int, int, int, int]], w_packed: np.ndarray,
+             cout: int, bias: Optional[np.ndarray] = None, bias_mode: int = BIAS_CHANNEL,
+             slope: Optional[np.ndarray] = None, act: int = ACT_NONE, res: Optional[int] = None,
+             res_mode: int = RES_SAME, act_after_res: int = 0, splitk: int = 1) -> None:
+        """segs: (tensor, KH, KW, stride, pad, cin_true) per K-segment (max 2)."""
+        assert 1 <= len(segs) <= 2
+        npad, ktot = w_packed.shape
+        w = [0] * 32
+        w[0] = OP_CONV
+        w[1] = out
+        w[2] = len(segs)
+        for i, (t, kh, kw, s, p, _cin) in enumerate(segs):
+            w[3 + 5 * i: 8 + 5 * i] = [t, kh, kw, s, p]
+            w[25 + i] = _cin
+        w[13] = self.arr(w_packed)
+        w[14] = npad
+        w[15] = ktot
+        w[16] = cout
+        w[17] = self.arr(bias) if bias is not None else -1
+        w[18] = bias_mode if bias is not None else BIAS_NONE
+        w[19] = self.arr(slope) if slope is not None else -1
+        w[20] = act
+        w[21] = res if res is not None else -1
+        w[22] = res_mode if res is not None else RES_NONE
+        w[23] = act_after_res
+        w[24] = splitk
+        self.ops.append(w)
+        oh, ow, _ = self.dims(out)
+        for (t, kh, kw, s, p, cin) in segs:
+            self.flops_per_image += 2.0 * oh * ow * cout * kh * kw * cin
+
+    def stem(self, out: int, x: int, w: np.ndarray, bias: np.ndarray, stride: int, pad: int,
+             slope: Optional[np.ndarray] = None, act: int = ACT_NONE, cin_true: int = 3) -> None:
+        """w: [cout][3][3][4] folded filter (input channel 3 is padding)."""
+        cout = w.shape[0]
+        _, _, cp = self.dims(out)
+        ops = [0] * 32
+        ops[0] = OP_STEM
+        ops[1:13] = [out, x, 3, 3, stride, pad, self.arr(w), cout, self.arr(bias),
+                     self.arr(slope) if slope is not None else -1, act, cp]
+        ops[13] = cin_true
+        self.ops.append(ops)
+        oh, ow, _ = self.dims(out)
+        self.flops_per_image += 2.0 * oh * ow * cout * 9 * cin_true
+
+    def maxpool(self, out: int, x: int, k: int, s: int, p: int) -> None:
+        ops = [0] * 32
+        ops[0:6] = [OP_MAXPOOL, out, x, k, s, p]
+        self.ops.append(ops)
+
+    # ---- serialization --------------------------------------------------
+    def _op_io(self, w: List[int]) -> Tuple[List[int], int]:
+        if w[0] == OP_CONV:
+            ins = [w[3 + 5 * i] for i in range(w[2])]
+            if w[21] >= 0:
+                ins.append(w[21])
+            return ins, w[1]
+        return [w[2]], w[1]
+
+    def _assign_buffers(self) -> Tuple[List[List[int]], List[int]]:
+        """Liveness-based reuse of activation buffers (same dtype pool)."""
+        nv = len(self.vbufs)
+        first = [None] * nv
+        last = [-1] * nv
+        for i, w in enumerate(self.ops):
+            ins, out = self._op_io(w)
+            vb = self.tensors[out][0]
+            if vb >= 0 and first[vb] is None:
+                first[vb] = i
+            for t in ins:
+                vb = self.tensors[t][0]
+                if vb >= 0:
+                    last[vb] = max(last[vb], i)
+        for t in self.outputs:
+            vb = self.tensors[t][0]
+            if vb >= 0:
+                last[vb] = len(self.ops) + 1
+        phys: List[List[int]] = []     # [elems, is_f32, busy_until]
+        mapping = [-1] * nv
+        order = sorted([v for v in range(nv) if first[v] is not None], key=lambda v: first[v])
+        for v in order:
+            elems, f32 = self.vbufs[v]
+            lastv = max(last[v], first[v])
+            best = -1
+            for j, (pe, pf, busy) in enumerate(phys):
+                if pf == f32 and busy < first[v]:
+                    if best < 0 or abs(pe - elems) < abs(phys[best][0] - elems):
+                        best = j
+            if best < 0:
+                phys.append([elems, f32, lastv])
+                best = len(phys) - 1
+            else:
+                phys[best][0] = max(phys[best][0], elems)
+                phys[best][2] = lastv
+            mapping[v] = best
+        return phys, mapping
+
+    def serialize(self) -> bytes:
+        assert self.input is not None and self.outputs
+        phys, mapping = self._assign_buffers()
+        words: List[int] = [0x544E4350, 1, len(phys), len(self.tensors), len(self.arrays), len(self.ops),
+                            len(self.outputs), self.input]
+        for elems, f32, _ in phys:
+            words += [elems & 0xFFFFFFFF, elems >> 32, f32, 0]
+        for vb, H, W, C, cs, coff, f32 in self.tensors:
+            words += [mapping[vb] if vb >= 0 else -1, H, W, C, cs, coff, f32, 0]
+        off = 0
+        for a in self.arrays:
+            n = a.size
+            words += [off & 0xFFFFFFFF, off >> 32, n & 0xFFFFFFFF, n >> 32]
+            off += n
+        words += list(self.outputs)
+        for w in self.ops:
+            assert len(w) == 32
+            words += w
+        head = struct.pack("<%di" % len(words), *[int(x) if x < 2**31 else int(x) - 2**32 for x in words])
+        data = np.concatenate(self.arrays).astype("<f4").tobytes() if self.arrays else b""
+        return head + data
+
+
+def pack_conv_weights(ws: Sequence[np.ndarray], cin_pads: Sequence[int], npad: int) -> np.ndarray:
+    """[cout][cin][kh][kw] per segment -> [npad][sum_s kh*kw*cin_pad_s], K = tap-major, channel-minor."""
+    cols = []
+    for w, cp in zip(ws, cin_pads):
+        cout, cin, kh, kw = w.shape
+        t = np.zeros((npad, kh, kw, cp), dtype=np.float64)
+        t[:cout, :, :, :cin] = np.transpose(w, (0, 2, 3, 1))
+        cols.append(t.reshape(npad, kh * kw * cp))
+    return np.concatenate(cols, axis=1).astype(np.float32)
+
+
+def pad_vec(v: np.ndarray, n: int) -> np.ndarray:
+    out = np.zeros((n,), dtype=np.float64)
+    out[: v.shape[0]] = v
+    return out

@@ -1,0 +1,159 @@
+"""Thin Python handles over the pcgpu C ABI: a per-GPU context, device buffers
+and compiled networks. No torch types cross the boundary; device memory is
+owned by the native library (hipMalloc) and addressed by integer pointers."""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, Optional, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import PC_PREC_F16, PC_PREC_F32, check
+
+
+class DeviceBuffer:
+    """A raw device allocation owned by a GpuContext."""
+
+    def __init__(self, ctx: "GpuContext", nbytes: int):
+        self.ctx = ctx
+        self.nbytes = int(nbytes)
+        p = C.c_void_p()
+        check(ctx.lib.pc_device_alloc(ctx.handle, max(self.nbytes, 16), C.byref(p)), ctx.handle, "alloc")
+        self.ptr = int(p.value)
+
+    def free(self) -> None:
+        if self.ptr and self.ctx.handle:
+            self.ctx.lib.pc_device_free(self.ctx.handle, C.c_void_p(self.ptr))
+        self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class GpuContext:
+    """One context per (GPU, consumer): stream, zero page, staging ring."""
+
+    def __init__(self, device_id: int = 0):
+        self.lib = _lib.load()
+        self.device_id = int(device_id)
+        h = C.c_void_p()
+        rc = self.lib.pc_ctx_create(self.device_id, C.byref(h))
+        if rc != 0:
+            raise RuntimeError(f"pcgpu: cannot create a context on HIP device {device_id} (status {rc})")
+        self.handle = h
+        self._keep = []   # host arrays referenced by in-flight async copies
+        self._bufs: Dict[str, DeviceBuffer] = {}
+
+    def close(self) -> None:
+        if self.handle:
+            self._bufs.clear()
+            self.lib.pc_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- memory ----
+    def alloc(self, nbytes: int) -> DeviceBuffer:
+        return DeviceBuffer(self, nbytes)
+
+    def scratch(self, key: str, nbytes: int) -> DeviceBuffer:
+        """A named, growable scratch buffer (reused across calls)."""
+        b = self._bufs.get(key)
+        if b is None or b.nbytes < nbytes:
+            if b is not None:
+                self.sync()
+            b = DeviceBuffer(self, max(int(nbytes), 256))
+            self._bufs[key] = b
+        return b
+
+    def upload(self, arr: np.ndarray, dst: Optional[DeviceBuffer] = None, offset: int = 0) -> DeviceBuffer:
+        a = np.ascontiguousarray(arr)
+        if dst is None:
+            dst = self.alloc(a.nbytes)
+        check(self.lib.pc_copy_h2d(self.handle, C.c_void_p(dst.ptr + offset), a.ctypes.data_as(C.c_void_p), a.nbytes),
+              self.handle, "h2d")
+        self._keep.append(a)
+        return dst
+
+    def download(self, ptr: int, shape, dtype) -> np.ndarray:
+        out = np.empty(shape, dtype=dtype)
+        if out.nbytes:
+            check(self.lib.pc_copy_d2h(self.handle, out.ctypes.data_as(C.c_void_p), C.c_void_p(int(ptr)), out.nbytes),
+                  self.handle, "d2h")
+        self.sync()
+        return out
+
+    def memset(self, ptr: int, value: int, nbytes: int) -> None:
+        check(self.lib.pc_memset(self.handle, C.c_void_p(int(ptr)), int(value), int(nbytes)), self.handle, "memset")
+
+    def sync(self) -> None:
+        check(self.lib.pc_ctx_sync(self.handle), self.handle, "sync")
+        self._keep.clear()
+
+    @property
+    def stream(self) -> int:
+        return int(self.lib.pc_ctx_stream(self.handle) or 0)
+
+
+class Net:
+    """A compiled network resident on one GPU (weights + activation buffers)."""
+
+    def __init__(self, ctx: GpuContext, program: bytes, precision: int = PC_PREC_F16, max_batch: int = 1):
+        self.ctx = ctx
+        self.precision = int(precision)
+        self.max_batch = int(max_batch)
+        buf = C.create_string_buffer(program, len(program))
+        h = C.c_void_p()
+        check(ctx.lib.pc_net_create(ctx.handle, buf, len(program), self.precision, self.max_batch, C.byref(h)),
+              ctx.handle, "net_create")
+        self.handle = h
+        d = (C.c_int32 * 4)()
+        check(ctx.lib.pc_net_input_dims(h, d), ctx.handle, "input_dims")
+        self.input_dims = tuple(d)
+        fl = C.c_double()
+        nl = C.c_int32()
+        ctx.lib.pc_net_stats(h, C.byref(fl), C.byref(nl))
+        self.flops_per_image = fl.value
+        self.launches = nl.value
+
+    @property
+    def act_itemsize(self) -> int:
+        return 4 if self.precision == PC_PREC_F32 else 2
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            self.ctx.lib.pc_net_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_graph(self, enable: bool) -> None:
+        check(self.ctx.lib.pc_net_set_graph(self.handle, 1 if enable else 0), self.ctx.handle, "set_graph")
+
+    def run(self, d_input: int, batch: int) -> None:
+        check(self.ctx.lib.pc_net_run(self.handle, C.c_void_p(int(d_input)), int(batch)), self.ctx.handle, "net_run")
+
+    def output(self, i: int) -> Tuple[int, Tuple[int, int, int, int, int]]:
+        p = C.c_void_p()
+        d = (C.c_int32 * 5)()
+        check(self.ctx.lib.pc_net_output(self.handle, i, C.byref(p), d), self.ctx.handle, "net_output")
+        return int(p.value), tuple(d)
+
+    def read_output(self, i: int, batch: int) -> np.ndarray:
+        """Download output i as float32 [batch][H][W][C] (channel padding dropped by caller)."""
+        ptr, (H, W, Cc, cs, is_f32) = self.output(i)
+        dt = np.float32 if is_f32 else np.float16
+        raw = self.ctx.download(ptr, (batch, H, W, cs), dt)
+        return raw[..., :Cc].astype(np.float32)

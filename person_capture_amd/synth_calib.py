@@ -1,0 +1,112 @@
+"""BatchNorm-statistics calibration for synthetic weights (weight synthesis only).
+
+No trained weights exist offline. Seeded random weights alone
+make activations explode or vanish over 100 layers, so synth_* runs ONE CPU
+forward on seeded synthetic inputs and sets every BatchNorm's running
+mean/variance to the statistics of its input there — the data-dependent init a
+trained network's running statistics stand in for. This module is part of
+weight synthesis (like downloading a checkpoint in the reference); inference
+never runs through it. The parity oracle is a separate implementation
+(oracle/nets_torch.py).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+BN_EPS = 1e-5
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _bn_cal(p, name, x, var_floor=1e-4):
+    torch = _torch()
+    F = torch.nn.functional
+    mean = x.mean(dim=(0, 2, 3)) if x.dim() == 4 else x.mean(dim=0)
+    var = x.var(dim=(0, 2, 3), unbiased=False) if x.dim() == 4 else x.var(dim=0, unbiased=False)
+    var = torch.clamp(var, min=var_floor)
+    p[name + ".running_mean"] = mean.numpy().astype(np.float32)
+    p[name + ".running_var"] = var.numpy().astype(np.float32)
+    w = torch.from_numpy(p[name + ".weight"])
+    b = torch.from_numpy(p[name + ".bias"])
+    return F.batch_norm(x, torch.from_numpy(p[name + ".running_mean"]), torch.from_numpy(p[name + ".running_var"]),
+                        w, b, False, 0.0, BN_EPS)
+
+
+def calibrate_iresnet(p, depth, imgs_bgr_u8):
+    from .models import iresnet_blocks
+    torch = _torch()
+    F = torch.nn.functional
+    T = lambda k: torch.from_numpy(p[k])
+    with torch.no_grad():
+        x = torch.from_numpy(imgs_bgr_u8[..., ::-1].astype(np.float32) / 127.5 - 1.0).permute(0, 3, 1, 2).contiguous()
+        x = F.conv2d(x, T("conv1.weight"), padding=1)
+        x = _bn_cal(p, "bn1", x)
+        x = F.prelu(x, T("prelu.weight"))
+        for pre, inp, pl, stride, ds in iresnet_blocks(depth):
+            o = _bn_cal(p, pre + ".bn1", x)
+            o = F.conv2d(o, T(pre + ".conv1.weight"), padding=1)
+            o = _bn_cal(p, pre + ".bn2", o)
+            o = F.prelu(o, T(pre + ".prelu.weight"))
+            o = F.conv2d(o, T(pre + ".conv2.weight"), stride=stride, padding=1)
+            o = _bn_cal(p, pre + ".bn3", o)
+            idt = x
+            if ds:
+                idt = _bn_cal(p, pre + ".downsample.1", F.conv2d(x, T(pre + ".downsample.0.weight"), stride=stride))
+            x = o + idt
+        x = _bn_cal(p, "bn2", x)
+        x = torch.flatten(x, 1)
+        x = F.linear(x, T("fc.weight"), T("fc.bias"))
+        _bn_cal(p, "features", x, var_floor=1e-2)
+
+
+def calibrate_scrfd(p, variant, rng, target_per_image, D=640, n=2):
+    from .models import SCRFD_CFG, SCRFD_STRIDES, scrfd_blocks
+    torch = _torch()
+    F = torch.nn.functional
+    T = lambda k: torch.from_numpy(p[k])
+    cfg = SCRFD_CFG[variant]
+    # synthetic letterboxed 16:9 frames: noise content in the top-left D x 9D/16 region
+    img = np.zeros((n, D, D, 3), np.uint8)
+    img[:, : D * 9 // 16] = rng.integers(0, 256, size=(n, D * 9 // 16, D, 3), dtype=np.uint8)
+    with torch.no_grad():
+        x = torch.from_numpy((img[..., ::-1].astype(np.float32) - 127.5) / 128.0).permute(0, 3, 1, 2).contiguous()
+        x = F.relu(_bn_cal(p, "backbone.stem.1", F.conv2d(x, T("backbone.stem.0.weight"), stride=2, padding=1)))
+        x = F.relu(_bn_cal(p, "backbone.stem.4", F.conv2d(x, T("backbone.stem.3.weight"), padding=1)))
+        x = F.relu(_bn_cal(p, "backbone.stem.7", F.conv2d(x, T("backbone.stem.6.weight"), padding=1)))
+        x = F.max_pool2d(x, 3, 2, 1)
+        feats = []
+        blocks = scrfd_blocks(cfg)
+        for i, (pre, inp, pl, stride, ds) in enumerate(blocks):
+            o = F.relu(_bn_cal(p, pre + ".bn1", F.conv2d(x, T(pre + ".conv1.weight"), stride=stride, padding=1)))
+            o = _bn_cal(p, pre + ".bn2", F.conv2d(o, T(pre + ".conv2.weight"), padding=1))
+            idt = x
+            if ds:
+                y = F.avg_pool2d(x, stride, stride, ceil_mode=True, count_include_pad=False) if stride > 1 else x
+                idt = _bn_cal(p, pre + ".downsample.2", F.conv2d(y, T(pre + ".downsample.1.weight")))
+            x = F.relu(o + idt)
+            last = i + 1 == len(blocks) or blocks[i + 1][0].split(".")[1] != pre.split(".")[1]
+            if last:
+                feats.append(x)
+        ins = feats[1:]
+        cv = lambda t, nm, s=1, pd=0: F.conv2d(t, T(nm + ".weight"), T(nm + ".bias"), stride=s, padding=pd)
+        lat = [cv(ins[i], f"neck.lateral_convs.{i}.conv") for i in range(3)]
+        for i in (2, 1):
+            lat[i - 1] = lat[i - 1] + F.interpolate(lat[i], size=lat[i - 1].shape[2:], mode="nearest")
+        inter = [cv(lat[i], f"neck.fpn_convs.{i}.conv", 1, 1) for i in range(3)]
+        for i in range(2):
+            inter[i + 1] = inter[i + 1] + cv(inter[i], f"neck.downsample_convs.{i}.conv", 2, 1)
+        outs = [inter[0]] + [cv(inter[i], f"neck.pafpn_convs.{i - 1}.conv", 1, 1) for i in (1, 2)]
+        for lvl, s in enumerate(SCRFD_STRIDES):
+            h = outs[lvl]
+            for j in range(cfg["stacked"]):
+                h = F.relu(_bn_cal(p, f"bbox_head.{s}.stack.{j}.bn",
+                                   F.conv2d(h, T(f"bbox_head.{s}.stack.{j}.conv.weight"), padding=1)))
+            logits = F.conv2d(h, T(f"bbox_head.{s}.cls.weight"), padding=1)  # no bias
+            flat = logits.reshape(-1).numpy().astype(np.float64)
+            per_img = flat.size / n
+            q = 1.0 - float(target_per_image[lvl]) / per_img
+            thr = float(np.quantile(flat, min(max(q, 0.0), 1.0)))
+            p[f"bbox_head.{s}.cls.bias"] = np.full(logits.shape[1], -thr, np.float32)
