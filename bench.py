@@ -1,0 +1,207 @@
+#!/usr/bin/env python3
+"""Benchmark: frames/sec of detect + embed + match @1080p (BASELINE.json `metric`).
+
+Workload (BASELINE.json configs[2], the single-GPU config the metric is quoted
+on): a batch of 64 synthetic 1080p BGR frames resident in HBM; one step =
+FaceEmbedder.extract_batch over the batch (SCRFD-10G letterbox + detect + NMS,
+5-point align, quality, ArcFace-R100 with flip-TTA, L2) + cosine match of every
+face against a 32-entry reference bank on the device. Seeded synthetic
+weights (no checkpoints exist offline). Frames shard across ranks with no
+collective (weak scaling): each rank runs its own batch; value = all frames /
+max-over-ranks time.
+
+Also reported: roofline of the dominant kernel family (the MFMA implicit-GEMM
+convs of both networks: algorithmic FLOPs / HIP-event time of their launches
+inside the timed region) and a bounded CPU baseline (the oracle port of the same
+pipeline, rank 0, N=1).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.dont_write_bytecode = True
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_F16_TFLOPS = 2500.0   # MI355X dense fp16 MFMA (MI355X_MICROARCH.md, chip table)
+PEAK_F32_TFLOPS = 157.3
+
+
+def _dist_init():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", init_method="env://", world_size=world, rank=rank)
+    return world, rank, local
+
+
+def _barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def _max_over_ranks(world, v: float) -> float:
+    if world == 1:
+        return v
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([v], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def _sum_over_ranks(world, v: float) -> float:
+    if world == 1:
+        return v
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([v], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def synth_frames(rank: int, n: int, H: int = 1080, W: int = 1920) -> np.ndarray:
+    """np.random.default_rng(seed=20260501 + frame_idx) u8 BGR frames."""
+    out = np.empty((n, H, W, 3), np.uint8)
+    for i in range(n):
+        out[i] = np.random.default_rng(20260501 + rank * 1_000_000 + i).integers(0, 256, (H, W, 3), dtype=np.uint8)
+    return out
+
+
+def synth_bank(n: int, dim: int = 512) -> np.ndarray:
+    b = np.random.default_rng(20260503).standard_normal((n, dim)).astype(np.float32)
+    return b / np.linalg.norm(b, axis=1, keepdims=True)
+
+
+def cpu_baseline(frames: np.ndarray, fe, bank: np.ndarray, n_sample: int):
+    """The oracle port of the same pipeline on the host cores, bounded sample."""
+    import torch
+    from oracle import pipeline as op
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    t0 = time.perf_counter()
+    faces = 0
+    for i in range(n_sample):
+        r = op.extract_frame(frames[i], fe._scrfd_params, fe.scrfd_variant, fe._arc_params, fe._arc_depth,
+                             conf=fe.conf, D=640, bank=bank)
+        faces += 0 if r == op.NEEDS_FALLBACK else len(r)
+    dt = time.perf_counter() - t0
+    return {"value": round(n_sample / dt, 4), "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{n_sample} of the bench's 1080p frames through oracle/pipeline.extract_frame "
+                      f"(fp32 torch-CPU SCRFD-10G + ArcFace-R100 flip-TTA, numpy/C post), {faces} faces, "
+                      f"{dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--bank", type=int, default=32)
+    ap.add_argument("--cpu-sample", type=int, default=12)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--precision", default="f16", choices=["f16", "f32"])
+    args = ap.parse_args()
+
+    world, rank, local = _dist_init()
+    os.environ.setdefault("PERSON_CAPTURE_AMD_PRECISION", args.precision)
+    os.environ.setdefault("PERSON_CAPTURE_AMD_DET_BATCH", str(args.batch))
+    os.environ.setdefault("PERSON_CAPTURE_AMD_ARC_BATCH", "512")
+    from person_capture_amd.face_embedder import FaceEmbedder, _DevImage
+    from person_capture_amd.match import DeviceBank
+
+    fe = FaceEmbedder(ctx=f"cuda:{local}", yolo_model="scrfd_10g_bnkps", conf=0.5)
+    frames = synth_frames(rank, args.batch)
+    ctx = fe._ctx
+    dframes = ctx.alloc(frames.nbytes)
+    ctx.upload(frames, dframes)
+    fsz = frames[0].nbytes
+    devs = [_DevImage(dframes.ptr + i * fsz, 1080, 1920, 1920 * 3) for i in range(args.batch)]
+    bank_h = synth_bank(args.bank)
+    bank = DeviceBank(ctx, bank_h)
+    ctx.sync()
+
+    def step():
+        res = fe.extract_batch([None] * args.batch, dev_frames=devs, bank=bank)
+        return res
+
+    for _ in range(args.warmup):
+        res = step()
+    nfaces = sum(len(r) for r in res)
+    accept = sum(1 for r in res for f in r if f["fd"] <= 0.45)
+    nets = [fe._engine(640).net, fe._arc.net]
+    for n in nets:
+        n.profile(True)
+    _barrier(world)
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    ctx.sync()
+    t1 = time.perf_counter()
+    _barrier(world)
+    elapsed = _max_over_ranks(world, t1 - t0)
+    prof = [n.profile_read() for n in nets]
+    for n in nets:
+        n.profile(False)
+    conv_ms = sum(p["conv_ms"] for p in prof)
+    conv_launches = sum(p["conv_launches"] for p in prof)
+    conv_flops = sum(p["conv_flops"] for p in prof)
+    total_frames = _sum_over_ranks(world, args.batch * args.steps)
+    value = total_frames / elapsed
+    achieved = conv_flops / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
+    peak = PEAK_F16_TFLOPS if args.precision == "f16" else PEAK_F32_TFLOPS
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.isfile(tpath):
+        try:
+            traffic = json.load(open(tpath)).get("conv_hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    out = {
+        "metric": "frames/sec detect+embed+match @1080p, 1/2/4/8 GPU; MFMA util %",
+        "value": round(value, 3),
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.precision,
+        "data": "synthetic (seeded u8 1080p frames, seeded synthetic SCRFD-10G/IResNet-100 weights)",
+        "config": {"workload": "C3: SCRFD-10G detect + ArcFace-R100 embed (flip-TTA) + cosine match vs "
+                               f"{args.bank}-embedding bank, 1080p, batch {args.batch} frames per GPU",
+                   "frames_per_step_per_gpu": args.batch, "det_size": 640, "bank": args.bank,
+                   "faces_per_frame": round(nfaces / args.batch, 3), "accepted_faces_per_step": accept,
+                   "parallelism": f"frame-shard x{world} (no collective)"},
+        "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                     "frac": round(achieved / peak, 4), "traffic": traffic,
+                     "kernel": "conv_igemm (SCRFD + ArcFace implicit-GEMM convs)",
+                     "launches": conv_launches, "avg_launch_us": round(conv_ms * 1e3 / max(1, conv_launches), 2),
+                     "flops_per_launch": round(conv_flops / max(1, conv_launches)),
+                     "conv_share_of_step": round(conv_ms * 1e-3 / (t1 - t0), 4)},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(frames, fe, bank_h, args.cpu_sample)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

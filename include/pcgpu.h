@@ -30,6 +30,7 @@
  *   pc_rotate_pad                      cv2.rotate + cv2.copyMakeBorder(BORDER_REPLICATE)
  *                                      (face_embedder.py:2165-2169, 2292-2294, 2394)
  *   pc_resize_area                     cv2.resize(..., INTER_AREA) (gui_app.py:1505-1507)
+ *   pc_resize_linear                   cv2.resize(..., INTER_LINEAR) (face_embedder.py:2264, 2460)
  */
 #ifndef PCGPU_H
 #define PCGPU_H
@@ -83,6 +84,17 @@ typedef struct pc_warp_desc {
   int32_t pad1_;
 } pc_warp_desc;
 
+/* One u8 -> u8 INTER_LINEAR resize job (cv2.resize semantics, BGR). */
+typedef struct pc_resize_desc {
+  const uint8_t* d_src;
+  int32_t H, W, row_stride;
+  int32_t new_w, new_h;
+  double scale_x, scale_y;
+  int32_t simd_end;
+  int32_t pad_;
+  uint8_t* d_dst; /* new_h x new_w x 3 contiguous */
+} pc_resize_desc;
+
 /* One INTER_AREA coefficient: source index, destination index, weight. */
 typedef struct pc_area_tab {
   int32_t si;
@@ -119,10 +131,15 @@ int pc_net_num_outputs(pc_net* net);
 int pc_net_stats(pc_net* net, double* h_flops_per_image, int32_t* h_launches);
 /* capture pc_net_run(batch) into a HIP graph and replay it on later runs of the same batch */
 int pc_net_set_graph(pc_net* net, int enable);
+/* HIP-event timing of every op of every later (non-graph) run; enable resets the counters.
+ * read: [0] conv ms, [1] conv launches, [2] conv FLOPs (algorithmic), [3] other ms, [4] other launches */
+int pc_net_profile(pc_net* net, int enable);
+int pc_net_profile_read(pc_net* net, double* h_out5);
 
 /* ---- image kernels ---- */
 int pc_letterbox(pc_ctx* ctx, int precision, const pc_letterbox_desc* h_descs, int n, int D, void* d_out);
 int pc_warp_affine(pc_ctx* ctx, const pc_warp_desc* h_descs, int n);
+int pc_resize_linear(pc_ctx* ctx, const pc_resize_desc* h_descs, int n);
 int pc_face_quality(pc_ctx* ctx, const uint8_t* d_chips, int n, int side, double* d_out);
 int pc_arcface_prep(pc_ctx* ctx, int precision, const uint8_t* d_chips, int n, int side, int flip, void* d_out);
 int pc_rotate_pad(pc_ctx* ctx, const uint8_t* d_src, int H, int W, int row_stride, int deg, int pad, uint8_t* d_dst);
@@ -145,6 +162,14 @@ int pc_embed_finalize(pc_ctx* ctx, const float* d_e, int ld, int n, int dim, int
 int pc_arcface_embed(pc_net* net, const uint8_t* d_chips, int n, int flip, float* d_feat);
 int pc_bank_match(pc_ctx* ctx, const float* d_q, int n, const float* d_bank, int b, int dim, float* d_fd,
                   int32_t* d_idx);
+
+/* ---- host-side align geometry (CPU, batched) ---- */
+/* cv::estimateAffinePartial2D(from, to, method=LMEDS) for n point sets of npts points each
+ * (h_from [n][npts][2], shared h_to [npts][2]); h_M [n][6] src->dst, h_ok [n] 0/1.
+ * Replaces the call at face_embedder.py:1466-1468. */
+int pc_estimate_affine_partial(const float* h_from, const float* h_to, int npts, int n, double* h_M, int32_t* h_ok);
+/* the inversion cv::warpAffine applies to M (no WARP_INVERSE_MAP) */
+int pc_invert_affine(const double* h_M, double* h_iM);
 
 #ifdef __cplusplus
 }

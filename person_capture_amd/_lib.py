@@ -32,11 +32,17 @@ class WarpDesc(C.Structure):
                 ("out_h", C.c_int32), ("border", C.c_int32), ("pad1_", C.c_int32)]
 
 
+class ResizeDesc(C.Structure):
+    _fields_ = [("d_src", C.c_void_p), ("H", C.c_int32), ("W", C.c_int32), ("row_stride", C.c_int32),
+                ("new_w", C.c_int32), ("new_h", C.c_int32), ("scale_x", C.c_double), ("scale_y", C.c_double),
+                ("simd_end", C.c_int32), ("pad_", C.c_int32), ("d_dst", C.c_void_p)]
+
+
 class AreaTab(C.Structure):
     _fields_ = [("si", C.c_int32), ("di", C.c_int32), ("alpha", C.c_float)]
 
 
-assert C.sizeof(LetterboxDesc) == 56 and C.sizeof(WarpDesc) == 96 and C.sizeof(AreaTab) == 12
+assert C.sizeof(ResizeDesc) == 64 and C.sizeof(LetterboxDesc) == 56 and C.sizeof(WarpDesc) == 96 and C.sizeof(AreaTab) == 12
 
 _P = C.c_void_p
 _I = C.c_int
@@ -65,8 +71,11 @@ SIGNATURES = {
     "pc_net_num_outputs": ([_P], _I),
     "pc_net_stats": ([_P, C.POINTER(C.c_double), C.POINTER(C.c_int32)], _I),
     "pc_net_set_graph": ([_P, _I], _I),
+    "pc_net_profile": ([_P, _I], _I),
+    "pc_net_profile_read": ([_P, C.POINTER(C.c_double)], _I),
     "pc_letterbox": ([_P, _I, C.POINTER(LetterboxDesc), _I, _I, _P], _I),
     "pc_warp_affine": ([_P, C.POINTER(WarpDesc), _I], _I),
+    "pc_resize_linear": ([_P, C.POINTER(ResizeDesc), _I], _I),
     "pc_face_quality": ([_P, _P, _I, _I, _P], _I),
     "pc_arcface_prep": ([_P, _I, _P, _I, _I, _I, _P], _I),
     "pc_rotate_pad": ([_P, _P, _I, _I, _I, _I, _I, _P], _I),
@@ -76,6 +85,8 @@ SIGNATURES = {
     "pc_embed_finalize": ([_P, _P, _I, _I, _I, _I, _P], _I),
     "pc_arcface_embed": ([_P, _P, _I, _I, _P], _I),
     "pc_bank_match": ([_P, _P, _I, _P, _I, _I, _P, _P], _I),
+    "pc_estimate_affine_partial": ([_P, _P, _I, _I, _P, _P], _I),
+    "pc_invert_affine": ([_P, _P], _I),
 }
 
 

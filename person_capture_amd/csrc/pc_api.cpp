@@ -25,6 +25,8 @@ hipError_t maxpool_launch(int f32, const PoolParams& p, hipStream_t s);
 struct LetterboxDesc;
 struct WarpDesc;
 struct AreaTab;
+struct ResizeDesc;
+hipError_t resize_linear_launch(const ResizeDesc* d_descs, int N, int max_pixels, hipStream_t s);
 hipError_t letterbox_launch(int f32, const LetterboxDesc* d_descs, int N, int D, void* out, hipStream_t s);
 hipError_t warp_launch(const WarpDesc* d_descs, int N, int max_pixels, hipStream_t s);
 hipError_t quality_launch(const uint8_t* chips, int N, int side, double* out, hipStream_t s);
@@ -62,6 +64,7 @@ using namespace pc;
 static_assert(sizeof(pc_letterbox_desc) == 56, "letterbox desc layout");
 static_assert(sizeof(pc_warp_desc) == 96, "warp desc layout");
 static_assert(sizeof(pc_area_tab) == 12, "area tab layout");
+static_assert(sizeof(pc_resize_desc) == 64, "resize desc layout");
 
 struct pc_ctx {
   int device = 0;
@@ -200,7 +203,8 @@ enum { OP_CONV = 1, OP_STEM = 2, OP_MAXPOOL = 3 };
 struct NetBuf { long long elems; int is_f32; void* d = nullptr; };
 struct NetTensor { int buf, H, W, C, cs, coff, is_f32; };
 struct NetOp { int w[32]; };
-struct ConvPlan { int rowb, bc, bp, splitk; long long M_per_image; };
+struct ConvPlan { int rowb, bc, bp, splitk; long long M_per_image; double flops_per_image; };
+struct ProfRec { int a, b, kind; double flops; };
 
 struct pc_net {
   pc_ctx* ctx = nullptr;
@@ -221,6 +225,11 @@ struct pc_net {
   const void* cur_input = nullptr;
   // graph replay
   int use_graph = 0;
+  // per-op HIP-event profiling (pc_net_profile)
+  int prof = 0;
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_used = 0;
+  std::vector<ProfRec> recs;
   std::map<std::pair<int, const void*>, hipGraphExec_t> graphs;
   // arcface scratch
   void* prep = nullptr;
@@ -355,6 +364,7 @@ extern "C" int pc_net_create(pc_ctx* c, const void* prog, size_t nbytes, int pre
         macs += (double)Y.H * Y.W * op.w[16] * op.w[4 + 5 * s] * op.w[5 + 5 * s] * cin_true;
       }
       n->flops_per_image += 2.0 * macs;
+      n->plans[i].flops_per_image = 2.0 * macs;
       n->launches += pl.splitk > 1 ? 2 : 1;
     } else if (op.w[0] == OP_STEM) {
       const NetTensor& Y = n->tens[op.w[1]];
@@ -392,11 +402,25 @@ extern "C" int pc_net_destroy(pc_net* n) {
   return PC_OK;
 }
 
+static int prof_event(pc_net* n, int* idx) {
+  if (n->ev_used == n->ev_pool.size()) {
+    hipEvent_t e;
+    HIPCHK(n->ctx, hipEventCreate(&e));
+    n->ev_pool.push_back(e);
+  }
+  *idx = (int)n->ev_used++;
+  HIPCHK(n->ctx, hipEventRecord(n->ev_pool[*idx], n->ctx->stream));
+  return PC_OK;
+}
+
 static int run_ops(pc_net* n, int N) {
   pc_ctx* c = n->ctx;
   hipStream_t s = c->stream;
+  const bool prof = n->prof && !n->use_graph;
   for (size_t i = 0; i < n->ops.size(); ++i) {
     const int* w = n->ops[i].w;
+    ProfRec rec{-1, -1, w[0], w[0] == OP_CONV ? n->plans[i].flops_per_image * N : 0.0};
+    if (prof) { int rc = prof_event(n, &rec.a); if (rc) return rc; }
     if (w[0] == OP_CONV) {
       const ConvPlan& pl = n->plans[i];
       ConvParams p;
@@ -470,7 +494,36 @@ static int run_ops(pc_net* n, int N) {
       p.k = w[3]; p.stride = w[4]; p.pad = w[5];
       HIPCHK(c, maxpool_launch(n->f32, p, s));
     }
+    if (prof) {
+      int rc = prof_event(n, &rec.b);
+      if (rc) return rc;
+      n->recs.push_back(rec);
+    }
   }
+  return PC_OK;
+}
+
+extern "C" int pc_net_profile(pc_net* n, int enable) {
+  if (!n) return PC_ERR_ARG;
+  HIPCHK(n->ctx, hipStreamSynchronize(n->ctx->stream));
+  n->prof = enable ? 1 : 0;
+  n->ev_used = 0;
+  n->recs.clear();
+  return PC_OK;
+}
+
+extern "C" int pc_net_profile_read(pc_net* n, double* out) {
+  if (!n || !out) return PC_ERR_ARG;
+  HIPCHK(n->ctx, hipStreamSynchronize(n->ctx->stream));
+  double conv_ms = 0, other_ms = 0, flops = 0;
+  int conv_n = 0, other_n = 0;
+  for (const ProfRec& r : n->recs) {
+    float ms = 0.f;
+    HIPCHK(n->ctx, hipEventElapsedTime(&ms, n->ev_pool[r.a], n->ev_pool[r.b]));
+    if (r.kind == OP_CONV) { conv_ms += ms; conv_n++; flops += r.flops; }
+    else { other_ms += ms; other_n++; }
+  }
+  out[0] = conv_ms; out[1] = conv_n; out[2] = flops; out[3] = other_ms; out[4] = other_n;
   return PC_OK;
 }
 
@@ -536,6 +589,18 @@ extern "C" int pc_letterbox(pc_ctx* c, int prec, const pc_letterbox_desc* h, int
   int rc = stage_copy(c, h, sizeof(pc_letterbox_desc) * n, &dd);
   if (rc) return rc;
   HIPCHK(c, letterbox_launch(prec == PC_PREC_F32, (const LetterboxDesc*)dd, n, D, d_out, c->stream));
+  return PC_OK;
+}
+
+extern "C" int pc_resize_linear(pc_ctx* c, const pc_resize_desc* h, int n) {
+  if (!c || !h || n < 0) return fail(c, PC_ERR_ARG, "pc_resize_linear: bad arguments");
+  if (n == 0) return PC_OK;
+  int maxpix = 0;
+  for (int i = 0; i < n; ++i) maxpix = std::max(maxpix, h[i].new_w * h[i].new_h);
+  void* dd;
+  int rc = stage_copy(c, h, sizeof(pc_resize_desc) * n, &dd);
+  if (rc) return rc;
+  HIPCHK(c, resize_linear_launch((const ResizeDesc*)dd, n, maxpix, c->stream));
   return PC_OK;
 }
 

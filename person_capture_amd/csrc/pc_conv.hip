@@ -341,9 +341,8 @@ __global__ void splitk_reduce(const float* __restrict__ part, int splitk, int M,
 // 36-value input patch stays in registers (compile-time indexed).
 template <typename T>
 __global__ __launch_bounds__(256) void stem_conv3x3(StemParams p) {
-  __shared__ __attribute__((aligned(16))) float sw[64 * 36];
-  for (int i = threadIdx.x; i < p.cout * 36; i += blockDim.x) sw[i] = p.w[i];
-  __syncthreads();
+  // filter taps are wave-uniform: read them through the scalar cache (s_load), not LDS
+  const float* __restrict__ sw = p.w;
   const long long pix = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long M = (long long)p.N * p.OH * p.OW;
   if (pix >= M) return;

@@ -63,13 +63,12 @@ __global__ void letterbox_blob(const LetterboxDesc* __restrict__ descs, int D, T
     const int sy1 = sy + 1 < d.H ? sy + 1 : sy;
     const uint8_t* r0 = d.src + (long long)sy * d.row_stride;
     const uint8_t* r1 = d.src + (long long)sy1 * d.row_stride;
-    const bool simd = x * 3 < d.simd_end;  // which rounding OpenCV's vertical pass used for these bytes
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       const int S0 = r0[sx * 3 + c] * a0 + r0[sx1 * 3 + c] * a1;
       const int S1 = r1[sx * 3 + c] * a0 + r1[sx1 * 3 + c] * a1;
       int val;
-      if (simd) {
+      if (x * 3 + c < d.simd_end) {  // which rounding OpenCV's vertical pass used for this byte
         const int t0 = ((S0 >> 4) * (int)b0) >> 16;
         const int t1 = ((S1 >> 4) * (int)b1) >> 16;
         val = (t0 + t1 + 2) >> 2;
@@ -90,6 +89,46 @@ __global__ void letterbox_blob(const LetterboxDesc* __restrict__ descs, int D, T
     *reinterpret_cast<f16x4*>(o) = h;
   } else {
     *reinterpret_cast<f32x4*>(o) = f32x4{r, g, b, 0.f};
+  }
+}
+
+// Plain u8 -> u8 INTER_LINEAR resize of a (crop of a) BGR frame, same fixed point
+// as the letterbox (TTA rescales face_embedder.py:2264, chip resize fallback :2460).
+struct ResizeDesc {
+  const uint8_t* src;
+  int H, W, row_stride;
+  int new_w, new_h;
+  double scale_x, scale_y;
+  int simd_end;
+  int pad_;
+  uint8_t* dst;  // new_h x new_w x 3 contiguous
+};
+
+__global__ void resize_linear_u8(const ResizeDesc* __restrict__ descs) {
+  const ResizeDesc d = descs[blockIdx.y];
+  const int pix = blockIdx.x * blockDim.x + threadIdx.x;
+  if (pix >= d.new_w * d.new_h) return;
+  const int y = pix / d.new_w, x = pix - (pix / d.new_w) * d.new_w;
+  int sx, sy;
+  short a0, a1, b0, b1;
+  lin_coef(x, d.scale_x, d.W, sx, a0, a1);
+  lin_coef(y, d.scale_y, d.H, sy, b0, b1);
+  const int sx1 = sx + 1 < d.W ? sx + 1 : sx;
+  const int sy1 = sy + 1 < d.H ? sy + 1 : sy;
+  const uint8_t* r0 = d.src + (long long)sy * d.row_stride;
+  const uint8_t* r1 = d.src + (long long)sy1 * d.row_stride;
+  uint8_t* o = d.dst + (long long)pix * 3;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const int S0 = r0[sx * 3 + c] * a0 + r0[sx1 * 3 + c] * a1;
+    const int S1 = r1[sx * 3 + c] * a0 + r1[sx1 * 3 + c] * a1;
+    int val;
+    if (x * 3 + c < d.simd_end) {
+      val = ((((S0 >> 4) * (int)b0) >> 16) + (((S1 >> 4) * (int)b1) >> 16) + 2) >> 2;
+    } else {
+      val = (S0 * (int)b0 + S1 * (int)b1 + (1 << 21)) >> 22;
+    }
+    o[c] = (uint8_t)(val < 0 ? 0 : (val > 255 ? 255 : val));
   }
 }
 
@@ -317,6 +356,12 @@ hipError_t letterbox_launch(int f32, const LetterboxDesc* d_descs, int N, int D,
   dim3 grid((D * D + 255) / 256, N);
   if (f32) hipLaunchKernelGGL(letterbox_blob<float>, grid, dim3(256), 0, s, d_descs, D, (float*)out);
   else hipLaunchKernelGGL(letterbox_blob<f16>, grid, dim3(256), 0, s, d_descs, D, (f16*)out);
+  return hipGetLastError();
+}
+
+hipError_t resize_linear_launch(const ResizeDesc* d_descs, int N, int max_pixels, hipStream_t s) {
+  dim3 grid((max_pixels + 255) / 256, N);
+  hipLaunchKernelGGL(resize_linear_u8, grid, dim3(256), 0, s, d_descs);
   return hipGetLastError();
 }
 

@@ -142,6 +142,15 @@ class Net:
     def set_graph(self, enable: bool) -> None:
         check(self.ctx.lib.pc_net_set_graph(self.handle, 1 if enable else 0), self.ctx.handle, "set_graph")
 
+    def profile(self, enable: bool) -> None:
+        check(self.ctx.lib.pc_net_profile(self.handle, 1 if enable else 0), self.ctx.handle, "profile")
+
+    def profile_read(self) -> dict:
+        out = (C.c_double * 5)()
+        check(self.ctx.lib.pc_net_profile_read(self.handle, out), self.ctx.handle, "profile_read")
+        return {"conv_ms": out[0], "conv_launches": int(out[1]), "conv_flops": out[2], "other_ms": out[3],
+                "other_launches": int(out[4])}
+
     def run(self, d_input: int, batch: int) -> None:
         check(self.ctx.lib.pc_net_run(self.handle, C.c_void_p(int(d_input)), int(batch)), self.ctx.handle, "net_run")
 

@@ -1,0 +1,89 @@
+"""CPU (torch fp32) interpreter of pcgpu programs — test infrastructure.
+
+Executes the serialized op list exactly as the device executor defines it
+(csrc/pc_api.cpp + pc_conv.hip semantics: K-segments, border-class bias,
+activation before/after the residual, nearest-2x residual, split-K, stem,
+max-pool), so the inference-time algebra in person_capture_amd/models.py (BN
+folding, pre-BN border tables, avg-down rewrite, PAFPN fusions) can be checked
+against the literal oracle nets without a GPU.
+"""
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from person_capture_amd import program as pg
+
+
+def _act(y, act, slope):
+    if act == pg.ACT_RELU:
+        return F.relu(y)
+    if act == pg.ACT_PRELU:
+        return torch.where(y > 0, y, y * slope.view(1, -1, 1, 1))
+    if act == pg.ACT_SILU:
+        return F.silu(y)
+    return y
+
+
+def run_program(P: pg.Program, x_nhwc: np.ndarray):
+    """x_nhwc: [N][H][W][C] input (padded channels). Returns list of outputs NCHW (padded channels)."""
+    T = {}
+    T[P.input] = torch.from_numpy(np.ascontiguousarray(np.transpose(x_nhwc, (0, 3, 1, 2)))).float()
+    A = [torch.from_numpy(a.astype(np.float32)) for a in P.arrays]
+    for w in P.ops:
+        if w[0] == pg.OP_CONV:
+            out = P.tensors[w[1]]
+            npad, ktot = w[14], w[15]
+            W = A[w[13]].view(npad, ktot)
+            acc = None
+            k0 = 0
+            for s in range(w[2]):
+                t, kh, kw, st, pd = w[3 + 5 * s: 8 + 5 * s]
+                X = T[t]
+                cp = X.shape[1]
+                n = kh * kw * cp
+                ws = W[:, k0:k0 + n].view(npad, kh, kw, cp).permute(0, 3, 1, 2).contiguous()
+                k0 += n
+                y = F.conv2d(X, ws, stride=st, padding=pd)
+                acc = y if acc is None else acc + y
+            Ho, Wo = acc.shape[2], acc.shape[3]
+            if w[17] >= 0:
+                b = A[w[17]]
+                if w[18] == pg.BIAS_BORDER9:
+                    t0, kh0, kw0, st0, pd0 = w[3:8]
+                    H, Wd = T[t0].shape[2], T[t0].shape[3]
+                    b9 = b.view(3, 3, npad)
+                    ih0 = torch.arange(Ho) * st0 - pd0
+                    iw0 = torch.arange(Wo) * st0 - pd0
+                    rc = torch.where(ih0 < 0, 0, torch.where(ih0 + kh0 - 1 >= H, 2, 1))
+                    cc = torch.where(iw0 < 0, 0, torch.where(iw0 + kw0 - 1 >= Wd, 2, 1))
+                    acc = acc + b9[rc[:, None], cc[None, :]].permute(2, 0, 1)[None]
+                else:
+                    acc = acc + b.view(1, -1, 1, 1)
+            slope = A[w[19]] if w[19] >= 0 else None
+            act = w[20]
+            res = T[w[21]] if w[21] >= 0 else None
+            if res is not None and w[22] == pg.RES_UP2:
+                res = F.interpolate(res, size=(Ho, Wo), mode="nearest")
+            if not w[23]:
+                acc = _act(acc, act, slope)
+            if res is not None:
+                acc = acc + res
+            if w[23]:
+                acc = _act(acc, act, slope)
+            C = out[3]
+            acc = acc[:, :C].clone()
+            acc[:, w[16]:] = 0
+            T[w[1]] = acc
+        elif w[0] == pg.OP_STEM:
+            X = T[w[2]]
+            cout = w[8]
+            wt = A[w[7]].view(cout, 3, 3, 4).permute(0, 3, 1, 2).contiguous()
+            y = F.conv2d(X, wt, stride=w[5], padding=w[6]) + A[w[9]].view(1, -1, 1, 1)
+            y = _act(y, w[11], A[w[10]] if w[10] >= 0 else None)
+            cp = P.tensors[w[1]][3]
+            out = torch.zeros(y.shape[0], cp, y.shape[2], y.shape[3])
+            out[:, :cout] = y
+            T[w[1]] = out
+        elif w[0] == pg.OP_MAXPOOL:
+            T[w[1]] = F.max_pool2d(T[w[2]], w[3], w[4], w[5])
+    return [T[o] for o in P.outputs]

@@ -1,0 +1,122 @@
+"""End-to-end parity of the drop-in FaceEmbedder (device path) against the CPU
+oracle pipeline (oracle/pipeline.py) on synthetic frames.
+
+Two levels:
+* chained (bit-exact where the arithmetic is integer): given the device's own
+  landmarks for a face, the oracle's canonicalisation + LMEDS + warpAffine must
+  reproduce the device chip byte for byte, the oracle quality of that chip must
+  equal the device quality (1e-9 rel), and the oracle ArcFace of those chips
+  must match the device embedding within 1e-4 (f32) / 1e-2 (f16).
+* end to end (independent nets on both sides): same boxes (int32, exact), quality
+  within 1e-3 rel (landmark low bits move a few warped pixels), embeddings and
+  bank distances within 2e-3 / 1e-3 (f32) and 1e-2 / 5e-3 (f16), identical
+  accept/reject decisions at the reference thresholds outside a 5e-3 margin.
+"""
+import numpy as np
+import pytest
+
+from oracle import cv_ops
+from oracle import nets_torch as nt
+from oracle import pipeline as op
+from oracle import ref_algos as ra
+from person_capture_amd import face_embedder as fe_mod
+from person_capture_amd.match import DeviceBank
+
+pytestmark = pytest.mark.gpu
+
+
+def _bank(n=8, seed=3):
+    b = np.random.default_rng(seed).standard_normal((n, 512)).astype(np.float32)
+    return b / np.linalg.norm(b, axis=1, keepdims=True)
+
+
+def _frames():
+    fr = [np.random.default_rng(40 + i).integers(0, 256, (1080, 1920, 3), dtype=np.uint8) for i in range(3)]
+    fr.append(np.random.default_rng(50).integers(0, 256, (480, 640, 3), dtype=np.uint8))
+    return fr
+
+
+@pytest.mark.parametrize("prec,tol_f", [("f32", 1e-4), ("f16", 1e-2)])
+def test_chained_align_quality_embed(gpu_ctx, monkeypatch, prec, tol_f):
+    monkeypatch.setenv("PERSON_CAPTURE_AMD_PRECISION", prec)
+    fe = fe_mod.FaceEmbedder(ctx="cuda:0", yolo_model="scrfd_10g_bnkps", conf=0.5)
+    fe.debug_chips = True
+    frames = _frames()
+    got_all = fe.extract_batch(frames)
+    n = 0
+    for frame, got in zip(frames, got_all):
+        for f in got:
+            x1, y1, x2, y2 = f["bbox"]
+            canon = ra.canon_5pts(f["kps5"])
+            assert canon is not None
+            chip = op.align_chip(frame[y1:y2, x1:x2], canon)
+            assert np.array_equal(chip, f["chip"])
+            q = cv_ops.face_quality(chip)
+            assert abs(q - f["quality"]) <= 1e-9 * max(1.0, q)
+            e = nt.iresnet_forward(fe._arc_params, 100, nt.arcface_input_from_chips(chip[None])).numpy()
+            ef = nt.iresnet_forward(fe._arc_params, 100, nt.arcface_input_from_chips(chip[None, :, ::-1])).numpy()
+            ref = ra.arcface_postprocess(e, ef)[0]
+            assert np.abs(ref - f["feat"]).max() < tol_f
+            n += 1
+    assert n >= 4
+
+
+@pytest.mark.parametrize("prec,tol_f,tol_fd", [("f32", 2e-3, 1e-3), ("f16", 1e-2, 5e-3)])
+def test_face_embedder_end_to_end(gpu_ctx, monkeypatch, prec, tol_f, tol_fd):
+    monkeypatch.setenv("PERSON_CAPTURE_AMD_PRECISION", prec)
+    fe = fe_mod.FaceEmbedder(ctx="cuda:0", yolo_model="scrfd_10g_bnkps", conf=0.5)
+    frames = _frames()
+    bank = _bank()
+    got_all = fe.extract_batch(frames, bank=DeviceBank(fe._ctx, bank))
+    nchecked = 0
+    for frame, got in zip(frames, got_all):
+        ref = op.extract_frame(frame, fe._scrfd_params, fe.scrfd_variant, fe._arc_params, fe._arc_depth, conf=0.5,
+                               D=640, bank=bank)
+        assert ref != op.NEEDS_FALLBACK
+        assert len(got) == len(ref)
+        got_s = sorted(got, key=lambda f: tuple(f["bbox"]))
+        ref_s = sorted(ref, key=lambda f: tuple(f["bbox"]))
+        for a, b in zip(got_s, ref_s):
+            assert np.array_equal(a["bbox"], b["bbox"])
+            assert abs(a["quality"] - b["quality"]) <= 1e-3 * max(1.0, b["quality"])
+            assert np.abs(a["feat"] - b["feat"]).max() < tol_f
+            assert abs(a["fd"] - b["fd"]) < tol_fd
+            for thr in (0.32, 0.45):   # CLI and GUI face_thresh defaults
+                if abs(b["fd"] - thr) > 5e-3:
+                    assert (a["fd"] <= thr) == (b["fd"] <= thr)
+            nchecked += 1
+    assert nchecked >= 4
+
+
+def test_extract_single_matches_batch(gpu_ctx):
+    fe = fe_mod.FaceEmbedder(ctx="cuda:0", yolo_model="scrfd_10g_bnkps", conf=0.5)
+    frames = [np.random.default_rng(60 + i).integers(0, 256, (720, 1280, 3), dtype=np.uint8) for i in range(3)]
+    one = [fe.extract(f) for f in frames]
+    fe2 = fe_mod.FaceEmbedder(ctx="cuda:0", yolo_model="scrfd_10g_bnkps", conf=0.5)
+    many = fe2.extract_batch(frames)
+    for a, b in zip(one, many):
+        assert len(a) == len(b)
+        for x, y in zip(a, b):
+            assert np.array_equal(x["bbox"], y["bbox"])
+            assert np.array_equal(x["feat"], y["feat"])
+    assert fe.best_face(one[0]) is not None
+    assert fe.extract(np.zeros((0, 0, 3), np.uint8)) == []
+    assert fe.extract(None) == []
+    # a non-contiguous slice (the callers pass frame[y1:y2, x1:x2]) works
+    crop = frames[0][100:600, 200:900]
+    assert isinstance(fe.extract(crop), list)
+
+
+def test_fallback_paths_run(gpu_ctx):
+    """A constant frame yields no 0-degree face: the TTA / edge-pad / rotation fallbacks
+    (face_embedder.py:2251-2433) must run on the device and update the no-face streak
+    as the reference's state machine does."""
+    fe = fe_mod.FaceEmbedder(ctx="cuda:0", yolo_model="scrfd_10g_bnkps", conf=0.99)
+    fe.configure_rotation_strategy(adaptive=False)
+    flat = np.full((300, 400, 3), 77, np.uint8)
+    out = fe.extract(flat)
+    assert isinstance(out, list)
+    assert fe._no_face_streak == (0 if out else 1)
+    fe.set_prescan_fast(True)
+    out2 = fe.extract(flat)
+    assert isinstance(out2, list)
