@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string>
 #include <vector>
 #include <map>
@@ -17,7 +18,7 @@
 #include "pc_common.h"
 
 namespace pc {
-hipError_t conv_launch(int f32, int rowb, int bc, int bp, const ConvParams& p, hipStream_t s);
+hipError_t conv_launch(int f32, int rowb, int cfg, const ConvParams& p, hipStream_t s);
 hipError_t splitk_reduce_launch(int f32, const float* part, int splitk, int M, int npad, int cout, const float* bias,
                                 const float* slope, int act, void* y, int ycs, int out_f32, hipStream_t s);
 hipError_t stem_launch(int f32, const StemParams& p, hipStream_t s);
@@ -203,7 +204,7 @@ enum { OP_CONV = 1, OP_STEM = 2, OP_MAXPOOL = 3 };
 struct NetBuf { long long elems; int is_f32; void* d = nullptr; };
 struct NetTensor { int buf, H, W, C, cs, coff, is_f32; };
 struct NetOp { int w[32]; };
-struct ConvPlan { int rowb, bc, bp, splitk; long long M_per_image; double flops_per_image; };
+struct ConvPlan { int rowb, cfg, splitk; long long M_per_image; double flops_per_image; };
 struct ProfRec { int a, b, kind; double flops; };
 
 struct pc_net {
@@ -254,18 +255,32 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl) {
     if ((X.C * esz) % 128) rowb = 64;
     if ((X.C * esz) % 64) return fail(n->ctx, PC_ERR_FORMAT, "conv input channels not a multiple of the K tile");
   }
-  int bc = 0;
-  for (int cand : {128, 96, 64, 32})
-    if (npad % cand == 0) { bc = cand; break; }
-  if (!bc) return fail(n->ctx, PC_ERR_FORMAT, "conv npad must be a multiple of 32");
+  // tile configuration (pc_conv.hip launch_rowb): channel tile BC must divide npad
+  static const int cfg_bc[9] = {128, 128, 64, 64, 96, 32, 32, 128, 256};
+  static const int cfg_bp[9] = {128, 64, 256, 128, 128, 256, 128, 256, 128};
   const NetTensor& Y = n->tens[out];
   const long long Mimg = (long long)Y.H * Y.W;
   const long long M = Mimg * n->max_batch;
-  int bp;
-  if (bc == 128) bp = (M / 128) * (npad / 128) >= 512 ? 128 : 64;
-  else if (bc == 96) bp = 128;
-  else bp = (M / 256) * (npad / bc) >= 512 ? 256 : 128;
-  pl.rowb = rowb; pl.bc = bc; pl.bp = bp; pl.M_per_image = Mimg;
+  auto tiles = [&](int c) { return (M + cfg_bp[c] - 1) / cfg_bp[c] * (npad / cfg_bc[c]); };
+  int cfg = -1;
+  if (npad % 128 == 0) {
+    if (tiles(7) >= 256) cfg = 7;
+    else if (npad % 256 == 0 && tiles(8) >= 256) cfg = 8;
+    else cfg = tiles(0) >= 256 ? 0 : 1;
+  } else if (npad % 96 == 0) {
+    cfg = 4;
+  } else if (npad % 64 == 0) {
+    cfg = tiles(2) >= 512 ? 2 : 3;
+  } else if (npad % 32 == 0) {
+    cfg = tiles(5) >= 512 ? 5 : 6;
+  } else {
+    return fail(n->ctx, PC_ERR_FORMAT, "conv npad must be a multiple of 32");
+  }
+  if (const char* e = getenv("PC_CONV_CFG")) {   // testing / tuning override
+    const int f = atoi(e);
+    if (f >= 0 && f < 9 && npad % cfg_bc[f] == 0) cfg = f;
+  }
+  pl.rowb = rowb; pl.cfg = cfg; pl.M_per_image = Mimg;
   pl.splitk = w[24] > 1 ? w[24] : 1;
   if (Y.C > npad) return fail(n->ctx, PC_ERR_FORMAT, "conv output tensor wider than npad");
   return PC_OK;
@@ -463,7 +478,7 @@ static int run_ops(pc_net* n, int N) {
       p.splitk = pl.splitk;
       p.partial = n->partial;
       p.zero = c->zero;
-      HIPCHK(c, conv_launch(n->f32, pl.rowb, pl.bc, pl.bp, p, s));
+      HIPCHK(c, conv_launch(n->f32, pl.rowb, pl.cfg, p, s));
       if (pl.splitk > 1) {
         HIPCHK(c, splitk_reduce_launch(n->f32, n->partial, pl.splitk, p.M, p.npad, p.cout, p.bias, p.slope, p.act,
                                        p.y, p.ycs, p.out_f32, s));

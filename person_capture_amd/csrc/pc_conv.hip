@@ -72,28 +72,70 @@ __device__ __forceinline__ void load4(const T* src, float* v, int n) {
   for (int j = 0; j < n; ++j) v[j] = (float)src[j];
 }
 
-template <typename T, int BC, int BP, int ROWB>
-__global__ __launch_bounds__(256, 2) void conv_igemm(ConvParams p) {
+// Workgroup order: the dispatcher deals blocks round-robin over the 8 XCDs (b and
+// b+8 share one), so hand each XCD a contiguous range of tiles; with the channel
+// tile fastest, the channel tiles of one pixel tile share its im2col rows in the
+// same L2. Bijective for any grid size (MI355X_MICROARCH.md, T1).
+__device__ __forceinline__ int xcd_remap(int b, int nwg) {
+  const int xcd = b & 7, idx = b >> 3;
+  const int q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+// s_waitcnt vmcnt(n) with n known only at run time but wave-uniform (per-wave DMA count)
+__device__ __forceinline__ void vmcnt_wait(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
+    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+    case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+  }
+}
+
+// BC x BP output tile per workgroup of WC x WP waves; NSTAGE-deep LDS ring of
+// K-tiles filled by LDS-DMA, tile k+NSTAGE-1 issued right after the barrier that
+// retires tile k (counted vmcnt, one raw s_barrier per K-tile, no drain to 0).
+template <typename T, int BC, int BP, int ROWB, int WC, int WP, int NSTAGE>
+__global__ __launch_bounds__(64 * WC * WP, 1) void conv_igemm(ConvParams p) {
+  constexpr int NW = WC * WP;
   constexpr int CHUNKS = ROWB / 16;       // 16-byte chunks per LDS row
-  constexpr int EPC = 16 / sizeof(T);     // elements per chunk
   constexpr int BKE = ROWB / sizeof(T);   // K elements per tile
   constexpr int ROWS = BC + BP;
   constexpr int RPI = 1024 / ROWB;        // LDS rows written by one wave-instruction
   constexpr int NTOT = ROWS / RPI;        // wave-instructions per tile
-  constexpr int NI = (NTOT + 3) / 4;      // per wave
-  constexpr int TC = BC / 32, TP = BP / 32;
+  constexpr int NI = (NTOT + NW - 1) / NW;
+  constexpr int WTC = BC / WC, WTP = BP / WP;
+  constexpr int TC = WTC / 16, TP = WTP / 16;
   constexpr int BUF = ROWS * ROWB;
   static_assert(ROWS % RPI == 0, "tile rows");
-  static_assert(BC % 32 == 0 && BP % 32 == 0, "tile dims");
+  static_assert(WTC % 16 == 0 && WTP % 16 == 0, "wave tile");
+  static_assert(NSTAGE >= 2, "ring depth");
 
-  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  __shared__ __attribute__((aligned(16))) char smem[NSTAGE * BUF];
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int wr = wave >> 1, wc = wave & 1;
-  const int p0 = blockIdx.x * BP;
-  const int c0 = blockIdx.y * BC;
+  const int wr = wave / WP, wc = wave % WP;
+  const int nct = p.npad / BC;
+  const int npt = (p.M + BP - 1) / BP;
+  const int tile = xcd_remap(blockIdx.x, nct * npt);
+  const int p0 = (tile / nct) * BP;
+  const int c0 = (tile % nct) * BC;
   const int z = blockIdx.z;
+  const int myni = NI - ((NTOT % NW) != 0 && wave >= (NTOT % NW) ? 1 : 0);
 
   // ---- split-K range ----
   const int per = (p.kt_total + p.splitk - 1) / p.splitk;
@@ -117,7 +159,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(ConvParams p) {
   int x_oh[NI], x_ow[NI], x_n[NI];
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
-    const int g = i * 4 + wave;
+    const int g = i * NW + wave;
     const int r = g * RPI + lrow;
     x_n[i] = -1; x_oh[i] = 0; x_ow[i] = 0;
     if (g < NTOT && r >= BC) {
@@ -143,7 +185,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(ConvParams p) {
     const char* xb = reinterpret_cast<const char*>(S.x);
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const int g = i * 4 + wave;
+      const int g = i * NW + wave;
       if (g < NTOT) {
         const int r = g * RPI + lrow;
         const int lc = pchunk ^ ((r >> 1) & (CHUNKS - 1));
@@ -186,12 +228,12 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(ConvParams p) {
         const int c = ks * 4 + (lane >> 4);
 #pragma unroll
         for (int t = 0; t < TC; ++t) {
-          const int row = wr * (BC / 2) + t * 16 + (lane & 15);
+          const int row = wr * WTC + t * 16 + (lane & 15);
           fa[t] = *reinterpret_cast<const f16x8*>(base + row * ROWB + ((c ^ ((row >> 1) & (CHUNKS - 1))) << 4));
         }
 #pragma unroll
         for (int t = 0; t < TP; ++t) {
-          const int row = BC + wc * (BP / 2) + t * 16 + (lane & 15);
+          const int row = BC + wc * WTP + t * 16 + (lane & 15);
           fb[t] = *reinterpret_cast<const f16x8*>(base + row * ROWB + ((c ^ ((row >> 1) & (CHUNKS - 1))) << 4));
         }
 #pragma unroll
@@ -208,12 +250,12 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(ConvParams p) {
         const int woff = (lane >> 4) << 2;
 #pragma unroll
         for (int t = 0; t < TC; ++t) {
-          const int row = wr * (BC / 2) + t * 16 + (lane & 15);
+          const int row = wr * WTC + t * 16 + (lane & 15);
           fa[t] = *reinterpret_cast<const float*>(base + row * ROWB + ((ks ^ ((row >> 1) & (CHUNKS - 1))) << 4) + woff);
         }
 #pragma unroll
         for (int t = 0; t < TP; ++t) {
-          const int row = BC + wc * (BP / 2) + t * 16 + (lane & 15);
+          const int row = BC + wc * WTP + t * 16 + (lane & 15);
           fb[t] = *reinterpret_cast<const float*>(base + row * ROWB + ((ks ^ ((row >> 1) & (CHUNKS - 1))) << 4) + woff);
         }
 #pragma unroll
@@ -225,21 +267,26 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(ConvParams p) {
     }
   };
 
-  // ---- main loop: 2-deep LDS ring, DMA of tile k+1 under the MFMAs of tile k ----
+  // ---- main loop: NSTAGE-deep LDS ring ----
   if (nk > 0) {
-    stage(0, kb, seg, tap, cb);
-    advance();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int it = 0; it < nk; ++it) {
-      const int cur = it & 1;
-      if (it + 1 < nk) {
-        stage(cur ^ 1, kb + it + 1, seg, tap, cb);
+#pragma unroll
+    for (int s = 0; s < NSTAGE - 1; ++s) {
+      if (s < nk) {
+        stage(s, kb + s, seg, tap, cb);
         advance();
       }
-      compute(cur);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+    }
+    for (int it = 0; it < nk; ++it) {
+      const int ahead = min(NSTAGE - 2, nk - 1 - it);   // tiles issued after tile `it`
+      vmcnt_wait(ahead * myni);
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (it + NSTAGE - 1 < nk) {
+        stage((it + NSTAGE - 1) % NSTAGE, kb + it + NSTAGE - 1, seg, tap, cb);
+        advance();
+      }
+      compute(it % NSTAGE);
     }
   }
 
@@ -247,12 +294,12 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(ConvParams p) {
   const int chq = (lane >> 4) * 4;
 #pragma unroll
   for (int b = 0; b < TP; ++b) {
-    const int pix = p0 + wc * (BP / 2) + b * 16 + (lane & 15);
+    const int pix = p0 + wc * WTP + b * 16 + (lane & 15);
     if (pix >= p.M) continue;
     if (p.splitk > 1) {
 #pragma unroll
       for (int a = 0; a < TC; ++a) {
-        const int ch = c0 + wr * (BC / 2) + a * 16 + chq;
+        const int ch = c0 + wr * WTC + a * 16 + chq;
         float* dst = p.partial + ((long long)z * p.M + pix) * p.npad + ch;
         *reinterpret_cast<f32x4*>(dst) = acc[a][b];
       }
@@ -280,7 +327,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(ConvParams p) {
     if (p.res_mode == RES_UP2) rpix = ((long long)n * p.rH + (oh >> 1)) * p.rW + (ow >> 1);
 #pragma unroll
     for (int a = 0; a < TC; ++a) {
-      const int ch = c0 + wr * (BC / 2) + a * 16 + chq;
+      const int ch = c0 + wr * WTC + a * 16 + chq;
       if (ch >= p.cwrite) continue;
       const int nv = min(4, p.cwrite - ch);
       float v[4] = {acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]};
@@ -413,28 +460,37 @@ __global__ void maxpool_nhwc(PoolParams p) {
 // ---------------------------------------------------------------------------
 // host-side launchers
 // ---------------------------------------------------------------------------
-template <typename T, int BC, int BP, int ROWB>
+template <typename T, int BC, int BP, int ROWB, int WC, int WP, int NS>
 static hipError_t launch_cfg(const ConvParams& p, hipStream_t s) {
-  dim3 grid((p.M + BP - 1) / BP, p.npad / BC, p.splitk);
-  hipLaunchKernelGGL((conv_igemm<T, BC, BP, ROWB>), grid, dim3(256), 0, s, p);
+  const int nwg = (p.M + BP - 1) / BP * (p.npad / BC);
+  dim3 grid(nwg, 1, p.splitk);
+  hipLaunchKernelGGL((conv_igemm<T, BC, BP, ROWB, WC, WP, NS>), grid, dim3(64 * WC * WP), 0, s, p);
   return hipGetLastError();
 }
 
+// tile configurations (cfg ids are chosen on the host, pc_api.cpp plan_conv):
+//   0: 128x128, 4 waves, 2-stage     1: 128x64, 4 waves, 2-stage    2: 64x256, 4 waves, 2-stage
+//   3: 64x128, 4 waves, 2-stage      4: 96x128, 4 waves, 2-stage    5: 32x256, 4 waves, 2-stage
+//   6: 32x128, 4 waves, 2-stage      7: 128x256, 8 waves, 3-stage   8: 256x128, 8 waves, 3-stage
 template <typename T, int ROWB>
-static hipError_t launch_rowb(const ConvParams& p, int bc, int bp, hipStream_t s) {
-  if (bc == 128 && bp == 128) return launch_cfg<T, 128, 128, ROWB>(p, s);
-  if (bc == 128 && bp == 64) return launch_cfg<T, 128, 64, ROWB>(p, s);
-  if (bc == 64 && bp == 256) return launch_cfg<T, 64, 256, ROWB>(p, s);
-  if (bc == 64 && bp == 128) return launch_cfg<T, 64, 128, ROWB>(p, s);
-  if (bc == 96 && bp == 128) return launch_cfg<T, 96, 128, ROWB>(p, s);
-  if (bc == 32 && bp == 256) return launch_cfg<T, 32, 256, ROWB>(p, s);
-  if (bc == 32 && bp == 128) return launch_cfg<T, 32, 128, ROWB>(p, s);
-  return hipErrorInvalidValue;
+static hipError_t launch_rowb(const ConvParams& p, int cfg, hipStream_t s) {
+  switch (cfg) {
+    case 0: return launch_cfg<T, 128, 128, ROWB, 2, 2, 2>(p, s);
+    case 1: return launch_cfg<T, 128, 64, ROWB, 2, 2, 2>(p, s);
+    case 2: return launch_cfg<T, 64, 256, ROWB, 2, 2, 2>(p, s);
+    case 3: return launch_cfg<T, 64, 128, ROWB, 2, 2, 2>(p, s);
+    case 4: return launch_cfg<T, 96, 128, ROWB, 2, 2, 2>(p, s);
+    case 5: return launch_cfg<T, 32, 256, ROWB, 2, 2, 2>(p, s);
+    case 6: return launch_cfg<T, 32, 128, ROWB, 2, 2, 2>(p, s);
+    case 7: return launch_cfg<T, 128, 256, ROWB, 2, 4, 3>(p, s);
+    case 8: return launch_cfg<T, 256, 128, ROWB, 4, 2, 3>(p, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 
-hipError_t conv_launch(int f32, int rowb, int bc, int bp, const ConvParams& p, hipStream_t s) {
-  if (f32) return rowb == 128 ? launch_rowb<float, 128>(p, bc, bp, s) : launch_rowb<float, 64>(p, bc, bp, s);
-  return rowb == 128 ? launch_rowb<f16, 128>(p, bc, bp, s) : launch_rowb<f16, 64>(p, bc, bp, s);
+hipError_t conv_launch(int f32, int rowb, int cfg, const ConvParams& p, hipStream_t s) {
+  if (f32) return rowb == 128 ? launch_rowb<float, 128>(p, cfg, s) : launch_rowb<float, 64>(p, cfg, s);
+  return rowb == 128 ? launch_rowb<f16, 128>(p, cfg, s) : launch_rowb<f16, 64>(p, cfg, s);
 }
 
 hipError_t splitk_reduce_launch(int f32, const float* part, int splitk, int M, int npad, int cout,

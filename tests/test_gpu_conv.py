@@ -58,9 +58,14 @@ CASES = [
 ]
 
 
+@pytest.mark.parametrize("cfg", [None, "0", "7", "8", "2", "5"])
 @pytest.mark.parametrize("prec", [PC_PREC_F32, PC_PREC_F16])
 @pytest.mark.parametrize("case", CASES)
-def test_single_conv(gpu_ctx, prec, case):
+def test_single_conv(gpu_ctx, monkeypatch, prec, case, cfg):
+    """Every tile configuration of pc_conv.hip (PC_CONV_CFG forces one where the
+    channel tile divides npad; otherwise the planner's choice runs)."""
+    if cfg is not None:
+        monkeypatch.setenv("PC_CONV_CFG", cfg)
     H, cin, cout, k, s, act, bmode, out_f32 = case
     rng = np.random.default_rng(hash(case) & 0xFFFF)
     N = 3
@@ -101,8 +106,11 @@ def test_single_conv(gpu_ctx, prec, case):
     assert np.all(got[..., cout:] == 0), "channel padding must be zero"
 
 
+@pytest.mark.parametrize("cfg", [None, "0", "7", "8"])
 @pytest.mark.parametrize("prec", [PC_PREC_F32, PC_PREC_F16])
-def test_two_segments_residual_upsample_splitk(gpu_ctx, prec):
+def test_two_segments_residual_upsample_splitk(gpu_ctx, monkeypatch, prec, cfg):
+    if cfg is not None:
+        monkeypatch.setenv("PC_CONV_CFG", cfg)
     """op1: conv3x3/s2 on x -> r (14x14); op2: conv3x3 on r + 1x1/s2 on x (2 segments), + up2(q) residual;
     op3: 7x7 valid split-K conv on op2 -> f32; op4: 1x1 conv with same-pixel residual, act after res."""
     rng = np.random.default_rng(7)

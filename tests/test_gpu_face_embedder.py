@@ -8,7 +8,7 @@ Two levels:
   equal the device quality (1e-9 rel), and the oracle ArcFace of those chips
   must match the device embedding within 1e-4 (f32) / 1e-2 (f16).
 * end to end (independent nets on both sides): same boxes (int32, exact), quality
-  within 1e-3 rel (landmark low bits move a few warped pixels), embeddings and
+  within 1e-3 rel (f32; 5e-2 f16 — landmark low bits move warped pixels), embeddings and
   bank distances within 2e-3 / 1e-3 (f32) and 1e-2 / 5e-3 (f16), identical
   accept/reject decisions at the reference thresholds outside a 5e-3 margin.
 """
@@ -61,8 +61,8 @@ def test_chained_align_quality_embed(gpu_ctx, monkeypatch, prec, tol_f):
     assert n >= 4
 
 
-@pytest.mark.parametrize("prec,tol_f,tol_fd", [("f32", 2e-3, 1e-3), ("f16", 1e-2, 5e-3)])
-def test_face_embedder_end_to_end(gpu_ctx, monkeypatch, prec, tol_f, tol_fd):
+@pytest.mark.parametrize("prec,tol_q,tol_f,tol_fd", [("f32", 1e-3, 2e-3, 1e-3), ("f16", 5e-2, 1e-2, 5e-3)])
+def test_face_embedder_end_to_end(gpu_ctx, monkeypatch, prec, tol_q, tol_f, tol_fd):
     monkeypatch.setenv("PERSON_CAPTURE_AMD_PRECISION", prec)
     fe = fe_mod.FaceEmbedder(ctx="cuda:0", yolo_model="scrfd_10g_bnkps", conf=0.5)
     frames = _frames()
@@ -78,7 +78,7 @@ def test_face_embedder_end_to_end(gpu_ctx, monkeypatch, prec, tol_f, tol_fd):
         ref_s = sorted(ref, key=lambda f: tuple(f["bbox"]))
         for a, b in zip(got_s, ref_s):
             assert np.array_equal(a["bbox"], b["bbox"])
-            assert abs(a["quality"] - b["quality"]) <= 1e-3 * max(1.0, b["quality"])
+            assert abs(a["quality"] - b["quality"]) <= tol_q * max(1.0, b["quality"])
             assert np.abs(a["feat"] - b["feat"]).max() < tol_f
             assert abs(a["fd"] - b["fd"]) < tol_fd
             for thr in (0.32, 0.45):   # CLI and GUI face_thresh defaults

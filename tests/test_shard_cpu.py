@@ -1,0 +1,69 @@
+"""Multi-process (gloo, world_size 2, CPU) coverage of the frame-shard runner:
+round-robin assignment and frame-ordered gather on rank 0; and the bench's
+max-over-ranks timing reduction."""
+import os
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+from person_capture_amd.shard import FrameShardRunner, merge_in_order, shard_indices
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    frames = [f"frame{i}" for i in range(n)]
+    seen = []
+
+    def extract(fr):
+        seen.extend(fr)
+        return [{"frame": f, "rank": rank} for f in fr]
+
+    out = FrameShardRunner(extract).process(frames)
+    t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    q.put((rank, seen, out, float(t.item())))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n", [0, 1, 7, 8])
+def test_frame_shard_gloo_world2(n):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, n, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        r, seen, out, mx = q.get(timeout=120)
+        res[r] = (seen, out, mx)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][0] == [f"frame{i}" for i in range(0, n, 2)]
+    assert res[1][0] == [f"frame{i}" for i in range(1, n, 2)]
+    assert res[1][1] is None
+    assert [d["frame"] for d in res[0][1]] == [f"frame{i}" for i in range(n)]
+    assert all(d["rank"] == i % 2 for i, d in enumerate(res[0][1]))
+    assert res[0][2] == res[1][2] == 2.0
+
+
+def test_shard_helpers():
+    for n in range(0, 20):
+        for w in (1, 2, 3, 8):
+            parts = [shard_indices(n, r, w) for r in range(w)]
+            assert sorted(i for p in parts for i in p) == list(range(n))
+            assert merge_in_order(n, w, parts) == list(range(n))

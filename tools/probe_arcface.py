@@ -8,6 +8,8 @@ from person_capture_amd.runtime import GpuContext, Net
 from person_capture_amd._lib import PC_PREC_F16
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+import os
+if len(sys.argv) > 2: os.environ['PC_CONV_CFG'] = sys.argv[2]
 ctx = GpuContext(0)
 p = models.synth_iresnet(100, seed=0)
 P = models.compile_iresnet(p, 100)
@@ -25,4 +27,4 @@ for _ in range(n):
 ctx.sync()
 dt = (time.perf_counter() - t) / n
 fl = net.flops_per_image * B
-print(f"batch {B}: {dt*1e3:.3f} ms/batch  {B/dt:.0f} fwd/s  {fl/dt/1e12:.1f} TFLOP/s  ({fl/dt/2.5e15*100:.1f}% of 2.5 PF)")
+print(f"cfg {os.environ.get('PC_CONV_CFG','auto')} batch {B}: {dt*1e3:.3f} ms/batch  {B/dt:.0f} fwd/s  {fl/dt/1e12:.1f} TFLOP/s  ({fl/dt/2.5e15*100:.1f}% of 2.5 PF)")

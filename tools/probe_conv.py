@@ -1,0 +1,64 @@
+"""Single-conv microbenchmark of the implicit-GEMM engine (HIP-event timed).
+usage: python tools/probe_conv.py [cfg ...]"""
+import os
+import sys
+
+sys.dont_write_bytecode = True
+sys.path.insert(0, __file__.rsplit('/tools/', 1)[0])
+import numpy as np
+
+from person_capture_amd import program as pg
+from person_capture_amd._lib import PC_PREC_F16
+from person_capture_amd.runtime import GpuContext, Net
+
+SHAPES = [
+    # name, N, H, cin, cout, k, stride
+    ("s3_3x3_256", 256, 14, 256, 256, 3, 1),
+    ("gemm_1x1_2304", 256, 14, 2304, 256, 1, 1),
+    ("s2_3x3_128", 256, 28, 128, 128, 3, 1),
+    ("s1_3x3_64", 256, 56, 64, 64, 3, 1),
+    ("s4_3x3_512", 256, 7, 512, 512, 3, 1),
+]
+
+
+def build(N, H, cin, cout, k, s):
+    P = pg.Program()
+    x = P.input_tensor(H, H, cin)
+    Ho = (H + 2 * (k // 2) - k) // s + 1
+    y = P.act(Ho, Ho, cout)
+    rng = np.random.default_rng(0)
+    w = rng.standard_normal((cout, cin, k, k)) * np.sqrt(2.0 / (cin * k * k))
+    P.conv(y, [(x, k, k, s, k // 2, cin)], pg.pack_conv_weights([w], [cin], cout), cout,
+           bias=np.zeros(cout), act=pg.ACT_RELU)
+    P.outputs = [y]
+    return P
+
+
+def main():
+    cfgs = sys.argv[1:] or ["auto"]
+    ctx = GpuContext(0)
+    for name, N, H, cin, cout, k, s in SHAPES:
+        P = build(N, H, cin, cout, k, s)
+        x = np.random.default_rng(1).standard_normal((N, H, H, cin)).astype(np.float16)
+        d = ctx.upload(x)
+        for c in cfgs:
+            if c == "auto":
+                os.environ.pop("PC_CONV_CFG", None)
+            else:
+                os.environ["PC_CONV_CFG"] = c
+            net = Net(ctx, P.serialize(), PC_PREC_F16, max_batch=N)
+            for _ in range(3):
+                net.run(d.ptr, N)
+            net.profile(True)
+            for _ in range(10):
+                net.run(d.ptr, N)
+            r = net.profile_read()
+            net.profile(False)
+            us = r["conv_ms"] * 1e3 / r["conv_launches"]
+            tf = r["conv_flops"] / (r["conv_ms"] * 1e-3) / 1e12
+            print(f"{name:16s} cfg {c:4s} {us:9.1f} us/launch  {tf:7.1f} TFLOP/s", flush=True)
+            net.close()
+
+
+if __name__ == "__main__":
+    main()
