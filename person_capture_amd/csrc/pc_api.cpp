@@ -224,6 +224,10 @@ struct pc_net {
   double flops_per_image = 0.0;
   int launches = 0;
   const void* cur_input = nullptr;
+  // when a conv reads the net input directly, the input is first copied here so the
+  // implicit-GEMM loader finds a zero tail behind it (ConvSeg::zero_off)
+  void* in_copy = nullptr;
+  size_t in_img_bytes = 0;
   // graph replay
   int use_graph = 0;
   // per-op HIP-event profiling (pc_net_profile)
@@ -241,8 +245,24 @@ static inline int esize(const pc_net* n, int is_f32) { return (is_f32 || n->f32)
 
 static void* tensor_ptr(pc_net* n, int t) {
   const NetTensor& T = n->tens[t];
-  if (T.buf < 0) return (void*)((const char*)n->cur_input + (size_t)T.coff * esize(n, T.is_f32));
+  if (T.buf < 0) {
+    const char* base = n->in_copy ? (const char*)n->in_copy : (const char*)n->cur_input;
+    return (void*)(base + (size_t)T.coff * esize(n, T.is_f32));
+  }
   return (char*)n->bufs[T.buf].d + (size_t)T.coff * esize(n, T.is_f32);
+}
+
+// Every activation buffer is followed by kZeroTail zero bytes: a padding tap of the
+// implicit-GEMM loader reads one K-tile row (any channel block of the pixel stride)
+// from there, so the tail covers the widest pixel row a conv reads.
+static const size_t kZeroTail = 16384;
+
+// bytes from a tensor's base to the zero tail of the buffer that holds it
+static unsigned tensor_zero_off(const pc_net* n, int t) {
+  const NetTensor& T = n->tens[t];
+  const int es = esize(n, T.is_f32);
+  const size_t end = T.buf < 0 ? n->in_img_bytes * n->max_batch : (size_t)n->bufs[T.buf].elems * n->max_batch * es;
+  return (unsigned)(end - (size_t)T.coff * es);
 }
 
 static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl) {
@@ -254,6 +274,7 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl) {
     const NetTensor& X = n->tens[w[3 + 5 * s]];
     if ((X.C * esz) % 128) rowb = 64;
     if ((X.C * esz) % 64) return fail(n->ctx, PC_ERR_FORMAT, "conv input channels not a multiple of the K tile");
+    if ((size_t)X.C * esz + 128 > kZeroTail) return fail(n->ctx, PC_ERR_FORMAT, "conv input wider than the zero tail");
   }
   // tile configuration (pc_conv.hip launch_rowb): channel tile BC must divide npad
   static const int cfg_bc[9] = {128, 128, 64, 64, 96, 32, 32, 128, 256};
@@ -354,9 +375,26 @@ extern "C" int pc_net_create(pc_ctx* c, const void* prog, size_t nbytes, int pre
   }
   for (size_t i = 0; i < n->bufs.size() && rc == PC_OK; ++i) {
     NetBuf& b = n->bufs[i];
-    const size_t bytes = (size_t)b.elems * max_batch * ((b.is_f32 || n->f32) ? 4 : 2) + 256;
-    if (hipMalloc(&b.d, bytes) != hipSuccess) rc = fail(c, PC_ERR_HIP, "activation buffer allocation failed");
-    else hipMemset(b.d, 0, bytes);  // channel padding lanes must read as zero
+    const size_t bytes = (size_t)b.elems * max_batch * ((b.is_f32 || n->f32) ? 4 : 2) + kZeroTail;
+    // the conv loader addresses activations with 32-bit offsets
+    if (bytes >= (1ull << 32)) rc = fail(c, PC_ERR_ARG, "activation buffer exceeds 4 GiB; lower max_batch");
+    else if (hipMalloc(&b.d, bytes) != hipSuccess) rc = fail(c, PC_ERR_HIP, "activation buffer allocation failed");
+    else hipMemset(b.d, 0, bytes);  // channel padding lanes and the zero tail must read as zero
+  }
+  if (rc == PC_OK && n->in_tensor >= 0 && n->in_tensor < (int)n->tens.size()) {
+    const NetTensor& I = n->tens[n->in_tensor];
+    n->in_img_bytes = (size_t)I.H * I.W * I.cs * esize(n, I.is_f32);
+    bool conv_reads_input = false;
+    for (auto& op : n->ops)
+      if (op.w[0] == OP_CONV)
+        for (int s = 0; s < op.w[2]; ++s)
+          if (n->tens[op.w[3 + 5 * s]].buf < 0) conv_reads_input = true;
+    if (conv_reads_input) {
+      const size_t bytes = n->in_img_bytes * max_batch + kZeroTail;
+      if (bytes >= (1ull << 32)) rc = fail(c, PC_ERR_ARG, "input buffer exceeds 4 GiB; lower max_batch");
+      else if (hipMalloc(&n->in_copy, bytes) != hipSuccess) rc = fail(c, PC_ERR_HIP, "input copy allocation failed");
+      else hipMemset(n->in_copy, 0, bytes);
+    }
   }
   // plans + split-K workspace + stats
   n->plans.resize(n->ops.size());
@@ -413,6 +451,7 @@ extern "C" int pc_net_destroy(pc_net* n) {
   for (auto& b : n->bufs) if (b.d) hipFree(b.d);
   if (n->partial) hipFree(n->partial);
   if (n->prep) hipFree(n->prep);
+  if (n->in_copy) hipFree(n->in_copy);
   delete n;
   return PC_OK;
 }
@@ -432,6 +471,8 @@ static int run_ops(pc_net* n, int N) {
   pc_ctx* c = n->ctx;
   hipStream_t s = c->stream;
   const bool prof = n->prof && !n->use_graph;
+  if (n->in_copy)
+    HIPCHK(c, hipMemcpyAsync(n->in_copy, n->cur_input, n->in_img_bytes * N, hipMemcpyDeviceToDevice, s));
   for (size_t i = 0; i < n->ops.size(); ++i) {
     const int* w = n->ops[i].w;
     ProfRec rec{-1, -1, w[0], w[0] == OP_CONV ? n->plans[i].flops_per_image * N : 0.0};
@@ -448,6 +489,7 @@ static int run_ops(pc_net* n, int N) {
         const NetTensor& X = n->tens[w[3 + 5 * sg]];
         ConvSeg& S = p.seg[sg];
         S.x = tensor_ptr(n, w[3 + 5 * sg]);
+        S.zero_off = tensor_zero_off(n, w[3 + 5 * sg]);
         S.H = X.H; S.W = X.W; S.C = X.C; S.cs = X.cs;
         S.KH = w[4 + 5 * sg]; S.KW = w[5 + 5 * sg]; S.stride = w[6 + 5 * sg]; S.pad = w[7 + 5 * sg];
         S.cblk = X.C / bke;

@@ -25,6 +25,7 @@ struct ConvSeg {
   int KH, KW, stride, pad;
   int kt;              // K tiles in this segment = KH*KW*(C/BKE)
   int cblk;            // C / BKE
+  unsigned zero_off;   // bytes from x to >= 256 zero bytes (padding taps read there)
 };
 
 struct ConvParams {

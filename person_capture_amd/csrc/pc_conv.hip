@@ -22,6 +22,7 @@
 // A second, optional K-segment lets a residual block's shortcut projection
 // (IResNet downsample 1x1/s2, ResNetV1e avg-down == 2x2/s2 conv) accumulate into
 // the same tile, so shortcut + main branch cost one launch and one output write.
+#include <type_traits>
 #include "pc_common.h"
 
 namespace pc {
@@ -127,7 +128,7 @@ __global__ __launch_bounds__(64 * WC * WP, 1) void conv_igemm(ConvParams p) {
   __shared__ __attribute__((aligned(16))) char smem[NSTAGE * BUF];
 
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform (SGPR)
   const int wr = wave / WP, wc = wave % WP;
   const int nct = p.npad / BC;
   const int npt = (p.M + BP - 1) / BP;
@@ -143,26 +144,46 @@ __global__ __launch_bounds__(64 * WC * WP, 1) void conv_igemm(ConvParams p) {
   const int ke = min(p.kt_total, kb + per);
   const int nk = ke > kb ? ke - kb : 0;
 
-  // ---- K iterator state: (segment, tap, channel block) ----
-  int seg = 0, tap = 0, cb = 0;
+  // ---- K iterator: (segment, tap row th, tap col tw, channel block cb), all scalar ----
+  int seg = 0, th = 0, tw = 0, cb = 0;
   {
     int rem = kb;
     if (p.nseg > 1 && rem >= p.seg[0].kt) { rem -= p.seg[0].kt; seg = 1; }
     const int cbl = p.seg[seg].cblk;
-    tap = rem / cbl;
+    const int tap = rem / cbl;
     cb = rem - tap * cbl;
+    th = tap / p.seg[seg].KW;
+    tw = tap - th * p.seg[seg].KW;
   }
+  // current segment, cached in scalars
+  const char* sx = reinterpret_cast<const char*>(p.seg[seg].x);
+  int sH = p.seg[seg].H, sW = p.seg[seg].W, scs = p.seg[seg].cs;
+  int sKH = p.seg[seg].KH, sKW = p.seg[seg].KW, sstr = p.seg[seg].stride, spad = p.seg[seg].pad;
+  int scblk = p.seg[seg].cblk;
+  unsigned szero = p.seg[seg].zero_off;
 
   // ---- per-lane staging geometry ----
+  // Every staged 16-byte chunk is addressed as (wave-uniform SGPR base) + (per-lane
+  // 32-bit offset). The per-row offset of the current tap (`xcur`) is recomputed only
+  // when the tap changes; the channel block rides in the scalar base. A tap that
+  // falls in the zero padding points at the zero tail the executor keeps behind
+  // every activation buffer (ConvSeg::zero_off), which is wider than any pixel row.
+  constexpr int ESZ = sizeof(T);
   const int lrow = lane / CHUNKS;
   const int pchunk = lane % CHUNKS;
-  int x_oh[NI], x_ow[NI], x_n[NI];
+  int x_ih[NI], x_iw[NI], x_n[NI];  // window origin of this lane's output pixel (current segment)
+  unsigned woff[NI], xpix[NI], zlane[NI], xcur[NI];
+  int x_oh[NI], x_ow[NI];
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
     const int g = i * NW + wave;
     const int r = g * RPI + lrow;
-    x_n[i] = -1; x_oh[i] = 0; x_ow[i] = 0;
-    if (g < NTOT && r >= BC) {
+    const int lc = pchunk ^ ((r >> 1) & (CHUNKS - 1));
+    x_n[i] = -1; x_oh[i] = 0; x_ow[i] = 0; x_ih[i] = 0; x_iw[i] = 0;
+    woff[i] = 0; xpix[i] = 0; zlane[i] = 0; xcur[i] = 0;
+    if (g < NTOT && g * RPI < BC) {
+      woff[i] = (unsigned)((long long)(c0 + r) * p.ktot * ESZ) + lc * 16;
+    } else if (g < NTOT) {
       const int pix = p0 + (r - BC);
       if (pix < p.M) {
         const int hw = p.OH * p.OW;
@@ -174,42 +195,67 @@ __global__ __launch_bounds__(64 * WC * WP, 1) void conv_igemm(ConvParams p) {
       }
     }
   }
+  auto prep_seg = [&]() __attribute__((always_inline)) {   // per-lane window origins for the current segment
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int g = i * NW + wave;
+      if (g < NTOT && g * RPI >= BC) {
+        const int r = g * RPI + lrow;
+        const int lc = pchunk ^ ((r >> 1) & (CHUNKS - 1));
+        zlane[i] = szero + lc * 16;
+        x_ih[i] = x_oh[i] * sstr - spad;
+        x_iw[i] = x_ow[i] * sstr - spad;
+        xpix[i] = (unsigned)((((long long)max(x_n[i], 0) * sH + x_ih[i]) * sW + x_iw[i]) * scs * ESZ) + lc * 16;
+      }
+    }
+  };
+  auto prep_tap = [&]() __attribute__((always_inline)) {   // per-lane source offsets for tap (th, tw)
+    const unsigned tapoff = (unsigned)((th * sW + tw) * scs * ESZ);
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int g = i * NW + wave;
+      if (g < NTOT && g * RPI >= BC) {
+        const bool ok = x_n[i] >= 0 && (unsigned)(x_ih[i] + th) < (unsigned)sH &&
+                        (unsigned)(x_iw[i] + tw) < (unsigned)sW;
+        xcur[i] = ok ? xpix[i] + tapoff : zlane[i];
+      }
+    }
+  };
+  prep_seg();
+  prep_tap();
 
-  const char* wbase = reinterpret_cast<const char*>(p.w);
-  const char* zero = reinterpret_cast<const char*>(p.zero);
-
-  auto stage = [&](int buf, int ktl, int sg, int tp_, int cb_) {
-    const ConvSeg& S = p.seg[sg];
-    const int th = tp_ / S.KW;
-    const int tw = tp_ - th * S.KW;
-    const char* xb = reinterpret_cast<const char*>(S.x);
+  auto stage = [&](auto bufc, int ktl) __attribute__((always_inline)) {
+    constexpr int buf = decltype(bufc)::value;
+    const char* xb = sx + cb * (BKE * ESZ);
+    const char* wb = reinterpret_cast<const char*>(p.w) + (long long)ktl * (BKE * ESZ);
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const int g = i * NW + wave;
       if (g < NTOT) {
-        const int r = g * RPI + lrow;
-        const int lc = pchunk ^ ((r >> 1) & (CHUNKS - 1));
-        const char* src;
-        if (g * RPI < BC) {  // weight row (wave-uniform branch)
-          const long long n = c0 + r;
-          src = wbase + ((n * p.ktot + (long long)ktl * BKE) * sizeof(T)) + lc * 16;
-        } else {
-          const int ih = x_oh[i] * S.stride - S.pad + th;
-          const int iw = x_ow[i] * S.stride - S.pad + tw;
-          const bool ok = x_n[i] >= 0 && (unsigned)ih < (unsigned)S.H && (unsigned)iw < (unsigned)S.W;
-          const long long pixoff = ((long long)x_n[i] * S.H + ih) * S.W + iw;
-          src = ok ? xb + ((pixoff * S.cs + (long long)cb_ * BKE) * sizeof(T)) + lc * 16 : zero + lc * 16;
-        }
+        unsigned off = g * RPI < BC ? woff[i] : xcur[i];
+        asm volatile("" : "+v"(off));   // keep the 32-bit offset in-block (SGPR base + VGPR offset form)
+        const char* src = (g * RPI < BC ? wb : xb) + off;
         char* dst = smem + buf * BUF + g * 1024;
         __builtin_amdgcn_global_load_lds((gptr_t)src, (lds_ptr_t)dst, 16, 0, 0);
       }
     }
   };
-  auto advance = [&]() {
-    if (++cb == p.seg[seg].cblk) {
-      cb = 0;
-      if (++tap == p.seg[seg].KH * p.seg[seg].KW) { tap = 0; ++seg; }
+  auto advance = [&]() __attribute__((always_inline)) {
+    if (++cb < scblk) return;
+    cb = 0;
+    if (++tw == sKW) {
+      tw = 0;
+      if (++th == sKH) {
+        th = 0;
+        if (++seg >= p.nseg) return;
+        sx = reinterpret_cast<const char*>(p.seg[seg].x);
+        sH = p.seg[seg].H; sW = p.seg[seg].W; scs = p.seg[seg].cs;
+        sKH = p.seg[seg].KH; sKW = p.seg[seg].KW; sstr = p.seg[seg].stride; spad = p.seg[seg].pad;
+        scblk = p.seg[seg].cblk; szero = p.seg[seg].zero_off;
+        prep_seg();
+      }
     }
+    prep_tap();
   };
 
   f32x4 acc[TC][TP];
@@ -218,46 +264,45 @@ __global__ __launch_bounds__(64 * WC * WP, 1) void conv_igemm(ConvParams p) {
 #pragma unroll
     for (int b = 0; b < TP; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto compute = [&](int buf) {
+  // fragment read addresses: row = tile base (multiple of 16) + (lane & 15), so the
+  // swizzle term ((row >> 1) & (CHUNKS-1)) depends on the lane only; every ds_read is
+  // one per-lane base + a compile-time immediate.
+  constexpr int KSTEPS = sizeof(T) == 2 ? BKE / 32 : BKE / 4;
+  const int fr = lane & 15;
+  const int sw = (fr >> 1) & (CHUNKS - 1);
+  unsigned koff[KSTEPS];
+#pragma unroll
+  for (int ks = 0; ks < KSTEPS; ++ks) {
+    if constexpr (sizeof(T) == 2) koff[ks] = ((ks * 4 + (lane >> 4)) ^ sw) << 4;
+    else koff[ks] = ((ks ^ sw) << 4) + ((lane >> 4) << 2);
+  }
+  const unsigned a_row = (wr * WTC + fr) * ROWB;
+  const unsigned b_row = (BC + wc * WTP + fr) * ROWB;
+
+  auto compute = [&](auto bufc) __attribute__((always_inline)) {
+    constexpr int buf = decltype(bufc)::value;
     const char* base = smem + buf * BUF;
-    if constexpr (sizeof(T) == 2) {
-      constexpr int KSTEPS = BKE / 32;
 #pragma unroll
-      for (int ks = 0; ks < KSTEPS; ++ks) {
+    for (int ks = 0; ks < KSTEPS; ++ks) {
+      const char* pa = base + a_row + koff[ks];
+      const char* pb = base + b_row + koff[ks];
+      if constexpr (sizeof(T) == 2) {
         f16x8 fa[TC], fb[TP];
-        const int c = ks * 4 + (lane >> 4);
 #pragma unroll
-        for (int t = 0; t < TC; ++t) {
-          const int row = wr * WTC + t * 16 + (lane & 15);
-          fa[t] = *reinterpret_cast<const f16x8*>(base + row * ROWB + ((c ^ ((row >> 1) & (CHUNKS - 1))) << 4));
-        }
+        for (int t = 0; t < TC; ++t) fa[t] = *reinterpret_cast<const f16x8*>(pa + t * 16 * ROWB);
 #pragma unroll
-        for (int t = 0; t < TP; ++t) {
-          const int row = BC + wc * WTP + t * 16 + (lane & 15);
-          fb[t] = *reinterpret_cast<const f16x8*>(base + row * ROWB + ((c ^ ((row >> 1) & (CHUNKS - 1))) << 4));
-        }
+        for (int t = 0; t < TP; ++t) fb[t] = *reinterpret_cast<const f16x8*>(pb + t * 16 * ROWB);
 #pragma unroll
         for (int a = 0; a < TC; ++a)
 #pragma unroll
           for (int b = 0; b < TP; ++b)
             acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[a], fb[b], acc[a][b], 0, 0, 0);
-      }
-    } else {
-      constexpr int KSTEPS = BKE / 4;
-#pragma unroll
-      for (int ks = 0; ks < KSTEPS; ++ks) {
+      } else {
         float fa[TC], fb[TP];
-        const int woff = (lane >> 4) << 2;
 #pragma unroll
-        for (int t = 0; t < TC; ++t) {
-          const int row = wr * WTC + t * 16 + (lane & 15);
-          fa[t] = *reinterpret_cast<const float*>(base + row * ROWB + ((ks ^ ((row >> 1) & (CHUNKS - 1))) << 4) + woff);
-        }
+        for (int t = 0; t < TC; ++t) fa[t] = *reinterpret_cast<const float*>(pa + t * 16 * ROWB);
 #pragma unroll
-        for (int t = 0; t < TP; ++t) {
-          const int row = BC + wc * WTP + t * 16 + (lane & 15);
-          fb[t] = *reinterpret_cast<const float*>(base + row * ROWB + ((ks ^ ((row >> 1) & (CHUNKS - 1))) << 4) + woff);
-        }
+        for (int t = 0; t < TP; ++t) fb[t] = *reinterpret_cast<const float*>(pb + t * 16 * ROWB);
 #pragma unroll
         for (int a = 0; a < TC; ++a)
 #pragma unroll
@@ -267,26 +312,38 @@ __global__ __launch_bounds__(64 * WC * WP, 1) void conv_igemm(ConvParams p) {
     }
   };
 
-  // ---- main loop: NSTAGE-deep LDS ring ----
+  // ---- main loop: NSTAGE-deep LDS ring, unrolled by NSTAGE so every LDS address is static ----
   if (nk > 0) {
-#pragma unroll
-    for (int s = 0; s < NSTAGE - 1; ++s) {
-      if (s < nk) {
-        stage(s, kb + s, seg, tap, cb);
-        advance();
-      }
-    }
-    for (int it = 0; it < nk; ++it) {
+    int it = 0;
+    auto step = [&](auto jc) __attribute__((always_inline)) {
+      constexpr int j = decltype(jc)::value;
       const int ahead = min(NSTAGE - 2, nk - 1 - it);   // tiles issued after tile `it`
       vmcnt_wait(ahead * myni);
       asm volatile("" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       if (it + NSTAGE - 1 < nk) {
-        stage((it + NSTAGE - 1) % NSTAGE, kb + it + NSTAGE - 1, seg, tap, cb);
+        stage(std::integral_constant<int, (j + NSTAGE - 1) % NSTAGE>{}, kb + it + NSTAGE - 1);
         advance();
       }
-      compute(it % NSTAGE);
+      compute(jc);
+      ++it;
+    };
+    stage(std::integral_constant<int, 0>{}, kb);
+    advance();
+    if (NSTAGE > 2 && nk > 1) {
+      stage(std::integral_constant<int, 1>{}, kb + 1);
+      advance();
+    }
+    while (true) {
+      step(std::integral_constant<int, 0>{});
+      if (it >= nk) break;
+      step(std::integral_constant<int, 1>{});
+      if (it >= nk) break;
+      if constexpr (NSTAGE > 2) {
+        step(std::integral_constant<int, 2 % NSTAGE>{});
+        if (it >= nk) break;
+      }
     }
   }
 
