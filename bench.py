@@ -108,7 +108,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--bank", type=int, default=32)
-    ap.add_argument("--cpu-sample", type=int, default=12)
+    ap.add_argument("--cpu-sample", type=int, default=48)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--precision", default="f16", choices=["f16", "f32"])
     args = ap.parse_args()

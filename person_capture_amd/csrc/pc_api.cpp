@@ -23,6 +23,7 @@ hipError_t splitk_reduce_launch(int f32, const float* part, int splitk, int M, i
                                 const float* slope, int act, void* y, int ycs, int out_f32, hipStream_t s);
 hipError_t stem_launch(int f32, const StemParams& p, hipStream_t s);
 hipError_t maxpool_launch(int f32, const PoolParams& p, hipStream_t s);
+hipError_t stem_im2col_launch(int f32, const StemParams& p, int cin_true, void* col, hipStream_t s);
 struct LetterboxDesc;
 struct WarpDesc;
 struct AreaTab;
@@ -205,6 +206,13 @@ struct NetBuf { long long elems; int is_f32; void* d = nullptr; };
 struct NetTensor { int buf, H, W, C, cs, coff, is_f32; };
 struct NetOp { int w[32]; };
 struct ConvPlan { int rowb, cfg, splitk; long long M_per_image; double flops_per_image; };
+// A stem (tiny Cin) runs as im2col + a 1x1 MFMA conv over 32-element K rows.
+struct StemPlan {
+  int use_mfma = 0, npad = 0, cfg = 0, rowb = 0, cin_true = 0;
+  void* w = nullptr;        // [npad][32] act dtype
+  float* bias = nullptr;    // [npad]
+  float* slope = nullptr;   // [npad] or null
+};
 struct ProfRec { int a, b, kind; double flops; };
 
 struct pc_net {
@@ -219,6 +227,9 @@ struct pc_net {
   std::vector<void*> arrays;  // device copies (conv weights in act dtype, others f32)
   std::vector<long long> array_count;
   std::vector<ConvPlan> plans;
+  std::vector<StemPlan> stems;
+  std::vector<const float*> host_arrays;   // program arrays, valid during pc_net_create only
+  void* stem_col = nullptr;   // im2col scratch shared by the stems
   float* partial = nullptr;
   size_t partial_bytes = 0;
   double flops_per_image = 0.0;
@@ -265,6 +276,8 @@ static unsigned tensor_zero_off(const pc_net* n, int t) {
   return (unsigned)(end - (size_t)T.coff * es);
 }
 
+static const int kNumConvCfgs = 14;   // pc_conv.hip launch_rowb
+
 static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl) {
   const int* w = op.w;
   const int out = w[1], nseg = w[2], npad = w[14];
@@ -277,33 +290,82 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl) {
     if ((size_t)X.C * esz + 128 > kZeroTail) return fail(n->ctx, PC_ERR_FORMAT, "conv input wider than the zero tail");
   }
   // tile configuration (pc_conv.hip launch_rowb): channel tile BC must divide npad
-  static const int cfg_bc[9] = {128, 128, 64, 64, 96, 32, 32, 128, 256};
-  static const int cfg_bp[9] = {128, 64, 256, 128, 128, 256, 128, 256, 128};
+  static const int cfg_bc[kNumConvCfgs] = {128, 128, 64, 64, 96, 32, 32, 128, 256, 256, 64, 96, 32, 128};
+  static const int cfg_bp[kNumConvCfgs] = {128, 64, 256, 128, 128, 256, 128, 256, 128, 256, 512, 256, 512, 128};
   const NetTensor& Y = n->tens[out];
   const long long Mimg = (long long)Y.H * Y.W;
   const long long M = Mimg * n->max_batch;
   auto tiles = [&](int c) { return (M + cfg_bp[c] - 1) / cfg_bp[c] * (npad / cfg_bc[c]); };
+  // Tile choice, from single-conv measurements on MI355X (tools/probe_conv.py,
+  // DESIGN.md §3.1): 8-wave tiles with 64x64 or 128x64 per wave whenever the grid has
+  // enough tiles; the 4-wave tiles for small grids.
   int cfg = -1;
-  if (npad % 128 == 0) {
-    if (tiles(7) >= 256) cfg = 7;
-    else if (npad % 256 == 0 && tiles(8) >= 256) cfg = 8;
-    else cfg = tiles(0) >= 256 ? 0 : 1;
-  } else if (npad % 96 == 0) {
-    cfg = 4;
-  } else if (npad % 64 == 0) {
-    cfg = tiles(2) >= 512 ? 2 : 3;
-  } else if (npad % 32 == 0) {
-    cfg = tiles(5) >= 512 ? 5 : 6;
-  } else {
-    return fail(n->ctx, PC_ERR_FORMAT, "conv npad must be a multiple of 32");
-  }
+  auto fits = [&](int c, long long min_tiles) { return npad % cfg_bc[c] == 0 && tiles(c) >= min_tiles; };
+  if (fits(9, 192)) cfg = 9;                 // 256x256, npad % 256
+  else if (fits(7, 192)) cfg = 7;            // 128x256
+  else if (fits(13, 192)) cfg = 13;          // 128x128 (8 waves)
+  else if (npad % 128 && fits(11, 128)) cfg = 11;   // 96x256
+  else if (npad % 128 && fits(10, 128)) cfg = 10;   // 64x512
+  else if (npad % 64 && fits(12, 128)) cfg = 12;    // 32x512
+  else if (npad % 128 == 0) cfg = tiles(0) >= 256 ? 0 : 1;
+  else if (npad % 96 == 0) cfg = 4;
+  else if (npad % 64 == 0) cfg = tiles(2) >= 512 ? 2 : 3;
+  else if (npad % 32 == 0) cfg = tiles(5) >= 512 ? 5 : 6;
+  else return fail(n->ctx, PC_ERR_FORMAT, "conv npad must be a multiple of 32");
   if (const char* e = getenv("PC_CONV_CFG")) {   // testing / tuning override
     const int f = atoi(e);
-    if (f >= 0 && f < 9 && npad % cfg_bc[f] == 0) cfg = f;
+    if (f >= 0 && f < kNumConvCfgs && npad % cfg_bc[f] == 0) cfg = f;
+  }
+  if (const char* e = getenv("PC_CONV_ROWB")) {  // tuning: force 64-byte K-tiles
+    if (atoi(e) == 64) rowb = 64;
   }
   pl.rowb = rowb; pl.cfg = cfg; pl.M_per_image = Mimg;
   pl.splitk = w[24] > 1 ? w[24] : 1;
   if (Y.C > npad) return fail(n->ctx, PC_ERR_FORMAT, "conv output tensor wider than npad");
+  return PC_OK;
+}
+
+// Stem as im2col + 1x1 MFMA conv when the window fits one 32-element K row
+// (3x3x3 = 27). Weights are repacked [npad][32], tap-major, channel-minor.
+static int plan_stem(pc_net* n, const NetOp& op, StemPlan& st, size_t& col_bytes) {
+  const int* w = op.w;
+  const int KH = w[3], KW = w[4], cout = w[8], cin_true = w[13] > 0 ? w[13] : 3;
+  const NetTensor& X = n->tens[w[2]];
+  const NetTensor& Y = n->tens[w[1]];
+  if (getenv("PC_STEM_DIRECT") || KH * KW * cin_true > 32 || X.C != 4) return PC_OK;   // direct kernel
+  const int esz = n->f32 ? 4 : 2;
+  st.use_mfma = 1;
+  st.cin_true = cin_true;
+  st.npad = (std::max(cout, Y.C) + 31) / 32 * 32;
+  st.rowb = 32 * esz;   // one K-tile of exactly 32 elements
+  const long long M = (long long)Y.H * Y.W * n->max_batch;
+  st.cfg = st.npad % 128 == 0 ? 7 : (st.npad % 64 == 0 ? 10 : 12);
+  col_bytes = std::max(col_bytes, (size_t)M * 32 * esz + 256);
+  const float* hw = reinterpret_cast<const float*>(n->host_arrays[w[7]]);
+  std::vector<float> wf((size_t)st.npad * 32, 0.f), b(st.npad, 0.f), sl(st.npad, 0.f);
+  for (int co = 0; co < cout; ++co)
+    for (int t = 0; t < KH * KW; ++t)
+      for (int ci = 0; ci < cin_true; ++ci) wf[(size_t)co * 32 + t * cin_true + ci] = hw[((size_t)co * KH * KW + t) * 4 + ci];
+  const float* hb = reinterpret_cast<const float*>(n->host_arrays[w[9]]);
+  for (int co = 0; co < cout; ++co) b[co] = hb[co];
+  if (w[10] >= 0) {
+    const float* hs = reinterpret_cast<const float*>(n->host_arrays[w[10]]);
+    for (int co = 0; co < cout; ++co) sl[co] = hs[co];
+  }
+  HIPCHK(n->ctx, hipMalloc(&st.w, wf.size() * esz));
+  if (n->f32) {
+    HIPCHK(n->ctx, hipMemcpy(st.w, wf.data(), wf.size() * 4, hipMemcpyHostToDevice));
+  } else {
+    std::vector<_Float16> h(wf.size());
+    for (size_t k = 0; k < wf.size(); ++k) h[k] = (_Float16)wf[k];
+    HIPCHK(n->ctx, hipMemcpy(st.w, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+  }
+  HIPCHK(n->ctx, hipMalloc((void**)&st.bias, st.npad * 4));
+  HIPCHK(n->ctx, hipMemcpy(st.bias, b.data(), st.npad * 4, hipMemcpyHostToDevice));
+  if (w[10] >= 0) {
+    HIPCHK(n->ctx, hipMalloc((void**)&st.slope, st.npad * 4));
+    HIPCHK(n->ctx, hipMemcpy(st.slope, sl.data(), st.npad * 4, hipMemcpyHostToDevice));
+  }
   return PC_OK;
 }
 
@@ -397,8 +459,11 @@ extern "C" int pc_net_create(pc_ctx* c, const void* prog, size_t nbytes, int pre
     }
   }
   // plans + split-K workspace + stats
+  n->host_arrays.assign(narr, nullptr);
+  for (int i = 0; i < narr; ++i) n->host_arrays[i] = data + arr[i].first;
   n->plans.resize(n->ops.size());
-  size_t part = 0;
+  n->stems.resize(n->ops.size());
+  size_t part = 0, stem_col_bytes = 0;
   for (size_t i = 0; i < n->ops.size() && rc == PC_OK; ++i) {
     const NetOp& op = n->ops[i];
     if (op.w[0] == OP_CONV) {
@@ -423,12 +488,19 @@ extern "C" int pc_net_create(pc_ctx* c, const void* prog, size_t nbytes, int pre
       const NetTensor& Y = n->tens[op.w[1]];
       const int cin_true = op.w[13] > 0 ? op.w[13] : 3;
       n->flops_per_image += 2.0 * Y.H * Y.W * op.w[8] * op.w[3] * op.w[4] * cin_true;
-      n->launches += 1;
+      rc = plan_stem(n, op, n->stems[i], stem_col_bytes);
+      n->plans[i].flops_per_image = 2.0 * Y.H * Y.W * op.w[8] * op.w[3] * op.w[4] * cin_true;
+      n->launches += n->stems[i].use_mfma ? 2 : 1;
     } else if (op.w[0] == OP_MAXPOOL) {
       n->launches += 1;
     } else {
       rc = fail(c, PC_ERR_FORMAT, "unknown op type");
     }
+  }
+  n->host_arrays.clear();
+  if (rc == PC_OK && stem_col_bytes) {
+    if (hipMalloc(&n->stem_col, stem_col_bytes) != hipSuccess) rc = fail(c, PC_ERR_HIP, "stem im2col workspace");
+    else hipMemset(n->stem_col, 0, stem_col_bytes);
   }
   if (rc == PC_OK && part) {
     if (hipMalloc((void**)&n->partial, part) != hipSuccess) rc = fail(c, PC_ERR_HIP, "split-K workspace");
@@ -452,6 +524,12 @@ extern "C" int pc_net_destroy(pc_net* n) {
   if (n->partial) hipFree(n->partial);
   if (n->prep) hipFree(n->prep);
   if (n->in_copy) hipFree(n->in_copy);
+  for (auto& st : n->stems) {
+    if (st.w) hipFree(st.w);
+    if (st.bias) hipFree(st.bias);
+    if (st.slope) hipFree(st.slope);
+  }
+  if (n->stem_col) hipFree(n->stem_col);
   delete n;
   return PC_OK;
 }
@@ -541,7 +619,37 @@ static int run_ops(pc_net* n, int N) {
       p.ycs = Y.cs;
       p.cpad = w[12];
       p.y = tensor_ptr(n, w[1]);
-      HIPCHK(c, stem_launch(n->f32, p, s));
+      const StemPlan& st = n->stems[i];
+      if (!st.use_mfma) {
+        HIPCHK(c, stem_launch(n->f32, p, s));
+      } else {
+        HIPCHK(c, stem_im2col_launch(n->f32, p, st.cin_true, n->stem_col, s));
+        if (prof) {   // im2col counts as "other", the MFMA part as a conv launch
+          int rc = prof_event(n, &rec.b);
+          if (rc) return rc;
+          n->recs.push_back(rec);
+          rec = ProfRec{-1, -1, OP_CONV, n->plans[i].flops_per_image * N};
+          rc = prof_event(n, &rec.a);
+          if (rc) return rc;
+        }
+        ConvParams q;
+        memset(&q, 0, sizeof(q));
+        q.nseg = 1;
+        ConvSeg& S = q.seg[0];
+        S.x = n->stem_col;
+        S.H = Y.H; S.W = Y.W; S.C = 32; S.cs = 32;
+        S.KH = 1; S.KW = 1; S.stride = 1; S.pad = 0;
+        S.cblk = 1; S.kt = 1;
+        S.zero_off = (unsigned)((size_t)N * Y.H * Y.W * 32 * (n->f32 ? 4 : 2));
+        q.w = st.w; q.ktot = 32;
+        q.N = N; q.OH = Y.H; q.OW = Y.W; q.M = N * Y.H * Y.W;
+        q.npad = st.npad; q.cout = p.cout; q.cwrite = std::min(Y.C, st.npad);
+        q.y = p.y; q.ycs = Y.cs; q.out_f32 = n->f32 ? 1 : (Y.is_f32 ? 1 : 0);
+        q.bias = st.bias; q.bias_mode = BIAS_CHANNEL;
+        q.slope = st.slope; q.act = p.act;
+        q.kt_total = 1; q.splitk = 1;
+        HIPCHK(c, conv_launch(n->f32, st.rowb, st.cfg, q, s));
+      }
     } else if (w[0] == OP_MAXPOOL) {
       PoolParams p;
       const NetTensor& X = n->tens[w[2]];

@@ -23,6 +23,7 @@
 // (IResNet downsample 1x1/s2, ResNetV1e avg-down == 2x2/s2 conv) accumulate into
 // the same tile, so shortcut + main branch cost one launch and one output write.
 #include <type_traits>
+#include <utility>
 #include "pc_common.h"
 
 namespace pc {
@@ -73,6 +74,16 @@ __device__ __forceinline__ void load4(const T* src, float* v, int n) {
   for (int j = 0; j < n; ++j) v[j] = (float)src[j];
 }
 
+// Compile-time loop: f(integral_constant<int, 0>) ... f(integral_constant<int, N-1>).
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
 // Workgroup order: the dispatcher deals blocks round-robin over the 8 XCDs (b and
 // b+8 share one), so hand each XCD a contiguous range of tiles; with the channel
 // tile fastest, the channel tiles of one pixel tile share its im2col rows in the
@@ -85,25 +96,15 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
 
 // s_waitcnt vmcnt(n) with n known only at run time but wave-uniform (per-wave DMA count)
 __device__ __forceinline__ void vmcnt_wait(int n) {
+#define PC_VMW(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
   switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
-    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
-    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
-    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
-    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
-    case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    PC_VMW(0) PC_VMW(1) PC_VMW(2) PC_VMW(3) PC_VMW(4) PC_VMW(5) PC_VMW(6) PC_VMW(7)
+    PC_VMW(8) PC_VMW(9) PC_VMW(10) PC_VMW(11) PC_VMW(12) PC_VMW(13) PC_VMW(14) PC_VMW(15)
+    PC_VMW(16) PC_VMW(17) PC_VMW(18) PC_VMW(19) PC_VMW(20) PC_VMW(21) PC_VMW(22) PC_VMW(23)
+    PC_VMW(24) PC_VMW(25) PC_VMW(26) PC_VMW(27) PC_VMW(28) PC_VMW(29) PC_VMW(30) PC_VMW(31)
+    default: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
   }
+#undef PC_VMW
 }
 
 // BC x BP output tile per workgroup of WC x WP waves; NSTAGE-deep LDS ring of
@@ -149,18 +150,27 @@ __global__ __launch_bounds__(64 * WC * WP, 1) void conv_igemm(ConvParams p) {
   {
     int rem = kb;
     if (p.nseg > 1 && rem >= p.seg[0].kt) { rem -= p.seg[0].kt; seg = 1; }
-    const int cbl = p.seg[seg].cblk;
+    // p.seg is only ever indexed by constants: a runtime index would copy the whole
+    // kernel-argument struct to scratch
+    const int cbl = seg ? p.seg[1].cblk : p.seg[0].cblk;
+    const int kw = seg ? p.seg[1].KW : p.seg[0].KW;
     const int tap = rem / cbl;
     cb = rem - tap * cbl;
-    th = tap / p.seg[seg].KW;
-    tw = tap - th * p.seg[seg].KW;
+    th = tap / kw;
+    tw = tap - th * kw;
   }
   // current segment, cached in scalars
-  const char* sx = reinterpret_cast<const char*>(p.seg[seg].x);
-  int sH = p.seg[seg].H, sW = p.seg[seg].W, scs = p.seg[seg].cs;
-  int sKH = p.seg[seg].KH, sKW = p.seg[seg].KW, sstr = p.seg[seg].stride, spad = p.seg[seg].pad;
-  int scblk = p.seg[seg].cblk;
-  unsigned szero = p.seg[seg].zero_off;
+  const char* sx;
+  int sH, sW, scs, sKH, sKW, sstr, spad, scblk;
+  unsigned szero;
+  auto load_seg = [&](const ConvSeg& S) __attribute__((always_inline)) {
+    sx = reinterpret_cast<const char*>(S.x);
+    sH = S.H; sW = S.W; scs = S.cs;
+    sKH = S.KH; sKW = S.KW; sstr = S.stride; spad = S.pad;
+    scblk = S.cblk; szero = S.zero_off;
+  };
+  if (seg) load_seg(p.seg[1]);
+  else load_seg(p.seg[0]);
 
   // ---- per-lane staging geometry ----
   // Every staged 16-byte chunk is addressed as (wave-uniform SGPR base) + (per-lane
@@ -174,8 +184,8 @@ __global__ __launch_bounds__(64 * WC * WP, 1) void conv_igemm(ConvParams p) {
   int x_ih[NI], x_iw[NI], x_n[NI];  // window origin of this lane's output pixel (current segment)
   unsigned woff[NI], xpix[NI], zlane[NI], xcur[NI];
   int x_oh[NI], x_ow[NI];
-#pragma unroll
-  for (int i = 0; i < NI; ++i) {
+  static_for<NI>([&](auto ic) __attribute__((always_inline)) {
+    constexpr int i = decltype(ic)::value;
     const int g = i * NW + wave;
     const int r = g * RPI + lrow;
     const int lc = pchunk ^ ((r >> 1) & (CHUNKS - 1));
@@ -194,10 +204,10 @@ __global__ __launch_bounds__(64 * WC * WP, 1) void conv_igemm(ConvParams p) {
         x_ow[i] = rem - x_oh[i] * p.OW;
       }
     }
-  }
+  });
   auto prep_seg = [&]() __attribute__((always_inline)) {   // per-lane window origins for the current segment
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
+    static_for<NI>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = decltype(ic)::value;
       const int g = i * NW + wave;
       if (g < NTOT && g * RPI >= BC) {
         const int r = g * RPI + lrow;
@@ -207,19 +217,19 @@ __global__ __launch_bounds__(64 * WC * WP, 1) void conv_igemm(ConvParams p) {
         x_iw[i] = x_ow[i] * sstr - spad;
         xpix[i] = (unsigned)((((long long)max(x_n[i], 0) * sH + x_ih[i]) * sW + x_iw[i]) * scs * ESZ) + lc * 16;
       }
-    }
+    });
   };
   auto prep_tap = [&]() __attribute__((always_inline)) {   // per-lane source offsets for tap (th, tw)
     const unsigned tapoff = (unsigned)((th * sW + tw) * scs * ESZ);
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
+    static_for<NI>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = decltype(ic)::value;
       const int g = i * NW + wave;
       if (g < NTOT && g * RPI >= BC) {
         const bool ok = x_n[i] >= 0 && (unsigned)(x_ih[i] + th) < (unsigned)sH &&
                         (unsigned)(x_iw[i] + tw) < (unsigned)sW;
         xcur[i] = ok ? xpix[i] + tapoff : zlane[i];
       }
-    }
+    });
   };
   prep_seg();
   prep_tap();
@@ -228,8 +238,8 @@ __global__ __launch_bounds__(64 * WC * WP, 1) void conv_igemm(ConvParams p) {
     constexpr int buf = decltype(bufc)::value;
     const char* xb = sx + cb * (BKE * ESZ);
     const char* wb = reinterpret_cast<const char*>(p.w) + (long long)ktl * (BKE * ESZ);
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
+    static_for<NI>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = decltype(ic)::value;
       const int g = i * NW + wave;
       if (g < NTOT) {
         unsigned off = g * RPI < BC ? woff[i] : xcur[i];
@@ -238,7 +248,7 @@ __global__ __launch_bounds__(64 * WC * WP, 1) void conv_igemm(ConvParams p) {
         char* dst = smem + buf * BUF + g * 1024;
         __builtin_amdgcn_global_load_lds((gptr_t)src, (lds_ptr_t)dst, 16, 0, 0);
       }
-    }
+    });
   };
   auto advance = [&]() __attribute__((always_inline)) {
     if (++cb < scblk) return;
@@ -248,10 +258,7 @@ __global__ __launch_bounds__(64 * WC * WP, 1) void conv_igemm(ConvParams p) {
       if (++th == sKH) {
         th = 0;
         if (++seg >= p.nseg) return;
-        sx = reinterpret_cast<const char*>(p.seg[seg].x);
-        sH = p.seg[seg].H; sW = p.seg[seg].W; scs = p.seg[seg].cs;
-        sKH = p.seg[seg].KH; sKW = p.seg[seg].KW; sstr = p.seg[seg].stride; spad = p.seg[seg].pad;
-        scblk = p.seg[seg].cblk; szero = p.seg[seg].zero_off;
+        load_seg(p.seg[1]);   // segments only advance 0 -> 1
         prep_seg();
       }
     }
@@ -329,38 +336,36 @@ __global__ __launch_bounds__(64 * WC * WP, 1) void conv_igemm(ConvParams p) {
       compute(jc);
       ++it;
     };
-    stage(std::integral_constant<int, 0>{}, kb);
-    advance();
-    if (NSTAGE > 2 && nk > 1) {
-      stage(std::integral_constant<int, 1>{}, kb + 1);
-      advance();
-    }
-    while (true) {
-      step(std::integral_constant<int, 0>{});
-      if (it >= nk) break;
-      step(std::integral_constant<int, 1>{});
-      if (it >= nk) break;
-      if constexpr (NSTAGE > 2) {
-        step(std::integral_constant<int, 2 % NSTAGE>{});
-        if (it >= nk) break;
+    // prologue: tiles 0 .. NSTAGE-2 in flight
+    static_for<NSTAGE - 1>([&](auto jc) __attribute__((always_inline)) {
+      constexpr int j = decltype(jc)::value;
+      if (j < nk) {
+        stage(jc, kb + j);
+        advance();
       }
+    });
+    while (it < nk) {
+      static_for<NSTAGE>([&](auto jc) __attribute__((always_inline)) {
+        if (it < nk) step(jc);
+      });
     }
   }
 
   // ---- epilogue ----
   const int chq = (lane >> 4) * 4;
-#pragma unroll
-  for (int b = 0; b < TP; ++b) {
+  // compile-time (a, b) everywhere: a runtime fragment index would demote acc to scratch
+  static_for<TP>([&](auto bc) __attribute__((always_inline)) {
+    constexpr int b = decltype(bc)::value;
     const int pix = p0 + wc * WTP + b * 16 + (lane & 15);
-    if (pix >= p.M) continue;
+    if (pix >= p.M) return;
     if (p.splitk > 1) {
-#pragma unroll
-      for (int a = 0; a < TC; ++a) {
+      static_for<TC>([&](auto ac) __attribute__((always_inline)) {
+        constexpr int a = decltype(ac)::value;
         const int ch = c0 + wr * WTC + a * 16 + chq;
         float* dst = p.partial + ((long long)z * p.M + pix) * p.npad + ch;
         *reinterpret_cast<f32x4*>(dst) = acc[a][b];
-      }
-      continue;
+      });
+      return;
     }
     int n = 0, oh = 0, ow = 0;
     if (p.bias_mode == BIAS_BORDER9 || p.res_mode == RES_UP2) {
@@ -382,10 +387,10 @@ __global__ __launch_bounds__(64 * WC * WP, 1) void conv_igemm(ConvParams p) {
     }
     long long rpix = pix;
     if (p.res_mode == RES_UP2) rpix = ((long long)n * p.rH + (oh >> 1)) * p.rW + (ow >> 1);
-#pragma unroll
-    for (int a = 0; a < TC; ++a) {
+    static_for<TC>([&](auto ac) __attribute__((always_inline)) {
+      constexpr int a = decltype(ac)::value;
       const int ch = c0 + wr * WTC + a * 16 + chq;
-      if (ch >= p.cwrite) continue;
+      if (ch >= p.cwrite) return;
       const int nv = min(4, p.cwrite - ch);
       float v[4] = {acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]};
       if (p.bias_mode != BIAS_NONE) {
@@ -418,8 +423,8 @@ __global__ __launch_bounds__(64 * WC * WP, 1) void conv_igemm(ConvParams p) {
         store4<float>(reinterpret_cast<float*>(p.y) + (long long)pix * p.ycs + ch, v, nv);
       else
         store4<T>(reinterpret_cast<T*>(p.y) + (long long)pix * p.ycs + ch, v, nv);
-    }
-  }
+    });
+  });
 }
 
 // Sum split-K partials, then the same bias/activation epilogue (no residual).
@@ -487,6 +492,42 @@ __global__ __launch_bounds__(256) void stem_conv3x3(StemParams p) {
   }
 }
 
+// Stem im2col: the KHxKWxcin_true window of every output pixel packed into one
+// 32-element K row (tap-major, channel-minor, zero past K_true and in the padding),
+// so the stem runs on the MFMA engine as a 1x1 conv with C = 32. Four threads per
+// pixel, 8 elements (16 B f16) each.
+template <typename T>
+__global__ void stem_im2col(StemParams p, int cin_true, T* __restrict__ col) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long M = (long long)p.N * p.OH * p.OW;
+  if (i >= M * 4) return;
+  const long long pix = i >> 2;
+  const int k0 = (int)(i & 3) * 8;
+  const int hw = p.OH * p.OW;
+  const int n = (int)(pix / hw);
+  const int rem = (int)(pix - (long long)n * hw);
+  const int oh = rem / p.OW, ow = rem - (rem / p.OW) * p.OW;
+  const int ktrue = p.KH * p.KW * cin_true;
+  const T* xb = reinterpret_cast<const T*>(p.x);
+  T v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = k0 + j;
+    T e = (T)0.f;
+    if (k < ktrue) {
+      const int tap = k / cin_true, c = k - tap * cin_true;
+      const int th = tap / p.KW, tw = tap - th * p.KW;
+      const int ih = oh * p.stride - p.pad + th, iw = ow * p.stride - p.pad + tw;
+      if ((unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W)
+        e = xb[(((long long)n * p.H + ih) * p.W + iw) * p.xcs + c];
+    }
+    v[j] = e;
+  }
+  T* dst = col + pix * 32 + k0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) dst[j] = v[j];
+}
+
 // NHWC max pool (padding = -inf, PyTorch semantics); one thread per pixel x 4 channels.
 template <typename T>
 __global__ void maxpool_nhwc(PoolParams p) {
@@ -517,30 +558,39 @@ __global__ void maxpool_nhwc(PoolParams p) {
 // ---------------------------------------------------------------------------
 // host-side launchers
 // ---------------------------------------------------------------------------
-template <typename T, int BC, int BP, int ROWB, int WC, int WP, int NS>
+// LDS ring depth: as many K-tiles as fit in 144 KiB, 2..8
+constexpr int ring_depth(int bc, int bp, int rowb) {
+  return (147456 / ((bc + bp) * rowb)) < 2 ? 2 : ((147456 / ((bc + bp) * rowb)) > 8 ? 8 : 147456 / ((bc + bp) * rowb));
+}
+
+template <typename T, int BC, int BP, int ROWB, int WC, int WP>
 static hipError_t launch_cfg(const ConvParams& p, hipStream_t s) {
+  constexpr int NS = ring_depth(BC, BP, ROWB);
   const int nwg = (p.M + BP - 1) / BP * (p.npad / BC);
   dim3 grid(nwg, 1, p.splitk);
   hipLaunchKernelGGL((conv_igemm<T, BC, BP, ROWB, WC, WP, NS>), grid, dim3(64 * WC * WP), 0, s, p);
   return hipGetLastError();
 }
 
-// tile configurations (cfg ids are chosen on the host, pc_api.cpp plan_conv):
-//   0: 128x128, 4 waves, 2-stage     1: 128x64, 4 waves, 2-stage    2: 64x256, 4 waves, 2-stage
-//   3: 64x128, 4 waves, 2-stage      4: 96x128, 4 waves, 2-stage    5: 32x256, 4 waves, 2-stage
-//   6: 32x128, 4 waves, 2-stage      7: 128x256, 8 waves, 3-stage   8: 256x128, 8 waves, 3-stage
+// Tile configurations (channels x pixels, waves as WC x WP); keep in sync with
+// kConvCfgs in pc_api.cpp.
 template <typename T, int ROWB>
 static hipError_t launch_rowb(const ConvParams& p, int cfg, hipStream_t s) {
   switch (cfg) {
-    case 0: return launch_cfg<T, 128, 128, ROWB, 2, 2, 2>(p, s);
-    case 1: return launch_cfg<T, 128, 64, ROWB, 2, 2, 2>(p, s);
-    case 2: return launch_cfg<T, 64, 256, ROWB, 2, 2, 2>(p, s);
-    case 3: return launch_cfg<T, 64, 128, ROWB, 2, 2, 2>(p, s);
-    case 4: return launch_cfg<T, 96, 128, ROWB, 2, 2, 2>(p, s);
-    case 5: return launch_cfg<T, 32, 256, ROWB, 2, 2, 2>(p, s);
-    case 6: return launch_cfg<T, 32, 128, ROWB, 2, 2, 2>(p, s);
-    case 7: return launch_cfg<T, 128, 256, ROWB, 2, 4, 3>(p, s);
-    case 8: return launch_cfg<T, 256, 128, ROWB, 4, 2, 3>(p, s);
+    case 0: return launch_cfg<T, 128, 128, ROWB, 2, 2>(p, s);
+    case 1: return launch_cfg<T, 128, 64, ROWB, 2, 2>(p, s);
+    case 2: return launch_cfg<T, 64, 256, ROWB, 2, 2>(p, s);
+    case 3: return launch_cfg<T, 64, 128, ROWB, 2, 2>(p, s);
+    case 4: return launch_cfg<T, 96, 128, ROWB, 2, 2>(p, s);
+    case 5: return launch_cfg<T, 32, 256, ROWB, 2, 2>(p, s);
+    case 6: return launch_cfg<T, 32, 128, ROWB, 2, 2>(p, s);
+    case 7: return launch_cfg<T, 128, 256, ROWB, 2, 4>(p, s);
+    case 8: return launch_cfg<T, 256, 128, ROWB, 4, 2>(p, s);
+    case 9: return launch_cfg<T, 256, 256, ROWB, 2, 4>(p, s);
+    case 10: return launch_cfg<T, 64, 512, ROWB, 1, 8>(p, s);
+    case 11: return launch_cfg<T, 96, 256, ROWB, 2, 4>(p, s);
+    case 12: return launch_cfg<T, 32, 512, ROWB, 1, 8>(p, s);
+    case 13: return launch_cfg<T, 128, 128, ROWB, 2, 4>(p, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -568,6 +618,15 @@ hipError_t stem_launch(int f32, const StemParams& p, hipStream_t s) {
   if (p.KH != 3 || p.KW != 3 || p.cin != 4 || p.cout > 64 || p.cpad % 4) return hipErrorInvalidValue;
   if (f32) hipLaunchKernelGGL(stem_conv3x3<float>, grid, dim3(256), 0, s, p);
   else hipLaunchKernelGGL(stem_conv3x3<f16>, grid, dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t stem_im2col_launch(int f32, const StemParams& p, int cin_true, void* col, hipStream_t s) {
+  const long long M = (long long)p.N * p.OH * p.OW;
+  dim3 grid((unsigned)((M * 4 + 255) / 256));
+  if (p.KH * p.KW * cin_true > 32) return hipErrorInvalidValue;
+  if (f32) hipLaunchKernelGGL(stem_im2col<float>, grid, dim3(256), 0, s, p, cin_true, (float*)col);
+  else hipLaunchKernelGGL(stem_im2col<f16>, grid, dim3(256), 0, s, p, cin_true, (f16*)col);
   return hipGetLastError();
 }
 

@@ -58,14 +58,26 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("cfg", [None, "0", "7", "8", "2", "5"])
+ALL_CFGS = [None] + [f"{c}{r}" for c in range(14) for r in ("", ":64")]
+
+
+def _set_cfg(monkeypatch, cfg):
+    """cfg = "<tile id>[:64]": PC_CONV_CFG forces the tile where its channel tile divides
+    npad (otherwise the planner's choice runs); ":64" forces 64-byte K-tiles."""
+    if cfg is None:
+        return
+    c, _, rowb = cfg.partition(":")
+    monkeypatch.setenv("PC_CONV_CFG", c)
+    if rowb:
+        monkeypatch.setenv("PC_CONV_ROWB", rowb)
+
+
+@pytest.mark.parametrize("cfg", ALL_CFGS)
 @pytest.mark.parametrize("prec", [PC_PREC_F32, PC_PREC_F16])
 @pytest.mark.parametrize("case", CASES)
 def test_single_conv(gpu_ctx, monkeypatch, prec, case, cfg):
-    """Every tile configuration of pc_conv.hip (PC_CONV_CFG forces one where the
-    channel tile divides npad; otherwise the planner's choice runs)."""
-    if cfg is not None:
-        monkeypatch.setenv("PC_CONV_CFG", cfg)
+    """Every tile configuration of pc_conv.hip at both K-tile widths."""
+    _set_cfg(monkeypatch, cfg)
     H, cin, cout, k, s, act, bmode, out_f32 = case
     rng = np.random.default_rng(hash(case) & 0xFFFF)
     N = 3
@@ -106,11 +118,10 @@ def test_single_conv(gpu_ctx, monkeypatch, prec, case, cfg):
     assert np.all(got[..., cout:] == 0), "channel padding must be zero"
 
 
-@pytest.mark.parametrize("cfg", [None, "0", "7", "8"])
+@pytest.mark.parametrize("cfg", ALL_CFGS)
 @pytest.mark.parametrize("prec", [PC_PREC_F32, PC_PREC_F16])
 def test_two_segments_residual_upsample_splitk(gpu_ctx, monkeypatch, prec, cfg):
-    if cfg is not None:
-        monkeypatch.setenv("PC_CONV_CFG", cfg)
+    _set_cfg(monkeypatch, cfg)
     """op1: conv3x3/s2 on x -> r (14x14); op2: conv3x3 on r + 1x1/s2 on x (2 segments), + up2(q) residual;
     op3: 7x7 valid split-K conv on op2 -> f32; op4: 1x1 conv with same-pixel residual, act after res."""
     rng = np.random.default_rng(7)

@@ -1,0 +1,63 @@
+"""Reduce rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes to HBM bytes per conv launch.
+
+usage: python tools/pmc_traffic.py <pmc_dir> [<pmc_dir> ...] <out.json>
+
+Corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and WRITE_SIZE are in KiB;
+on gfx950 FETCH_SIZE reports half the bytes of a wide coalesced read (16 B/lane
+global_load / LDS-DMA), so it is doubled; WRITE_SIZE is exact for 16-B stores.
+The conv epilogue stores 8 B (f16x4) or 16 B per lane, so WRITE_SIZE is taken
+as-is and flagged uncalibrated for the 8-B form.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def load(dirs):
+    vals = defaultdict(lambda: defaultdict(list))   # counter -> kernel -> [values]
+    for d in dirs:
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            with open(f) as fh:
+                for row in csv.DictReader(fh):
+                    name = row.get("Kernel_Name", "")
+                    ctr = row.get("Counter_Name", "")
+                    try:
+                        v = float(row.get("Counter_Value", "nan"))
+                    except ValueError:
+                        continue
+                    vals[ctr][name].append(v)
+    return vals
+
+
+def main():
+    *dirs, out = sys.argv[1:]
+    vals = load(dirs)
+    per_kernel = {}
+    for ctr, kern in vals.items():
+        for name, v in kern.items():
+            per_kernel.setdefault(name, {})[ctr] = (sum(v) / len(v), len(v))
+    conv = {k: v for k, v in per_kernel.items() if "conv_igemm" in k}
+    fetch = sum(v.get("FETCH_SIZE", (0, 0))[0] * v.get("FETCH_SIZE", (0, 0))[1] for v in conv.values())
+    nf = sum(v.get("FETCH_SIZE", (0, 0))[1] for v in conv.values())
+    write = sum(v.get("WRITE_SIZE", (0, 0))[0] * v.get("WRITE_SIZE", (0, 0))[1] for v in conv.values())
+    nw = sum(v.get("WRITE_SIZE", (0, 0))[1] for v in conv.values())
+    res = {
+        "source": [os.path.relpath(d) for d in dirs],
+        "conv_launches_fetch": nf, "conv_launches_write": nw,
+        "conv_fetch_bytes_per_launch": 2.0 * 1024.0 * fetch / nf if nf else None,
+        "conv_write_bytes_per_launch": 1024.0 * write / nw if nw else None,
+        "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count on 16-B/lane reads); WRITE_SIZE KiB x1024",
+        "per_kernel": {k: {c: {"mean_kib": round(m, 1), "dispatches": n} for c, (m, n) in v.items()}
+                       for k, v in sorted(per_kernel.items())},
+    }
+    if nf and nw:
+        res["conv_hbm_bytes_per_launch"] = res["conv_fetch_bytes_per_launch"] + res["conv_write_bytes_per_launch"]
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps({k: v for k, v in res.items() if k != "per_kernel"}))
+
+
+if __name__ == "__main__":
+    main()

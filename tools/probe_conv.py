@@ -1,5 +1,6 @@
 """Single-conv microbenchmark of the implicit-GEMM engine (HIP-event timed).
-usage: python tools/probe_conv.py [cfg ...]"""
+usage: python tools/probe_conv.py [cfg[:rowb] ...]   (cfg "auto" = planner's choice)
+env PROBE_SHAPES=name1,name2 restricts the shapes."""
 import os
 import sys
 
@@ -18,6 +19,10 @@ SHAPES = [
     ("s2_3x3_128", 256, 28, 128, 128, 3, 1),
     ("s1_3x3_64", 256, 56, 64, 64, 3, 1),
     ("s4_3x3_512", 256, 7, 512, 512, 3, 1),
+    ("sc_160_64", 64, 160, 64, 64, 3, 1),
+    ("sc_80_96", 64, 80, 96, 96, 3, 1),
+    ("sc_40_96", 64, 40, 96, 96, 3, 1),
+    ("sc_20_224", 64, 20, 224, 224, 3, 1),
 ]
 
 
@@ -37,16 +42,28 @@ def build(N, H, cin, cout, k, s):
 def main():
     cfgs = sys.argv[1:] or ["auto"]
     ctx = GpuContext(0)
+    only = [x for x in os.environ.get("PROBE_SHAPES", "").split(",") if x]
     for name, N, H, cin, cout, k, s in SHAPES:
+        if only and name not in only:
+            continue
         P = build(N, H, cin, cout, k, s)
         x = np.random.default_rng(1).standard_normal((N, H, H, cin)).astype(np.float16)
         d = ctx.upload(x)
-        for c in cfgs:
+        for spec in cfgs:
+            c, _, rowb = spec.partition(":")
+            if rowb:
+                os.environ["PC_CONV_ROWB"] = rowb
+            else:
+                os.environ.pop("PC_CONV_ROWB", None)
             if c == "auto":
                 os.environ.pop("PC_CONV_CFG", None)
             else:
                 os.environ["PC_CONV_CFG"] = c
-            net = Net(ctx, P.serialize(), PC_PREC_F16, max_batch=N)
+            try:
+                net = Net(ctx, P.serialize(), PC_PREC_F16, max_batch=N)
+            except RuntimeError as e:
+                print(f"{name:16s} cfg {spec:6s} n/a ({e})", flush=True)
+                continue
             for _ in range(3):
                 net.run(d.ptr, N)
             net.profile(True)
@@ -56,7 +73,7 @@ def main():
             net.profile(False)
             us = r["conv_ms"] * 1e3 / r["conv_launches"]
             tf = r["conv_flops"] / (r["conv_ms"] * 1e-3) / 1e12
-            print(f"{name:16s} cfg {c:4s} {us:9.1f} us/launch  {tf:7.1f} TFLOP/s", flush=True)
+            print(f"{name:16s} cfg {spec:6s} {us:9.1f} us/launch  {tf:7.1f} TFLOP/s", flush=True)
             net.close()
 
 
