@@ -19,6 +19,10 @@
 
 namespace pc {
 hipError_t conv_launch(int f32, int rowb, int cfg, const ConvParams& p, hipStream_t s);
+hipError_t conv_halo_launch(int f32, int cfg, const ConvParams& p, hipStream_t s);
+int conv_halo_num_cfgs();
+int conv_halo_tile(int cfg, int* bc, int* bp);
+int conv_halo_fits(int cfg, int KH, int KW, int W);
 hipError_t splitk_reduce_launch(int f32, const float* part, int splitk, int M, int npad, int cout, const float* bias,
                                 const float* slope, int act, void* y, int ycs, int out_f32, hipStream_t s);
 hipError_t stem_launch(int f32, const StemParams& p, hipStream_t s);
@@ -205,7 +209,7 @@ enum { OP_CONV = 1, OP_STEM = 2, OP_MAXPOOL = 3 };
 struct NetBuf { long long elems; int is_f32; void* d = nullptr; };
 struct NetTensor { int buf, H, W, C, cs, coff, is_f32; };
 struct NetOp { int w[32]; };
-struct ConvPlan { int rowb, cfg, splitk; long long M_per_image; double flops_per_image; };
+struct ConvPlan { int rowb, cfg, splitk, halo = -1; long long M_per_image; double flops_per_image; };
 // A stem (tiny Cin) runs as im2col + a 1x1 MFMA conv over 32-element K rows.
 struct StemPlan {
   int use_mfma = 0, npad = 0, cfg = 0, rowb = 0, cin_true = 0;
@@ -321,6 +325,40 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl) {
   }
   pl.rowb = rowb; pl.cfg = cfg; pl.M_per_image = Mimg;
   pl.splitk = w[24] > 1 ? w[24] : 1;
+  pl.halo = -1;
+  // Stride-1 "same" convs (the bulk of both trunks) run on the halo kernel
+  // (pc_conv_halo.hip): the input run of a pixel tile is staged once per channel chunk
+  // and every tap reads it from LDS. PC_CONV_HALO=0 disables, =k+1 forces cfg k.
+  {
+    const NetTensor& X = n->tens[w[3]];
+    const int KH = w[4], KW = w[5], st = w[6], pd = w[7];
+    const char* e = getenv("PC_CONV_HALO");
+    const int force = e ? atoi(e) : -1;
+    const bool ok = nseg == 1 && pl.splitk == 1 && st == 1 && KH == KW && pd * 2 + 1 == KH && X.H == Y.H &&
+                    X.W == Y.W && KH * KW <= 32 && (double)M * X.cs * esz < 4294967296.0 - 65536.0 && force != 0;
+    if (ok) {
+      auto htiles = [&](int hc) {
+        int bc = 0, bp = 0;
+        conv_halo_tile(hc, &bc, &bp);
+        return npad % bc ? 0LL : (M + bp - 1) / bp * (npad / bc);
+      };
+      auto hok = [&](int hc) { return htiles(hc) > 0 && conv_halo_fits(hc, KH, KW, X.W); };
+      int hc = -1;
+      if (force > 0) {
+        if (hok(force - 1)) hc = force - 1;
+      } else {
+        // largest tile whose grid still covers the CUs; smaller tiles otherwise
+        static const int order[] = {0, 1, 2, 3, 4};
+        for (int k : order)
+          if (hok(k) && htiles(k) >= 192) { hc = k; break; }
+        if (hc < 0)
+          for (int k : {2, 4, 3, 1, 0})
+            if (hok(k)) { hc = k; break; }
+      }
+      pl.halo = hc;
+      if (hc >= 0) pl.rowb = 64;   // the halo kernel steps K by one 64-byte LDS row
+    }
+  }
   if (Y.C > npad) return fail(n->ctx, PC_ERR_FORMAT, "conv output tensor wider than npad");
   return PC_OK;
 }
@@ -598,7 +636,12 @@ static int run_ops(pc_net* n, int N) {
       p.splitk = pl.splitk;
       p.partial = n->partial;
       p.zero = c->zero;
-      HIPCHK(c, conv_launch(n->f32, pl.rowb, pl.cfg, p, s));
+      if (const char* e = getenv("PC_CONV_DBG")) p.dbg = atoi(e);
+      if (pl.halo >= 0) {
+        HIPCHK(c, conv_halo_launch(n->f32, pl.halo, p, s));
+      } else {
+        HIPCHK(c, conv_launch(n->f32, pl.rowb, pl.cfg, p, s));
+      }
       if (pl.splitk > 1) {
         HIPCHK(c, splitk_reduce_launch(n->f32, n->partial, pl.splitk, p.M, p.npad, p.cout, p.bias, p.slope, p.act,
                                        p.y, p.ycs, p.out_f32, s));

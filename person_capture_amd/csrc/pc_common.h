@@ -51,6 +51,7 @@ struct ConvParams {
   int splitk;
   int kt_total;
   const void* zero;    // >= 256 zero bytes (padding taps read from here)
+  int dbg;             // tuning experiments only (PC_CONV_DBG): 1 no staging, 2 no MFMA, 4 one-image footprint
 };
 
 // Direct convolution for tiny input channel counts (network stems, Cin <= 4).

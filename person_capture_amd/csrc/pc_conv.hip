@@ -22,90 +22,9 @@
 // A second, optional K-segment lets a residual block's shortcut projection
 // (IResNet downsample 1x1/s2, ResNetV1e avg-down == 2x2/s2 conv) accumulate into
 // the same tile, so shortcut + main branch cost one launch and one output write.
-#include <type_traits>
-#include <utility>
-#include "pc_common.h"
+#include "pc_conv_common.h"
 
 namespace pc {
-
-__device__ __forceinline__ float act_apply(float v, int act, float slope) {
-  if (act == ACT_RELU) return v > 0.f ? v : 0.f;
-  if (act == ACT_PRELU) return v > 0.f ? v : v * slope;
-  if (act == ACT_SILU) return v / (1.0f + __expf(-v));
-  return v;
-}
-
-template <typename T>
-__device__ __forceinline__ void store4(T* dst, const float* v, int n);
-
-template <>
-__device__ __forceinline__ void store4<f16>(f16* dst, const float* v, int n) {
-  if (n >= 4) {
-    f16x4 h = {(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
-    *reinterpret_cast<f16x4*>(dst) = h;
-  } else {
-    for (int j = 0; j < n; ++j) dst[j] = (f16)v[j];
-  }
-}
-template <>
-__device__ __forceinline__ void store4<float>(float* dst, const float* v, int n) {
-  if (n >= 4) {
-    *reinterpret_cast<f32x4*>(dst) = f32x4{v[0], v[1], v[2], v[3]};
-  } else {
-    for (int j = 0; j < n; ++j) dst[j] = v[j];
-  }
-}
-
-template <typename T>
-__device__ __forceinline__ void load4(const T* src, float* v, int n) {
-  if constexpr (sizeof(T) == 2) {
-    if (n >= 4) {
-      f16x4 h = *reinterpret_cast<const f16x4*>(src);
-      v[0] = (float)h[0]; v[1] = (float)h[1]; v[2] = (float)h[2]; v[3] = (float)h[3];
-      return;
-    }
-  } else {
-    if (n >= 4) {
-      f32x4 h = *reinterpret_cast<const f32x4*>(src);
-      v[0] = h[0]; v[1] = h[1]; v[2] = h[2]; v[3] = h[3];
-      return;
-    }
-  }
-  for (int j = 0; j < n; ++j) v[j] = (float)src[j];
-}
-
-// Compile-time loop: f(integral_constant<int, 0>) ... f(integral_constant<int, N-1>).
-template <typename F, int... I>
-__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
-  (f(std::integral_constant<int, I>{}), ...);
-}
-template <int N, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  static_for_impl(f, std::make_integer_sequence<int, N>{});
-}
-
-// Workgroup order: the dispatcher deals blocks round-robin over the 8 XCDs (b and
-// b+8 share one), so hand each XCD a contiguous range of tiles; with the channel
-// tile fastest, the channel tiles of one pixel tile share its im2col rows in the
-// same L2. Bijective for any grid size (MI355X_MICROARCH.md, T1).
-__device__ __forceinline__ int xcd_remap(int b, int nwg) {
-  const int xcd = b & 7, idx = b >> 3;
-  const int q = nwg >> 3, r = nwg & 7;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
-}
-
-// s_waitcnt vmcnt(n) with n known only at run time but wave-uniform (per-wave DMA count)
-__device__ __forceinline__ void vmcnt_wait(int n) {
-#define PC_VMW(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
-  switch (n) {
-    PC_VMW(0) PC_VMW(1) PC_VMW(2) PC_VMW(3) PC_VMW(4) PC_VMW(5) PC_VMW(6) PC_VMW(7)
-    PC_VMW(8) PC_VMW(9) PC_VMW(10) PC_VMW(11) PC_VMW(12) PC_VMW(13) PC_VMW(14) PC_VMW(15)
-    PC_VMW(16) PC_VMW(17) PC_VMW(18) PC_VMW(19) PC_VMW(20) PC_VMW(21) PC_VMW(22) PC_VMW(23)
-    PC_VMW(24) PC_VMW(25) PC_VMW(26) PC_VMW(27) PC_VMW(28) PC_VMW(29) PC_VMW(30) PC_VMW(31)
-    default: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
-  }
-#undef PC_VMW
-}
 
 // BC x BP output tile per workgroup of WC x WP waves; NSTAGE-deep LDS ring of
 // K-tiles filled by LDS-DMA, tile k+NSTAGE-1 issued right after the barrier that
@@ -197,8 +116,8 @@ __global__ __launch_bounds__(64 * WC * WP, 1) void conv_igemm(ConvParams p) {
       const int pix = p0 + (r - BC);
       if (pix < p.M) {
         const int hw = p.OH * p.OW;
-        const int n = pix / hw;
-        const int rem = pix - n * hw;
+        const int n = (p.dbg & 4) ? 0 : pix / hw;
+        const int rem = pix % hw;
         x_n[i] = n;
         x_oh[i] = rem / p.OW;
         x_ow[i] = rem - x_oh[i] * p.OW;
@@ -330,10 +249,10 @@ __global__ __launch_bounds__(64 * WC * WP, 1) void conv_igemm(ConvParams p) {
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       if (it + NSTAGE - 1 < nk) {
-        stage(std::integral_constant<int, (j + NSTAGE - 1) % NSTAGE>{}, kb + it + NSTAGE - 1);
+        if (!(p.dbg & 1)) stage(std::integral_constant<int, (j + NSTAGE - 1) % NSTAGE>{}, kb + it + NSTAGE - 1);
         advance();
       }
-      compute(jc);
+      if (!(p.dbg & 2)) compute(jc);
       ++it;
     };
     // prologue: tiles 0 .. NSTAGE-2 in flight
@@ -351,80 +270,7 @@ __global__ __launch_bounds__(64 * WC * WP, 1) void conv_igemm(ConvParams p) {
     }
   }
 
-  // ---- epilogue ----
-  const int chq = (lane >> 4) * 4;
-  // compile-time (a, b) everywhere: a runtime fragment index would demote acc to scratch
-  static_for<TP>([&](auto bc) __attribute__((always_inline)) {
-    constexpr int b = decltype(bc)::value;
-    const int pix = p0 + wc * WTP + b * 16 + (lane & 15);
-    if (pix >= p.M) return;
-    if (p.splitk > 1) {
-      static_for<TC>([&](auto ac) __attribute__((always_inline)) {
-        constexpr int a = decltype(ac)::value;
-        const int ch = c0 + wr * WTC + a * 16 + chq;
-        float* dst = p.partial + ((long long)z * p.M + pix) * p.npad + ch;
-        *reinterpret_cast<f32x4*>(dst) = acc[a][b];
-      });
-      return;
-    }
-    int n = 0, oh = 0, ow = 0;
-    if (p.bias_mode == BIAS_BORDER9 || p.res_mode == RES_UP2) {
-      const int hw = p.OH * p.OW;
-      n = pix / hw;
-      const int rem = pix - n * hw;
-      oh = rem / p.OW;
-      ow = rem - oh * p.OW;
-    }
-    int bofs = 0;
-    if (p.bias_mode == BIAS_BORDER9) {
-      // class of this output pixel w.r.t. which taps of the (single) 3x3 segment fall
-      // into the zero padding of the folded pre-BN input
-      const ConvSeg& S = p.seg[0];
-      const int ih0 = oh * S.stride - S.pad, iw0 = ow * S.stride - S.pad;
-      const int rc = ih0 < 0 ? 0 : (ih0 + S.KH - 1 >= S.H ? 2 : 1);
-      const int cc = iw0 < 0 ? 0 : (iw0 + S.KW - 1 >= S.W ? 2 : 1);
-      bofs = (rc * 3 + cc) * p.npad;
-    }
-    long long rpix = pix;
-    if (p.res_mode == RES_UP2) rpix = ((long long)n * p.rH + (oh >> 1)) * p.rW + (ow >> 1);
-    static_for<TC>([&](auto ac) __attribute__((always_inline)) {
-      constexpr int a = decltype(ac)::value;
-      const int ch = c0 + wr * WTC + a * 16 + chq;
-      if (ch >= p.cwrite) return;
-      const int nv = min(4, p.cwrite - ch);
-      float v[4] = {acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]};
-      if (p.bias_mode != BIAS_NONE) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] += p.bias[bofs + ch + j];
-      }
-      float sl[4] = {0.f, 0.f, 0.f, 0.f};
-      if (p.act == ACT_PRELU) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) sl[j] = p.slope[ch + j];
-      }
-      if (!p.act_after_res) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = act_apply(v[j], p.act, sl[j]);
-      }
-      if (p.res_mode != RES_NONE) {
-        float r[4] = {0.f, 0.f, 0.f, 0.f};
-        load4<T>(reinterpret_cast<const T*>(p.res) + rpix * p.rcs + ch, r, nv);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] += r[j];
-      }
-      if (p.act_after_res) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = act_apply(v[j], p.act, sl[j]);
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (ch + j >= p.cout) v[j] = 0.f;  // keep channel padding exactly zero
-      if (p.out_f32)
-        store4<float>(reinterpret_cast<float*>(p.y) + (long long)pix * p.ycs + ch, v, nv);
-      else
-        store4<T>(reinterpret_cast<T*>(p.y) + (long long)pix * p.ycs + ch, v, nv);
-    });
-  });
+  conv_epilogue<T, TC, TP, WTC, WTP>(p, acc, c0, p0, wr, wc, lane, z);
 }
 
 // Sum split-K partials, then the same bias/activation epilogue (no residual).

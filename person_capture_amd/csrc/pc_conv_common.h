@@ -1,0 +1,322 @@
+// Device helpers shared by the implicit-GEMM conv kernels (pc_conv.hip,
+// pc_conv_halo.hip): activations, vector load/store, compile-time loops, the
+// XCD-aware workgroup remap, counted vmcnt waits and the fused epilogue.
+#pragma once
+#include <type_traits>
+#include <utility>
+#include <stdint.h>
+#include "pc_common.h"
+
+namespace pc {
+
+__device__ __forceinline__ float act_apply(float v, int act, float slope) {
+  if (act == ACT_RELU) return v > 0.f ? v : 0.f;
+  if (act == ACT_PRELU) return v > 0.f ? v : v * slope;
+  if (act == ACT_SILU) return v / (1.0f + __expf(-v));
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ void store4(T* dst, const float* v, int n);
+
+template <>
+__device__ __forceinline__ void store4<f16>(f16* dst, const float* v, int n) {
+  if (n >= 4) {
+    f16x4 h = {(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
+    *reinterpret_cast<f16x4*>(dst) = h;
+  } else {
+    for (int j = 0; j < n; ++j) dst[j] = (f16)v[j];
+  }
+}
+template <>
+__device__ __forceinline__ void store4<float>(float* dst, const float* v, int n) {
+  if (n >= 4) {
+    *reinterpret_cast<f32x4*>(dst) = f32x4{v[0], v[1], v[2], v[3]};
+  } else {
+    for (int j = 0; j < n; ++j) dst[j] = v[j];
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void load4(const T* src, float* v, int n) {
+  if constexpr (sizeof(T) == 2) {
+    if (n >= 4) {
+      f16x4 h = *reinterpret_cast<const f16x4*>(src);
+      v[0] = (float)h[0]; v[1] = (float)h[1]; v[2] = (float)h[2]; v[3] = (float)h[3];
+      return;
+    }
+  } else {
+    if (n >= 4) {
+      f32x4 h = *reinterpret_cast<const f32x4*>(src);
+      v[0] = h[0]; v[1] = h[1]; v[2] = h[2]; v[3] = h[3];
+      return;
+    }
+  }
+  for (int j = 0; j < n; ++j) v[j] = (float)src[j];
+}
+
+// Compile-time loop: f(integral_constant<int, 0>) ... f(integral_constant<int, N-1>).
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// Workgroup order: the dispatcher deals blocks round-robin over the 8 XCDs (b and
+// b+8 share one), so hand each XCD a contiguous range of tiles; with the channel
+// tile fastest, the channel tiles of one pixel tile share its im2col rows in the
+// same L2. Bijective for any grid size (MI355X_MICROARCH.md, T1).
+__device__ __forceinline__ int xcd_remap(int b, int nwg) {
+  const int xcd = b & 7, idx = b >> 3;
+  const int q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+// s_waitcnt vmcnt(n) with n known only at run time but wave-uniform (per-wave DMA count)
+__device__ __forceinline__ void vmcnt_wait(int n) {
+#define PC_VMW(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+  switch (n) {
+    PC_VMW(0) PC_VMW(1) PC_VMW(2) PC_VMW(3) PC_VMW(4) PC_VMW(5) PC_VMW(6) PC_VMW(7)
+    PC_VMW(8) PC_VMW(9) PC_VMW(10) PC_VMW(11) PC_VMW(12) PC_VMW(13) PC_VMW(14) PC_VMW(15)
+    PC_VMW(16) PC_VMW(17) PC_VMW(18) PC_VMW(19) PC_VMW(20) PC_VMW(21) PC_VMW(22) PC_VMW(23)
+    PC_VMW(24) PC_VMW(25) PC_VMW(26) PC_VMW(27) PC_VMW(28) PC_VMW(29) PC_VMW(30) PC_VMW(31)
+    PC_VMW(32) PC_VMW(33) PC_VMW(34) PC_VMW(35) PC_VMW(36) PC_VMW(37) PC_VMW(38) PC_VMW(39)
+    PC_VMW(40) PC_VMW(41) PC_VMW(42) PC_VMW(43) PC_VMW(44) PC_VMW(45) PC_VMW(46) PC_VMW(47)
+    default: asm volatile("s_waitcnt vmcnt(48)" ::: "memory"); break;
+  }
+#undef PC_VMW
+}
+
+// Fused epilogue shared by the conv kernels: acc[a][b] is the 16x16 fragment of
+// channels c0 + wr*WTC + a*16 + (lane>>4)*4 + j, pixels p0 + wc*WTP + b*16 + (lane&15).
+template <typename T, int TC, int TP, int WTC, int WTP>
+__device__ __forceinline__ void conv_epilogue(const ConvParams& p, f32x4 (&acc)[TC][TP], int c0, int p0, int wr,
+                                              int wc, int lane, int z) {
+  const int chq = (lane >> 4) * 4;
+  // compile-time (a, b) everywhere: a runtime fragment index would demote acc to scratch
+  static_for<TP>([&](auto bc) __attribute__((always_inline)) {
+    constexpr int b = decltype(bc)::value;
+    const int pix = p0 + wc * WTP + b * 16 + (lane & 15);
+    if (pix >= p.M) return;
+    if (p.splitk > 1) {
+      static_for<TC>([&](auto ac) __attribute__((always_inline)) {
+        constexpr int a = decltype(ac)::value;
+        const int ch = c0 + wr * WTC + a * 16 + chq;
+        float* dst = p.partial + ((long long)z * p.M + pix) * p.npad + ch;
+        *reinterpret_cast<f32x4*>(dst) = acc[a][b];
+      });
+      return;
+    }
+    int n = 0, oh = 0, ow = 0;
+    if (p.bias_mode == BIAS_BORDER9 || p.res_mode == RES_UP2) {
+      const int hw = p.OH * p.OW;
+      n = pix / hw;
+      const int rem = pix - n * hw;
+      oh = rem / p.OW;
+      ow = rem - oh * p.OW;
+    }
+    int bofs = 0;
+    if (p.bias_mode == BIAS_BORDER9) {
+      // class of this output pixel w.r.t. which taps of the (single) 3x3 segment fall
+      // into the zero padding of the folded pre-BN input
+      const ConvSeg& S = p.seg[0];
+      const int ih0 = oh * S.stride - S.pad, iw0 = ow * S.stride - S.pad;
+      const int rc = ih0 < 0 ? 0 : (ih0 + S.KH - 1 >= S.H ? 2 : 1);
+      const int cc = iw0 < 0 ? 0 : (iw0 + S.KW - 1 >= S.W ? 2 : 1);
+      bofs = (rc * 3 + cc) * p.npad;
+    }
+    long long rpix = pix;
+    if (p.res_mode == RES_UP2) rpix = ((long long)n * p.rH + (oh >> 1)) * p.rW + (ow >> 1);
+    static_for<TC>([&](auto ac) __attribute__((always_inline)) {
+      constexpr int a = decltype(ac)::value;
+      const int ch = c0 + wr * WTC + a * 16 + chq;
+      if (ch >= p.cwrite) return;
+      const int nv = min(4, p.cwrite - ch);
+      float v[4] = {acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]};
+      if (p.bias_mode != BIAS_NONE) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] += p.bias[bofs + ch + j];
+      }
+      float sl[4] = {0.f, 0.f, 0.f, 0.f};
+      if (p.act == ACT_PRELU) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sl[j] = p.slope[ch + j];
+      }
+      if (!p.act_after_res) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = act_apply(v[j], p.act, sl[j]);
+      }
+      if (p.res_mode != RES_NONE) {
+        float r[4] = {0.f, 0.f, 0.f, 0.f};
+        load4<T>(reinterpret_cast<const T*>(p.res) + rpix * p.rcs + ch, r, nv);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] += r[j];
+      }
+      if (p.act_after_res) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = act_apply(v[j], p.act, sl[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (ch + j >= p.cout) v[j] = 0.f;  // keep channel padding exactly zero
+      if (p.out_f32)
+        store4<float>(reinterpret_cast<float*>(p.y) + (long long)pix * p.ycs + ch, v, nv);
+      else
+        store4<T>(reinterpret_cast<T*>(p.y) + (long long)pix * p.ycs + ch, v, nv);
+    });
+  });
+}
+
+
+// Epilogue through LDS (the kernel's LDS is free once its main loop has drained):
+// the waves write their f32 accumulators into a padded [pixel][channel] image (one
+// or two passes of <= 128 KiB), then every thread finishes 8 channels of one pixel
+// - bias (per channel or border class), activation, residual, zeroed channel
+// padding - and stores them with one 16-byte (f16) or two (f32) stores, so each
+// pixel row of the tile leaves as contiguous bytes and no load waits behind a store.
+template <typename T, int BC, int BP, int WC, int WP>
+__device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, f32x4 (&acc)[BC / WC / 16][BP / WP / 16],
+                                                  int c0, int p0, int wr, int wc, int lane, char* smem) {
+  constexpr int NW = WC * WP, NT = 64 * NW;
+  constexpr int WTC = BC / WC, WTP = BP / WP, TC = WTC / 16, TP = WTP / 16;
+  constexpr bool ONE = BC * BP * 4 <= 131072;
+  constexpr bool SPLIT_C = !ONE && WC >= 2;
+  static_assert(ONE || WC >= 2 || WP >= 2, "epilogue split");
+  constexpr int PC = ONE ? BC : (SPLIT_C ? BC / 2 : BC);
+  constexpr int PP = ONE ? BP : (SPLIT_C ? BP : BP / 2);
+  constexpr int NPASS = ONE ? 1 : 2;
+  constexpr int RS = PC + 4;            // padded row: 16 pixel rows of a fragment hit distinct banks
+  constexpr int CG = PC / 8;            // 8-channel groups per pixel row
+  static_assert(PP * RS * 4 <= 163840, "epilogue image exceeds LDS");
+  static_assert((CG & (CG - 1)) == 0, "channel groups per row must be a power of two");
+  constexpr int ESZ = sizeof(T);
+  const int oesz = p.out_f32 ? 4 : ESZ;
+  const bool vec_ok = ((reinterpret_cast<uintptr_t>(p.y) | (uintptr_t)(p.ycs * oesz)) & 15) == 0 &&
+                      (p.res_mode == RES_NONE ||
+                       ((reinterpret_cast<uintptr_t>(p.res) | (uintptr_t)(p.rcs * ESZ)) & 15) == 0);
+  const int hw = p.OH * p.OW;
+#pragma unroll
+  for (int pass = 0; pass < NPASS; ++pass) {
+    const int cbase = ONE ? 0 : (SPLIT_C ? pass * PC : 0);
+    const int pbase = ONE ? 0 : (SPLIT_C ? 0 : pass * PP);
+    const bool mine = ONE || (SPLIT_C ? (wr / (WC / 2) == pass) : (wc / (WP / 2) == pass));
+    if (mine) {
+      static_for<TC>([&](auto ac) __attribute__((always_inline)) {
+        constexpr int a = decltype(ac)::value;
+        static_for<TP>([&](auto bc) __attribute__((always_inline)) {
+          constexpr int b = decltype(bc)::value;
+          const int cl = wr * WTC + a * 16 + (lane >> 4) * 4 - cbase;
+          const int pl = wc * WTP + b * 16 + (lane & 15) - pbase;
+          *reinterpret_cast<f32x4*>(smem + (pl * RS + cl) * 4) = acc[a][b];
+        });
+      });
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < PP * CG; i += NT) {
+      const int pl = i / CG, cg = i & (CG - 1);
+      const int pix = p0 + pbase + pl;
+      const int ch = c0 + cbase + cg * 8;
+      if (pix >= p.M || ch >= p.cwrite) continue;
+      float v[8];
+      {
+        const f32x4 lo = *reinterpret_cast<const f32x4*>(smem + (pl * RS + cg * 8) * 4);
+        const f32x4 hi = *reinterpret_cast<const f32x4*>(smem + (pl * RS + cg * 8 + 4) * 4);
+        v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+        v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+      }
+      const int nv = min(8, p.cwrite - ch);
+      const bool full = nv == 8 && vec_ok;
+      int n = 0, oh = 0, ow = 0;
+      if (p.bias_mode == BIAS_BORDER9 || p.res_mode == RES_UP2) {
+        n = pix / hw;
+        const int rem = pix - n * hw;
+        oh = rem / p.OW;
+        ow = rem - oh * p.OW;
+      }
+      if (p.bias_mode != BIAS_NONE) {
+        int bofs = 0;
+        if (p.bias_mode == BIAS_BORDER9) {
+          const ConvSeg& S = p.seg[0];
+          const int ih0 = oh * S.stride - S.pad, iw0 = ow * S.stride - S.pad;
+          const int rc = ih0 < 0 ? 0 : (ih0 + S.KH - 1 >= S.H ? 2 : 1);
+          const int cc = iw0 < 0 ? 0 : (iw0 + S.KW - 1 >= S.W ? 2 : 1);
+          bofs = (rc * 3 + cc) * p.npad;
+        }
+        const float* bp = p.bias + bofs + ch;   // bias arrays span npad >= ch + 8
+        const f32x4 b0 = *reinterpret_cast<const f32x4*>(bp);
+        const f32x4 b1 = *reinterpret_cast<const f32x4*>(bp + 4);
+        v[0] += b0[0]; v[1] += b0[1]; v[2] += b0[2]; v[3] += b0[3];
+        v[4] += b1[0]; v[5] += b1[1]; v[6] += b1[2]; v[7] += b1[3];
+      }
+      float sl[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (p.act == ACT_PRELU) {
+        const f32x4 s0 = *reinterpret_cast<const f32x4*>(p.slope + ch);
+        const f32x4 s1 = *reinterpret_cast<const f32x4*>(p.slope + ch + 4);
+        sl[0] = s0[0]; sl[1] = s0[1]; sl[2] = s0[2]; sl[3] = s0[3];
+        sl[4] = s1[0]; sl[5] = s1[1]; sl[6] = s1[2]; sl[7] = s1[3];
+      }
+      if (!p.act_after_res) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j], p.act, sl[j]);
+      }
+      if (p.res_mode != RES_NONE) {
+        long long rpix = pix;
+        if (p.res_mode == RES_UP2) rpix = ((long long)n * p.rH + (oh >> 1)) * p.rW + (ow >> 1);
+        const T* rp = reinterpret_cast<const T*>(p.res) + rpix * p.rcs + ch;
+        if (full) {
+          if constexpr (ESZ == 2) {
+            const f16x8 r = *reinterpret_cast<const f16x8*>(rp);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] += (float)r[j];
+          } else {
+            const f32x4 r0 = *reinterpret_cast<const f32x4*>(rp);
+            const f32x4 r1 = *reinterpret_cast<const f32x4*>(rp + 4);
+            v[0] += r0[0]; v[1] += r0[1]; v[2] += r0[2]; v[3] += r0[3];
+            v[4] += r1[0]; v[5] += r1[1]; v[6] += r1[2]; v[7] += r1[3];
+          }
+        } else {
+          for (int j = 0; j < nv; ++j) v[j] += (float)rp[j];
+        }
+      }
+      if (p.act_after_res) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j], p.act, sl[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (ch + j >= p.cout) v[j] = 0.f;   // keep channel padding exactly zero
+      if (p.out_f32) {
+        float* yp = reinterpret_cast<float*>(p.y) + (long long)pix * p.ycs + ch;
+        if (full) {
+          *reinterpret_cast<f32x4*>(yp) = f32x4{v[0], v[1], v[2], v[3]};
+          *reinterpret_cast<f32x4*>(yp + 4) = f32x4{v[4], v[5], v[6], v[7]};
+        } else {
+          for (int j = 0; j < nv; ++j) yp[j] = v[j];
+        }
+      } else {
+        T* yp = reinterpret_cast<T*>(p.y) + (long long)pix * p.ycs + ch;
+        if constexpr (ESZ == 2) {
+          if (full) {
+            *reinterpret_cast<f16x8*>(yp) = f16x8{(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3],
+                                                  (f16)v[4], (f16)v[5], (f16)v[6], (f16)v[7]};
+          } else {
+            for (int j = 0; j < nv; ++j) yp[j] = (T)v[j];
+          }
+        } else {
+          if (full) {
+            *reinterpret_cast<f32x4*>(yp) = f32x4{v[0], v[1], v[2], v[3]};
+            *reinterpret_cast<f32x4*>(yp + 4) = f32x4{v[4], v[5], v[6], v[7]};
+          } else {
+            for (int j = 0; j < nv; ++j) yp[j] = v[j];
+          }
+        }
+      }
+    }
+    if (pass + 1 < NPASS) __syncthreads();
+  }
+}
+
+}  // namespace pc
