@@ -333,7 +333,8 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl) {
     const NetTensor& X = n->tens[w[3]];
     const int KH = w[4], KW = w[5], st = w[6], pd = w[7];
     const char* e = getenv("PC_CONV_HALO");
-    const int force = e ? atoi(e) : -1;
+    // a forced igemm tile (PC_CONV_CFG) without PC_CONV_HALO means "test that tile"
+    const int force = e ? atoi(e) : (getenv("PC_CONV_CFG") ? 0 : -1);
     const bool ok = nseg == 1 && pl.splitk == 1 && st == 1 && KH == KW && pd * 2 + 1 == KH && X.H == Y.H &&
                     X.W == Y.W && KH * KW <= 32 && (double)M * X.cs * esz < 4294967296.0 - 65536.0 && force != 0;
     if (ok) {

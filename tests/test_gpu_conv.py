@@ -58,13 +58,17 @@ CASES = [
 ]
 
 
-ALL_CFGS = [None] + [f"{c}{r}" for c in range(14) for r in ("", ":64")]
+ALL_CFGS = [None] + [f"{c}{r}" for c in range(14) for r in ("", ":64")] + [f"h{k}" for k in range(5)]
 
 
 def _set_cfg(monkeypatch, cfg):
     """cfg = "<tile id>[:64]": PC_CONV_CFG forces the tile where its channel tile divides
-    npad (otherwise the planner's choice runs); ":64" forces 64-byte K-tiles."""
+    npad (otherwise the planner's choice runs) and turns the halo kernel off; ":64" forces
+    64-byte K-tiles. cfg = "h<k>" forces halo tile k where it applies."""
     if cfg is None:
+        return
+    if cfg.startswith("h"):   # halo kernel tile k (pc_conv_halo.hip), stride-1 "same" convs only
+        monkeypatch.setenv("PC_CONV_HALO", str(int(cfg[1:]) + 1))
         return
     c, _, rowb = cfg.partition(":")
     monkeypatch.setenv("PC_CONV_CFG", c)

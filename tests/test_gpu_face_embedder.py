@@ -78,6 +78,7 @@ def test_face_embedder_end_to_end(gpu_ctx, monkeypatch, prec, tol_box, tol_count
     unmatched faces per frame, boxes within `tol_box`."""
     monkeypatch.setenv("PERSON_CAPTURE_AMD_PRECISION", prec)
     fe = fe_mod.FaceEmbedder(ctx="cuda:0", yolo_model="scrfd_10g_bnkps", conf=0.5)
+    fe.debug_chips = True   # f16: a chip that differs from the oracle's was re-aligned, not mis-embedded
     frames = _frames()
     bank = _bank()
     got_all = fe.extract_batch(frames, bank=DeviceBank(fe._ctx, bank))
