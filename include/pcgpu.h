@@ -135,6 +135,9 @@ int pc_net_set_graph(pc_net* net, int enable);
  * read: [0] conv ms, [1] conv launches, [2] conv FLOPs (algorithmic), [3] other ms, [4] other launches */
 int pc_net_profile(pc_net* net, int enable);
 int pc_net_profile_read(pc_net* net, double* h_out5);
+/* Per-launch detail of the profiled runs, 6 doubles per record: op index, op kind, ms, FLOPs,
+   kernel (100+k: static-schedule tile k, k >= 0: halo tile k, -1: generic implicit-GEMM), implicit-GEMM tile. Returns the record count (<0: -status). */
+int pc_net_profile_ops(pc_net* net, double* h_out, int max_recs);
 
 /* ---- image kernels ---- */
 int pc_letterbox(pc_ctx* ctx, int precision, const pc_letterbox_desc* h_descs, int n, int D, void* d_out);

@@ -73,6 +73,7 @@ SIGNATURES = {
     "pc_net_set_graph": ([_P, _I], _I),
     "pc_net_profile": ([_P, _I], _I),
     "pc_net_profile_read": ([_P, C.POINTER(C.c_double)], _I),
+    "pc_net_profile_ops": ([_P, C.POINTER(C.c_double), _I], _I),
     "pc_letterbox": ([_P, _I, C.POINTER(LetterboxDesc), _I, _I, _P], _I),
     "pc_warp_affine": ([_P, C.POINTER(WarpDesc), _I], _I),
     "pc_resize_linear": ([_P, C.POINTER(ResizeDesc), _I], _I),

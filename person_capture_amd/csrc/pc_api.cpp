@@ -20,6 +20,10 @@
 namespace pc {
 hipError_t conv_launch(int f32, int rowb, int cfg, const ConvParams& p, hipStream_t s);
 hipError_t conv_halo_launch(int f32, int cfg, const ConvParams& p, hipStream_t s);
+hipError_t conv_fast_launch(int f32, int rowb, int cfg, const ConvParams& p, hipStream_t s);
+int conv_fast_num_cfgs();
+int conv_fast_tile(int cfg, int* bc, int* bp);
+int conv_fast_valid(int cfg, int rowb);
 int conv_halo_num_cfgs();
 int conv_halo_tile(int cfg, int* bc, int* bp);
 int conv_halo_fits(int cfg, int KH, int KW, int W);
@@ -209,7 +213,7 @@ enum { OP_CONV = 1, OP_STEM = 2, OP_MAXPOOL = 3 };
 struct NetBuf { long long elems; int is_f32; void* d = nullptr; };
 struct NetTensor { int buf, H, W, C, cs, coff, is_f32; };
 struct NetOp { int w[32]; };
-struct ConvPlan { int rowb, cfg, splitk, halo = -1; long long M_per_image; double flops_per_image; };
+struct ConvPlan { int rowb, cfg, splitk, halo = -1, fast = -1; long long M_per_image; double flops_per_image; };
 // A stem (tiny Cin) runs as im2col + a 1x1 MFMA conv over 32-element K rows.
 struct StemPlan {
   int use_mfma = 0, npad = 0, cfg = 0, rowb = 0, cin_true = 0;
@@ -217,7 +221,7 @@ struct StemPlan {
   float* bias = nullptr;    // [npad]
   float* slope = nullptr;   // [npad] or null
 };
-struct ProfRec { int a, b, kind; double flops; };
+struct ProfRec { int a, b, kind; double flops; int op = -1; };
 
 struct pc_net {
   pc_ctx* ctx = nullptr;
@@ -358,6 +362,39 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl) {
       }
       pl.halo = hc;
       if (hc >= 0) pl.rowb = 64;   // the halo kernel steps K by one 64-byte LDS row
+    }
+  }
+  // The statically scheduled kernel (pc_conv_fast.hip) takes every conv it can run:
+  // no split-K, offsets within 32 bits. Tile choice: fewest rounds of workgroups over
+  // the 256 CUs (one workgroup per CU), then the per-tile cost factor measured on
+  // MI355X (bigger wave tiles stage fewer LDS bytes per MFMA).
+  // PC_CONV_FAST=0 disables, =k+1 forces tile k.
+  pl.fast = -1;
+  {
+    const char* e = getenv("PC_CONV_FAST");
+    const int force = e ? atoi(e) : ((getenv("PC_CONV_CFG") || getenv("PC_CONV_HALO")) ? 0 : -1);
+    bool ok = pl.splitk == 1 && force != 0;
+    for (int sg = 0; sg < nseg && ok; ++sg) {
+      const NetTensor& X = n->tens[w[3 + 5 * sg]];
+      if ((double)X.H * X.W * n->max_batch * X.cs * esz + kZeroTail >= 4294967296.0) ok = false;
+    }
+    if ((double)npad * w[15] * esz >= 4294967296.0) ok = false;
+    if (ok) {
+      static const double cost[] = {1.0, 1.12, 1.12, 1.3, 1.3, 1.3, 1.15, 1.45, 1.3};
+      int best = -1;
+      double best_t = 0;
+      for (int k = 0; k < conv_fast_num_cfgs(); ++k) {
+        int bc = 0, bp = 0;
+        conv_fast_tile(k, &bc, &bp);
+        if (npad % bc || !conv_fast_valid(k, rowb)) continue;
+        if (force > 0 && k != force - 1) continue;
+        const long long t = (M + bp - 1) / bp * (npad / bc);
+        const double rounds = (double)((t + 255) / 256);
+        const double est = rounds * bc * bp * cost[k];
+        if (best < 0 || est < best_t) { best = k; best_t = est; }
+      }
+      pl.fast = best;
+      if (best >= 0) { pl.halo = -1; pl.rowb = rowb; }
     }
   }
   if (Y.C > npad) return fail(n->ctx, PC_ERR_FORMAT, "conv output tensor wider than npad");
@@ -592,7 +629,7 @@ static int run_ops(pc_net* n, int N) {
     HIPCHK(c, hipMemcpyAsync(n->in_copy, n->cur_input, n->in_img_bytes * N, hipMemcpyDeviceToDevice, s));
   for (size_t i = 0; i < n->ops.size(); ++i) {
     const int* w = n->ops[i].w;
-    ProfRec rec{-1, -1, w[0], w[0] == OP_CONV ? n->plans[i].flops_per_image * N : 0.0};
+    ProfRec rec{-1, -1, w[0], w[0] == OP_CONV ? n->plans[i].flops_per_image * N : 0.0, (int)i};
     if (prof) { int rc = prof_event(n, &rec.a); if (rc) return rc; }
     if (w[0] == OP_CONV) {
       const ConvPlan& pl = n->plans[i];
@@ -638,7 +675,9 @@ static int run_ops(pc_net* n, int N) {
       p.partial = n->partial;
       p.zero = c->zero;
       if (const char* e = getenv("PC_CONV_DBG")) p.dbg = atoi(e);
-      if (pl.halo >= 0) {
+      if (pl.fast >= 0) {
+        HIPCHK(c, conv_fast_launch(n->f32, pl.rowb, pl.fast, p, s));
+      } else if (pl.halo >= 0) {
         HIPCHK(c, conv_halo_launch(n->f32, pl.halo, p, s));
       } else {
         HIPCHK(c, conv_launch(n->f32, pl.rowb, pl.cfg, p, s));
@@ -672,7 +711,7 @@ static int run_ops(pc_net* n, int N) {
           int rc = prof_event(n, &rec.b);
           if (rc) return rc;
           n->recs.push_back(rec);
-          rec = ProfRec{-1, -1, OP_CONV, n->plans[i].flops_per_image * N};
+          rec = ProfRec{-1, -1, OP_CONV, n->plans[i].flops_per_image * N, (int)i};
           rc = prof_event(n, &rec.a);
           if (rc) return rc;
         }
@@ -734,6 +773,25 @@ extern "C" int pc_net_profile_read(pc_net* n, double* out) {
   }
   out[0] = conv_ms; out[1] = conv_n; out[2] = flops; out[3] = other_ms; out[4] = other_n;
   return PC_OK;
+}
+
+// Per-record detail of the profiled runs: 6 doubles per record
+// [op index, kind, ms, flops, kernel (100+k fast tile k, k halo tile k, -1 igemm), igemm cfg]; returns the count.
+extern "C" int pc_net_profile_ops(pc_net* n, double* out, int max_recs) {
+  if (!n || !out) return -PC_ERR_ARG;
+  HIPCHK(n->ctx, hipStreamSynchronize(n->ctx->stream));
+  int k = 0;
+  for (const ProfRec& r : n->recs) {
+    if (k >= max_recs) break;
+    float ms = 0.f;
+    HIPCHK(n->ctx, hipEventElapsedTime(&ms, n->ev_pool[r.a], n->ev_pool[r.b]));
+    double* o = out + 6 * k++;
+    const bool conv = r.op >= 0 && n->ops[r.op].w[0] == OP_CONV;
+    o[0] = r.op; o[1] = r.kind; o[2] = ms; o[3] = r.flops;
+    o[4] = conv ? (n->plans[r.op].fast >= 0 ? 100 + n->plans[r.op].fast : n->plans[r.op].halo) : -1;
+    o[5] = conv ? n->plans[r.op].cfg : -1;
+  }
+  return k;
 }
 
 extern "C" int pc_net_run(pc_net* n, const void* d_in, int N) {

@@ -1,0 +1,312 @@
+// Statically scheduled implicit-GEMM convolution (gfx950).
+//
+// Same math, layouts and fused epilogue as conv_igemm (pc_conv.hip), but the
+// K loop carries no data-dependent control flow, because the generic kernel's loop
+// was measured to be scalar-issue bound (≈400 SALU + ≈90 branches per K-step from
+// a run-time vmcnt switch and the nested tap iterator, ≈2.9k cycles per step against
+// a 1k-cycle MFMA floor):
+//
+//  * every wave issues exactly NI = NIA + NIB LDS-DMA instructions per K-tile
+//    (static_assert'ed tile shapes), and the loop always issues a tile - past the
+//    last real tile it re-issues the last one into the ring slot nobody reads - so
+//    the wait before each barrier is one compile-time s_waitcnt vmcnt((NSTAGE-2)*NI);
+//  * the K-tile iterator (segment, tap row/col, channel block) advances with scalar
+//    selects; the per-lane im2col source offset is recomputed every step from a
+//    per-row window origin (≈6 VALU per staged row: bounds test, tap shift, select of
+//    the zero-tail offset), so tap changes need no branch. The only branch in the
+//    loop is the (once per launch) switch to the second K-segment;
+//  * one raw s_barrier per K-tile; the DMA for tile k+NSTAGE-1 is issued right after
+//    it and overlaps the MFMAs of tile k (cdna_hip_programming.md "Pipelining across
+//    barriers"); the loop is unrolled by NSTAGE so every LDS address is static.
+//
+// LDS rows are ROWB bytes (one tap x ROWB of channels for the im2col side, one
+// output channel x ROWB of K for the weights); 16-byte chunk c of row r sits at
+// c ^ ((r >> 1) & (CHUNKS - 1)) - bank-conflict-free ds_read_b128 fragment reads.
+#include "pc_conv_common.h"
+
+namespace pc {
+
+template <int BC, int BP, int WC, int WP>
+__host__ __device__ constexpr int fast_epi_bytes() {
+  // LDS image of conv_epilogue_lds (one or two passes)
+  return BC * BP * 4 <= 131072 ? BP * (BC + 4) * 4
+                               : (WC >= 2 ? BP * (BC / 2 + 4) * 4 : (BP / 2) * (BC + 4) * 4);
+}
+
+template <typename T, int BC, int BP, int ROWB, int WC, int WP, int NSTAGE>
+__global__ __launch_bounds__(64 * WC * WP, 1) void conv_fast(ConvParams p) {
+  constexpr int NW = WC * WP;
+  constexpr int ESZ = sizeof(T);
+  constexpr int CHUNKS = ROWB / 16;
+  constexpr int BKE = ROWB / ESZ;             // K elements per tile
+  constexpr int RPI = 1024 / ROWB;            // LDS rows per DMA wave-instruction
+  constexpr int NA = BC / RPI, NB = BP / RPI; // DMA instructions per tile (weights, im2col)
+  static_assert(NA % NW == 0 && NB % NW == 0, "every wave must issue the same DMA count");
+  constexpr int NIA = NA / NW, NIB = NB / NW, NI = NIA + NIB;
+  constexpr int WTC = BC / WC, WTP = BP / WP;
+  constexpr int TC = WTC / 16, TP = WTP / 16;
+  constexpr int BUF = (BC + BP) * ROWB;
+  constexpr int RING = NSTAGE * BUF;
+  constexpr int EPI = fast_epi_bytes<BC, BP, WC, WP>();
+  constexpr int SMEM = RING > EPI ? RING : EPI;
+  static_assert(SMEM <= 163840, "LDS");
+  static_assert(WTC % 16 == 0 && WTP % 16 == 0, "wave tile");
+  static_assert(NSTAGE >= 2, "ring depth");
+
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  __builtin_assume(wave >= 0 && wave < NW);
+  const int wr = wave / WP, wc = wave % WP;
+  const int nct = p.npad / BC;
+  const int npt = (p.M + BP - 1) / BP;
+  const int tile = xcd_remap(blockIdx.x, nct * npt);
+  const int p0 = (tile / nct) * BP;
+  const int c0 = (tile % nct) * BC;
+  const int nk = p.kt_total;
+
+  // ---- staging geometry ----
+  const int lrow = lane / CHUNKS, pchunk = lane % CHUNKS;
+  unsigned woff[NIA];
+  static_for<NIA>([&](auto ic) __attribute__((always_inline)) {
+    constexpr int i = decltype(ic)::value;
+    const int r = (i * NW + wave) * RPI + lrow;
+    woff[i] = (unsigned)((long long)(c0 + r) * p.ktot * ESZ) + ((pchunk ^ ((r >> 1) & (CHUNKS - 1))) << 4);
+  });
+  // im2col rows: window origin (ih0, iw0) and byte offset of the staged row's output
+  // pixel under the current segment (recomputed from the pixel index at a segment switch)
+  int b_ih[NIB], b_iw[NIB];
+  unsigned b_base[NIB];
+  unsigned b_zero;   // zero tail + a chunk offset (any 16 zero bytes do; the tail is wider than a row)
+  // current issue segment (scalars)
+  const char* sx;
+  int sH, sW, scs, sKW, scblk;
+  auto load_seg = [&](const ConvSeg& S) __attribute__((always_inline)) {
+    sx = reinterpret_cast<const char*>(S.x);
+    sH = S.H; sW = S.W; scs = S.cs; sKW = S.KW; scblk = S.cblk;
+    const int hw = p.OH * p.OW;
+    static_for<NIB>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = decltype(ic)::value;
+      const int r = (i * NW + wave) * RPI + lrow;
+      const unsigned lc = (unsigned)((pchunk ^ ((r >> 1) & (CHUNKS - 1))) << 4);
+      const int q = p0 + r;
+      const int n = q / hw, rem = q - n * hw;
+      const int oh = q < p.M ? rem / p.OW : -(1 << 16);   // rows past M never pass the bounds test
+      const int ow = rem - (rem / p.OW) * p.OW;
+      b_ih[i] = oh * S.stride - S.pad;
+      b_iw[i] = ow * S.stride - S.pad;
+      b_base[i] = (unsigned)((n * S.H + b_ih[i]) * S.W + b_iw[i]) * (unsigned)(S.cs * ESZ) + lc;
+      if constexpr (i == 0) b_zero = S.zero_off + lc;
+    });
+  };
+  load_seg(p.seg[0]);
+  int iseg = 0, ith = 0, itw = 0, icb = 0;
+  const int seg0_kh = p.seg[0].KH;
+  const char* wsrc = reinterpret_cast<const char*>(p.w);
+
+  // DMA of the current iterator position (K-tile index kt) into ring slot `slot`
+  auto issue = [&](auto slotc, int kt) __attribute__((always_inline)) {
+    constexpr int slot = decltype(slotc)::value;
+    const char* wb = wsrc + (long long)kt * ROWB;
+    static_for<NIA>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = decltype(ic)::value;
+      unsigned off = woff[i];
+      asm volatile("" : "+v"(off));
+      __builtin_amdgcn_global_load_lds((gptr_t)(wb + off), (lds_ptr_t)(smem + slot * BUF + (i * NW + wave) * 1024),
+                                       16, 0, 0);
+    });
+    const char* xb = sx + icb * ROWB;
+    const unsigned tapoff = (unsigned)((ith * sW + itw) * scs * ESZ);
+    static_for<NIB>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = decltype(ic)::value;
+      const bool ok = (unsigned)(b_ih[i] + ith) < (unsigned)sH && (unsigned)(b_iw[i] + itw) < (unsigned)sW;
+      unsigned off = ok ? b_base[i] + tapoff : b_zero;
+      asm volatile("" : "+v"(off));
+      __builtin_amdgcn_global_load_lds((gptr_t)(xb + off),
+                                       (lds_ptr_t)(smem + slot * BUF + BC * ROWB + (i * NW + wave) * 1024), 16, 0, 0);
+    });
+  };
+  // advance the issue iterator by one K-tile (no-op once the last tile was issued)
+  auto advance = [&](bool more) __attribute__((always_inline)) {
+    if (!more) return;
+    const int cb1 = icb + 1;
+    const bool w1 = cb1 == scblk;
+    icb = w1 ? 0 : cb1;
+    const int tw1 = itw + (w1 ? 1 : 0);
+    const bool w2 = tw1 == sKW;
+    itw = w2 ? 0 : tw1;
+    ith += w2 ? 1 : 0;
+    if (iseg == 0 && ith == seg0_kh) {   // once per launch, 2-segment convs only
+      iseg = 1;
+      ith = 0;
+      load_seg(p.seg[1]);
+    }
+  };
+
+  f32x4 acc[TC][TP];
+#pragma unroll
+  for (int a = 0; a < TC; ++a)
+#pragma unroll
+    for (int b = 0; b < TP; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  constexpr int KSTEPS = ESZ == 2 ? BKE / 32 : BKE / 4;
+  const int fr = lane & 15;
+  const int sw = (fr >> 1) & (CHUNKS - 1);
+  const unsigned a_row = (wr * WTC + fr) * ROWB;
+  const unsigned b_row = (BC + wc * WTP + fr) * ROWB;
+  auto compute = [&](auto slotc) __attribute__((always_inline)) {
+    constexpr int slot = decltype(slotc)::value;
+    const char* base = smem + slot * BUF;
+#pragma unroll
+    for (int ks = 0; ks < KSTEPS; ++ks) {
+      if constexpr (ESZ == 2) {
+        const unsigned ko = ((ks * 4 + (lane >> 4)) ^ sw) << 4;
+        f16x8 fa[TC], fb[TP];
+#pragma unroll
+        for (int t = 0; t < TC; ++t) fa[t] = *reinterpret_cast<const f16x8*>(base + a_row + ko + t * 16 * ROWB);
+#pragma unroll
+        for (int t = 0; t < TP; ++t) fb[t] = *reinterpret_cast<const f16x8*>(base + b_row + ko + t * 16 * ROWB);
+#pragma unroll
+        for (int a = 0; a < TC; ++a)
+#pragma unroll
+          for (int b = 0; b < TP; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[a], fb[b], acc[a][b], 0, 0, 0);
+        // 128x64 wave tiles: keep the next k-substep's fragment reads behind these MFMAs
+        // (hoisting all of them needs 96 fragment VGPRs beside 128 accumulators -> spills)
+        if constexpr (TC * TP >= 32) __builtin_amdgcn_sched_barrier(0);
+      } else {
+        // f32: K-substep ks is the 16-byte chunk ks (4 floats), lane group selects the float
+        const unsigned kof = ((ks ^ sw) << 4) + ((lane >> 4) << 2);
+        float fa[TC], fb[TP];
+#pragma unroll
+        for (int t = 0; t < TC; ++t) fa[t] = *reinterpret_cast<const float*>(base + a_row + kof + t * 16 * ROWB);
+#pragma unroll
+        for (int t = 0; t < TP; ++t) fb[t] = *reinterpret_cast<const float*>(base + b_row + kof + t * 16 * ROWB);
+#pragma unroll
+        for (int a = 0; a < TC; ++a)
+#pragma unroll
+          for (int b = 0; b < TP; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[a], fb[b], acc[a][b], 0, 0, 0);
+      }
+    }
+  };
+  auto bar = [&]() __attribute__((always_inline)) {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  // ---- prologue: tiles 0 .. NSTAGE-2 in flight ----
+  int kiss = 0;   // next K-tile index the iterator points at
+  static_for<NSTAGE - 1>([&](auto jc) __attribute__((always_inline)) {
+    constexpr int j = decltype(jc)::value;
+    issue(std::integral_constant<int, j>{}, kiss);
+    const bool more = kiss + 1 < nk;
+    advance(more);
+    kiss += more ? 1 : 0;
+  });
+  // one step: retire tile `it`, refill the slot of tile it-1 with tile it+NSTAGE-1
+  auto step = [&](auto jc) __attribute__((always_inline)) {
+    constexpr int j = decltype(jc)::value;
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NSTAGE - 2) * NI) : "memory");
+    bar();
+    issue(std::integral_constant<int, (j + NSTAGE - 1) % NSTAGE>{}, kiss);
+    const bool more = kiss + 1 < nk;
+    advance(more);
+    kiss += more ? 1 : 0;
+    compute(std::integral_constant<int, j>{});
+  };
+  int it = 0;
+  for (; it + NSTAGE <= nk; it += NSTAGE)
+    static_for<NSTAGE>([&](auto jc) __attribute__((always_inline)) { step(jc); });
+  static_for<NSTAGE - 1>([&](auto jc) __attribute__((always_inline)) {
+    if (it + decltype(jc)::value < nk) step(jc);
+  });
+
+  // drain the (dummy) tail DMAs and every wave's last reads before the LDS is reused
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if constexpr (((BC / 8) & (BC / 8 - 1)) == 0 && ((BC / 16) & (BC / 16 - 1)) == 0)
+    conv_epilogue_lds<T, BC, BP, WC, WP>(p, acc, c0, p0, wr, wc, lane, smem);
+  else   // 96 / 224 channel tiles: per-fragment stores
+    conv_epilogue<T, TC, TP, WTC, WTP>(p, acc, c0, p0, wr, wc, lane, 0);
+}
+
+// tile shapes whose DMA count divides evenly over the waves at this row width
+template <int BC, int BP, int ROWB, int NW>
+constexpr bool fast_valid() {
+  return (BC / (1024 / ROWB)) % NW == 0 && (BP / (1024 / ROWB)) % NW == 0;
+}
+
+// ---------------------------------------------------------------------------
+// host side: tile table (keep kFastCfgs and launch_fast_t in sync)
+// ---------------------------------------------------------------------------
+struct FastCfg { int bc, bp, nw; };
+static const FastCfg kFastCfgs[] = {
+    {256, 256, 8},   // 0: 2x4 waves, 128x64 per wave, 2 stages
+    {128, 256, 8},   // 1: 2x4 waves, 64x64 per wave, 3 stages (ROWB 64: 4)
+    {256, 128, 8},   // 2: 4x2 waves, 64x64 per wave, 3 stages
+    {128, 128, 4},   // 3: 2x2 waves, 64x64 per wave, 3 stages
+    {64, 256, 4},    // 4: 1x4 waves, 64x64 per wave, 3 stages
+    {96, 256, 4},    // 5: 1x4 waves, 96x64 per wave, 3 stages
+    {64, 512, 8},    // 6: 1x8 waves, 64x64 per wave, 3 stages
+    {32, 256, 4},    // 7: 1x4 waves, 32x64 per wave, 3 stages
+    {224, 128, 4},   // 8: 2x2 waves, 112x64 per wave, 2 stages
+};
+static const int kNumFastCfgs = sizeof(kFastCfgs) / sizeof(kFastCfgs[0]);
+
+int conv_fast_num_cfgs() { return kNumFastCfgs; }
+
+int conv_fast_tile(int cfg, int* bc, int* bp) {
+  if (cfg < 0 || cfg >= kNumFastCfgs) return 0;
+  *bc = kFastCfgs[cfg].bc;
+  *bp = kFastCfgs[cfg].bp;
+  return 1;
+}
+
+template <typename T, int BC, int BP, int ROWB, int WC, int WP, int NSTAGE>
+static hipError_t launch_fast_cfg(const ConvParams& p, hipStream_t s) {
+  if constexpr (!fast_valid<BC, BP, ROWB, WC * WP>()) {
+    return hipErrorInvalidValue;
+  } else {
+    const int nwg = (p.M + BP - 1) / BP * (p.npad / BC);
+    hipLaunchKernelGGL((conv_fast<T, BC, BP, ROWB, WC, WP, NSTAGE>), dim3(nwg), dim3(64 * WC * WP), 0, s, p);
+    return hipGetLastError();
+  }
+}
+
+template <typename T, int ROWB>
+static hipError_t launch_fast_t(const ConvParams& p, int cfg, hipStream_t s) {
+  constexpr int S3 = ROWB == 128 ? 3 : 4;
+  switch (cfg) {
+    case 0: return launch_fast_cfg<T, 256, 256, ROWB, 2, 4, ROWB == 128 ? 2 : 4>(p, s);
+    case 1: return launch_fast_cfg<T, 128, 256, ROWB, 2, 4, S3>(p, s);
+    case 2: return launch_fast_cfg<T, 256, 128, ROWB, 4, 2, S3>(p, s);
+    case 3: return launch_fast_cfg<T, 128, 128, ROWB, 2, 2, S3>(p, s);
+    case 4: return launch_fast_cfg<T, 64, 256, ROWB, 1, 4, S3>(p, s);
+    case 5: return launch_fast_cfg<T, 96, 256, ROWB, 1, 4, S3>(p, s);
+    case 6: return launch_fast_cfg<T, 64, 512, ROWB, 1, 8, ROWB == 128 ? 2 : 4>(p, s);
+    case 7: return launch_fast_cfg<T, 32, 256, ROWB, 1, 4, S3>(p, s);
+    case 8: return launch_fast_cfg<T, 224, 128, ROWB, 2, 2, S3>(p, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// can cfg run convs whose K rows are rowb bytes?
+int conv_fast_valid(int cfg, int rowb) {
+  if (cfg < 0 || cfg >= kNumFastCfgs || (rowb != 64 && rowb != 128)) return 0;
+  const FastCfg& c = kFastCfgs[cfg];
+  const int rpi = 1024 / rowb;
+  return (c.bc / rpi) % c.nw == 0 && (c.bp / rpi) % c.nw == 0;
+}
+
+hipError_t conv_fast_launch(int f32, int rowb, int cfg, const ConvParams& p, hipStream_t s) {
+  if (cfg < 0 || cfg >= kNumFastCfgs || p.splitk != 1 || p.npad % kFastCfgs[cfg].bc || p.nseg < 1 || p.nseg > 2 ||
+      (rowb != 64 && rowb != 128))
+    return hipErrorInvalidValue;
+  if (f32) return rowb == 128 ? launch_fast_t<float, 128>(p, cfg, s) : launch_fast_t<float, 64>(p, cfg, s);
+  return rowb == 128 ? launch_fast_t<f16, 128>(p, cfg, s) : launch_fast_t<f16, 64>(p, cfg, s);
+}
+
+}  // namespace pc

@@ -151,6 +151,14 @@ class Net:
         return {"conv_ms": out[0], "conv_launches": int(out[1]), "conv_flops": out[2], "other_ms": out[3],
                 "other_launches": int(out[4])}
 
+    def profile_ops(self, max_recs: int = 65536) -> np.ndarray:
+        """[n][6]: op index, kind, ms, flops, halo tile (-1 = igemm), igemm tile (profiled runs)."""
+        out = (C.c_double * (6 * max_recs))()
+        k = self.ctx.lib.pc_net_profile_ops(self.handle, out, max_recs)
+        if k < 0:
+            check(-k, self.ctx.handle, "profile_ops")
+        return np.frombuffer(out, dtype=np.float64, count=6 * k).reshape(k, 6).copy()
+
     def run(self, d_input: int, batch: int) -> None:
         check(self.ctx.lib.pc_net_run(self.handle, C.c_void_p(int(d_input)), int(batch)), self.ctx.handle, "net_run")
 

@@ -58,19 +58,26 @@ CASES = [
 ]
 
 
-ALL_CFGS = [None] + [f"{c}{r}" for c in range(14) for r in ("", ":64")] + [f"h{k}" for k in range(5)]
+ALL_CFGS = ([None] + [f"{c}{r}" for c in range(14) for r in ("", ":64")] + [f"h{k}" for k in range(5)]
+            + [f"f{k}{r}" for k in range(9) for r in ("", ":64")])
 
 
 def _set_cfg(monkeypatch, cfg):
     """cfg = "<tile id>[:64]": PC_CONV_CFG forces the tile where its channel tile divides
     npad (otherwise the planner's choice runs) and turns the halo kernel off; ":64" forces
-    64-byte K-tiles. cfg = "h<k>" forces halo tile k where it applies."""
+    64-byte K-tiles. cfg = "h<k>" forces halo tile k where it applies, "f<k>[:64]" the
+    static-schedule tile k (where its channel tile divides npad)."""
     if cfg is None:
         return
     if cfg.startswith("h"):   # halo kernel tile k (pc_conv_halo.hip), stride-1 "same" convs only
         monkeypatch.setenv("PC_CONV_HALO", str(int(cfg[1:]) + 1))
         return
     c, _, rowb = cfg.partition(":")
+    if c.startswith("f"):     # static-schedule kernel tile k (pc_conv_fast.hip)
+        monkeypatch.setenv("PC_CONV_FAST", str(int(c[1:]) + 1))
+        if rowb:
+            monkeypatch.setenv("PC_CONV_ROWB", rowb)
+        return
     monkeypatch.setenv("PC_CONV_CFG", c)
     if rowb:
         monkeypatch.setenv("PC_CONV_ROWB", rowb)

@@ -55,8 +55,16 @@ def main():
                 os.environ["PC_CONV_ROWB"] = rowb
             else:
                 os.environ.pop("PC_CONV_ROWB", None)
-            if c == "auto":
+            os.environ.pop("PC_CONV_HALO", None)
+            os.environ.pop("PC_CONV_FAST", None)
+            if c.startswith("f"):
                 os.environ.pop("PC_CONV_CFG", None)
+                os.environ["PC_CONV_FAST"] = str(int(c[1:]) + 1)
+            elif c == "auto":
+                os.environ.pop("PC_CONV_CFG", None)
+            elif c.startswith("h"):
+                os.environ.pop("PC_CONV_CFG", None)
+                os.environ["PC_CONV_HALO"] = str(int(c[1:]) + 1)
             else:
                 os.environ["PC_CONV_CFG"] = c
             try:
