@@ -166,7 +166,7 @@ def extract_frame(frame: np.ndarray, scrfd_params, variant: str, arc_params, dep
     for d in dets:
         if all(ra.iou(d[0], k[0]) < 0.45 for k in kept):
             kept.append(d)
-    chips, boxes = [], []
+    chips, boxes, kps5 = [], [], []
     for (x1, y1, x2, y2), pts, _ in kept:
         face = frame[y1:y2, x1:x2]
         canon = ra.canon_5pts(pts)
@@ -174,6 +174,7 @@ def extract_frame(frame: np.ndarray, scrfd_params, variant: str, arc_params, dep
             raise NotImplementedError("eye-roll fallback")
         chips.append(align_chip(face, canon))
         boxes.append((x1, y1, x2, y2))
+        kps5.append(pts)
     chips = np.stack(chips)
     q = [cv_ops.face_quality(c) for c in chips]
     e = nt.iresnet_forward(arc_params, depth, nt.arcface_input_from_chips(chips)).numpy()
@@ -181,7 +182,8 @@ def extract_frame(frame: np.ndarray, scrfd_params, variant: str, arc_params, dep
     feats = ra.arcface_postprocess(e, ef)
     out = []
     for i, b in enumerate(boxes):
-        f = {"bbox": np.array(b, np.int32), "feat": feats[i], "quality": float(q[i]), "chip": chips[i]}
+        f = {"bbox": np.array(b, np.int32), "feat": feats[i], "quality": float(q[i]), "chip": chips[i],
+             "kps5": kps5[i]}
         if bank is not None:
             f["fd"] = ra.fd_min(feats[i], bank)
         out.append(f)

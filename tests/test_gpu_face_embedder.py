@@ -102,6 +102,14 @@ def test_face_embedder_end_to_end(gpu_ctx, monkeypatch, prec, tol_box, tol_count
                 nshifted += 1
                 continue
             if prec == "f16" and not np.array_equal(a["chip"], b["chip"]):
+                # f16 landmarks moved by a fraction of a pixel and the warp resampled:
+                # the landmarks must agree closely, and the device embedding must be the
+                # oracle embedding of the device's own chip (the chained check)
+                assert np.abs(a["kps5"] - b["kps5"]).max() < 1.0
+                e = nt.iresnet_forward(fe._arc_params, 100, nt.arcface_input_from_chips(a["chip"][None])).numpy()
+                ef = nt.iresnet_forward(fe._arc_params, 100,
+                                        nt.arcface_input_from_chips(a["chip"][None, :, ::-1])).numpy()
+                assert np.abs(ra.arcface_postprocess(e, ef)[0] - a["feat"]).max() < 1e-2
                 nrealigned += 1
                 continue
             assert abs(a["quality"] - b["quality"]) <= tol_q * max(1.0, b["quality"])
@@ -112,7 +120,10 @@ def test_face_embedder_end_to_end(gpu_ctx, monkeypatch, prec, tol_box, tol_count
                     assert (a["fd"] <= thr) == (b["fd"] <= thr)
             nchecked += 1
         assert unmatched <= tol_count
-    assert nchecked >= 4 and nshifted + nrealigned <= nchecked
+    if prec == "f32":
+        assert nchecked >= 4 and nshifted + nrealigned <= nchecked
+    else:
+        assert nchecked + nrealigned >= 4 and nshifted <= (nchecked + nrealigned) // 2
 
 
 def test_extract_single_matches_batch(gpu_ctx):
