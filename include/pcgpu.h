@@ -31,6 +31,13 @@
  *                                      (face_embedder.py:2165-2169, 2292-2294, 2394)
  *   pc_resize_area                     cv2.resize(..., INTER_AREA) (gui_app.py:1505-1507)
  *   pc_resize_linear                   cv2.resize(..., INTER_LINEAR) (face_embedder.py:2264, 2460)
+ *   pc_yolo_detect                     PersonDetector.detect -> [ext] ultralytics YOLO.predict(conf, iou=0.45,
+ *                                      classes=[0], max_det=40, imgsz=640) (detectors.py:271-296)
+ *   pc_clip_prep / pc_clip_embed       ReIDEmbedder.extract: BGR2RGB + open_clip preprocess + encode_image +
+ *                                      F.normalize (reid_embedder.py:38-57)
+ *   pc_l2_normalize                    torch.nn.functional.normalize(feats, dim=1) (reid_embedder.py:55)
+ *   pc_pil_bicubic_coeffs              Pillow Image.resize(BICUBIC) coefficients inside the open_clip
+ *                                      preprocess (reid_embedder.py:49)
  */
 #ifndef PCGPU_H
 #define PCGPU_H
@@ -102,6 +109,30 @@ typedef struct pc_area_tab {
   float alpha;
 } pc_area_tab;
 
+/* One YOLOv8 letterbox job ([ext] ultralytics LetterBox(auto=True, stride=32), detectors.py:274):
+ * BGR u8 frame -> cv2.resize INTER_LINEAR to new_w x new_h placed at (left, top) of an
+ * Hp x Wp canvas filled with 114; identity = 1 when no resize happens (same shape). */
+typedef struct pc_yolo_letterbox_desc {
+  const uint8_t* d_src;
+  int32_t H, W, row_stride;
+  int32_t new_w, new_h;
+  int32_t top, left;
+  double scale_x, scale_y;
+  int32_t simd_end;
+  int32_t identity;
+} pc_yolo_letterbox_desc;
+
+/* [ext] ultralytics ops.scale_boxes per frame: box = clip((box - pad) / gain, [0,W0] x [0,H0]) */
+typedef struct pc_yolo_scale {
+  float gain, pad_x, pad_y, W0, H0;
+} pc_yolo_scale;
+
+/* One BGR u8 image crop on the device (top-left pointer, size, bytes per row). */
+typedef struct pc_crop_desc {
+  const uint8_t* d_src;
+  int32_t H, W, row_stride, pad_;
+} pc_crop_desc;
+
 int pc_abi_version(void);
 
 /* ---- context ---- */
@@ -165,6 +196,30 @@ int pc_embed_finalize(pc_ctx* ctx, const float* d_e, int ld, int n, int dim, int
 int pc_arcface_embed(pc_net* net, const uint8_t* d_chips, int n, int flip, float* d_feat);
 int pc_bank_match(pc_ctx* ctx, const float* d_q, int n, const float* d_bank, int b, int dim, float* d_fd,
                   int32_t* d_idx);
+
+/* ---- person detection (YOLOv8) ---- */
+/* letterbox -> YOLOv8 net -> DFL decode (best class 0, score > conf) -> NMS(iou) -> scale_boxes,
+ * for n frames sharing one Hp x Wp canvas. d_dets [n][max_det][5] (x1, y1, x2, y2, conf) in frame
+ * pixels, d_count [n] kept (<= max_det), d_ncand [n] candidates (capacity 16384 per frame). */
+/* letterbox only (the first stage of pc_yolo_detect): d_out [n][Hp][Wp][4] in the precision's dtype */
+int pc_yolo_letterbox(pc_ctx* ctx, int precision, const pc_yolo_letterbox_desc* h_descs, int n, int Hp, int Wp,
+                      void* d_out);
+int pc_yolo_detect(pc_net* net, const pc_yolo_letterbox_desc* h_descs, int n, int Hp, int Wp, float conf, float iou,
+                   const pc_yolo_scale* h_scale, int max_det, float* d_dets, int32_t* d_count, int32_t* d_ncand);
+
+/* ---- ReID body embedding (OpenCLIP ViT-L/14 image tower) ---- */
+/* preprocess n crops -> ViT-L/14 patch matrix [n][257][608] (token 0 and K padding zero) */
+int pc_clip_prep(pc_ctx* ctx, int precision, const pc_crop_desc* h_crops, int n, void* d_out);
+/* preprocess + image tower + F.normalize: d_feat [n][dim] unit f32 */
+int pc_clip_embed(pc_net* net, const pc_crop_desc* h_crops, int n, float* d_feat);
+/* rows of d_e (stride ld floats) / max(||row||, eps) -> d_out [n][dim] */
+int pc_l2_normalize(pc_ctx* ctx, const float* d_e, int ld, int n, int dim, float eps, float* d_out);
+/* Pillow BICUBIC resample coefficients (precompute_coeffs + normalize_coeffs_8bpc) for output
+ * positions [first, first+count) of an in_size -> out_size resize: h_bounds [count][2] (min, n),
+ * h_kk [count][ksize] Q22. Returns ksize (< 0: -status). */
+int pc_pil_bicubic_coeffs(int in_size, int out_size, int first, int count, int32_t* h_bounds, int32_t* h_kk, int kmax);
+/* torchvision Resize(side) + CenterCrop(side) geometry: h_out4 = resized w, h, crop top, left */
+int pc_clip_geometry(int h, int w, int side, int32_t* h_out4);
 
 /* ---- host-side align geometry (CPU, batched) ---- */
 /* cv::estimateAffinePartial2D(from, to, method=LMEDS) for n point sets of npts points each

@@ -290,3 +290,96 @@ def scrfd_detect_post(head_outs, thresh: float, det_scale: float, nms_thresh: fl
     kps = kps[order]
     keep = scrfd_nms_keep(pre, nms_thresh)
     return pre[keep], kps[keep]
+
+
+# ---------------------------------------------------------------------------
+# YOLOv8 person detection: [ext] ultralytics 8.3.205 as called by PersonDetector.detect
+# (detectors.py:271-296). Restated from its published algorithm (not vendored, no
+# fixtures in the reference -> parity unpinned against ultralytics itself).
+# ---------------------------------------------------------------------------
+def yolo_letterbox(frame: np.ndarray, imgsz: int = 640, stride: int = 32) -> Tuple[np.ndarray, tuple]:
+    """LetterBox(auto=True, center=True) + preprocess: returns the [Hp][Wp][3] f32 RGB/255
+    canvas and the geometry (new_w, new_h, top, left, Hp, Wp)."""
+    from oracle import cv_ops
+    from person_capture_amd.models_yolo import letterbox_geometry   # sizing formulas only
+    H, W = frame.shape[:2]
+    g = letterbox_geometry(H, W, imgsz, stride)
+    new_w, new_h, top, left, Hp, Wp = g
+    if (W, H) != (new_w, new_h):
+        x = (new_w * 3 // 16) * 16 if new_w * 3 >= 16 else 0
+        while x < new_w * 3 - 8:
+            x += 8
+        img = cv_ops.resize_linear(frame, new_w, new_h, 1.0 / (float(new_w) / W), 1.0 / (float(new_h) / H), x)
+    else:
+        img = np.ascontiguousarray(frame)
+    canvas = np.full((Hp, Wp, 3), 114, np.uint8)
+    canvas[top:top + new_h, left:left + new_w] = img
+    return canvas[..., ::-1].astype(np.float32) / np.float32(255.0), g
+
+
+def yolo_postprocess(heads: Sequence[np.ndarray], conf: float, iou: float, max_det: int, Hp: int, Wp: int,
+                     H0: int, W0: int) -> np.ndarray:
+    """Detect inference decode + ops.non_max_suppression(classes=[0]) + ops.scale_boxes for one
+    image. heads: per stride [H][W][64+nc] f32. Returns [k][5] (x1, y1, x2, y2, conf)."""
+    f32 = np.float32
+    cand = []
+    aoff = 0
+    for hd, s in zip(heads, (8, 16, 32)):
+        h, w, _ = hd.shape
+        flat = hd.reshape(h * w, -1).astype(f32)
+        cls = flat[:, 64:]
+        j = np.argmax(cls, axis=1)
+        best = cls[np.arange(h * w), j]
+        score = (1.0 / (1.0 + np.exp(-best.astype(np.float64)))).astype(f32)   # f64, rounded (as the device)
+        keep = np.nonzero((j == 0) & (score > f32(conf)))[0]
+        for a in keep:
+            d = []
+            for k in range(4):
+                b = flat[a, 16 * k:16 * k + 16]
+                e = np.exp((b - b.max()).astype(np.float64)).astype(f32)
+                ssum = f32(0.0)
+                for v in e:
+                    ssum = f32(ssum + v)
+                dist = f32(0.0)
+                for i in range(16):
+                    dist = f32(dist + f32(e[i] / ssum) * f32(i))
+                d.append(dist)
+            y, x = divmod(int(a), w)
+            ax, ay, sf = f32(x) + f32(0.5), f32(y) + f32(0.5), f32(s)
+            x1, y1, x2, y2 = f32(ax - d[0]), f32(ay - d[1]), f32(ax + d[2]), f32(ay + d[3])
+            cx, cy = f32(f32(f32(x1 + x2) / f32(2)) * sf), f32(f32(f32(y1 + y2) / f32(2)) * sf)
+            bw, bh = f32(f32(x2 - x1) * sf), f32(f32(y2 - y1) * sf)
+            hw_, hh_ = f32(bw / f32(2)), f32(bh / f32(2))
+            cand.append((f32(cx - hw_), f32(cy - hh_), f32(cx + hw_), f32(cy + hh_), score[a], aoff + int(a)))
+        aoff += h * w
+    cand.sort(key=lambda c: (-float(c[4]), c[5]))
+    kept = []
+    supp = [False] * len(cand)
+    for i, ci in enumerate(cand):
+        if supp[i]:
+            continue
+        kept.append(ci)
+        if len(kept) >= max_det:
+            break
+        ai = f32(f32(ci[2] - ci[0]) * f32(ci[3] - ci[1]))
+        for jx in range(i + 1, len(cand)):
+            if supp[jx]:
+                continue
+            cj = cand[jx]
+            ww = max(f32(min(ci[2], cj[2]) - max(ci[0], cj[0])), f32(0.0))
+            hh = max(f32(min(ci[3], cj[3]) - max(ci[1], cj[1])), f32(0.0))
+            inter = f32(ww * hh)
+            aj = f32(f32(cj[2] - cj[0]) * f32(cj[3] - cj[1]))
+            if f32(inter / f32(f32(ai + aj) - inter)) > f32(iou):
+                supp[jx] = True
+    from person_capture_amd.models_yolo import scale_geometry   # sizing formulas only
+    gain, px, py = scale_geometry(Hp, Wp, H0, W0)
+    g = f32(gain)
+    out = np.zeros((len(kept), 5), f32)
+    for r, c in enumerate(kept):
+        out[r, 0] = min(max(f32(f32(c[0] - f32(px)) / g), f32(0)), f32(W0))
+        out[r, 1] = min(max(f32(f32(c[1] - f32(py)) / g), f32(0)), f32(H0))
+        out[r, 2] = min(max(f32(f32(c[2] - f32(px)) / g), f32(0)), f32(W0))
+        out[r, 3] = min(max(f32(f32(c[3] - f32(py)) / g), f32(0)), f32(H0))
+        out[r, 4] = c[4]
+    return out

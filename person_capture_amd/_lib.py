@@ -42,6 +42,23 @@ class AreaTab(C.Structure):
     _fields_ = [("si", C.c_int32), ("di", C.c_int32), ("alpha", C.c_float)]
 
 
+class YoloLetterboxDesc(C.Structure):
+    _fields_ = [("d_src", C.c_void_p), ("H", C.c_int32), ("W", C.c_int32), ("row_stride", C.c_int32),
+                ("new_w", C.c_int32), ("new_h", C.c_int32), ("top", C.c_int32), ("left", C.c_int32),
+                ("scale_x", C.c_double), ("scale_y", C.c_double), ("simd_end", C.c_int32), ("identity", C.c_int32)]
+
+
+class YoloScale(C.Structure):
+    _fields_ = [("gain", C.c_float), ("pad_x", C.c_float), ("pad_y", C.c_float), ("W0", C.c_float),
+                ("H0", C.c_float)]
+
+
+class CropDesc(C.Structure):
+    _fields_ = [("d_src", C.c_void_p), ("H", C.c_int32), ("W", C.c_int32), ("row_stride", C.c_int32),
+                ("pad_", C.c_int32)]
+
+
+assert C.sizeof(YoloLetterboxDesc) == 64 and C.sizeof(YoloScale) == 20 and C.sizeof(CropDesc) == 24
 assert C.sizeof(ResizeDesc) == 64 and C.sizeof(LetterboxDesc) == 56 and C.sizeof(WarpDesc) == 96 and C.sizeof(AreaTab) == 12
 
 _P = C.c_void_p
@@ -88,6 +105,14 @@ SIGNATURES = {
     "pc_bank_match": ([_P, _P, _I, _P, _I, _I, _P, _P], _I),
     "pc_estimate_affine_partial": ([_P, _P, _I, _I, _P, _P], _I),
     "pc_invert_affine": ([_P, _P], _I),
+    "pc_yolo_letterbox": ([_P, _I, C.POINTER(YoloLetterboxDesc), _I, _I, _I, _P], _I),
+    "pc_yolo_detect": ([_P, C.POINTER(YoloLetterboxDesc), _I, _I, _I, _F, _F, C.POINTER(YoloScale), _I, _P, _P,
+                        _P], _I),
+    "pc_clip_prep": ([_P, _I, C.POINTER(CropDesc), _I, _P], _I),
+    "pc_clip_embed": ([_P, C.POINTER(CropDesc), _I, _P], _I),
+    "pc_l2_normalize": ([_P, _P, _I, _I, _I, _F, _P], _I),
+    "pc_pil_bicubic_coeffs": ([_I, _I, _I, _I, C.POINTER(C.c_int32), C.POINTER(C.c_int32), _I], _I),
+    "pc_clip_geometry": ([_I, _I, _I, C.POINTER(C.c_int32)], _I),
 }
 
 

@@ -67,6 +67,33 @@ struct DecodeParams {
 hipError_t scrfd_decode_launch(const DecodeParams& p, int N, hipStream_t s);
 hipError_t scrfd_nms_launch(const float* cand, const int* count, int cap, float nms_thresh, int max_det, float* dets,
                             float* kps, int* nkeep, int N, hipStream_t s);
+hipError_t embed_l2_launch(const float* e, int ld, int n, int dim, float eps, float* out, hipStream_t s);
+// pc_ops.hip
+struct UpsampleParams { const void* x; int N, H, W, C, xcs; void* y; int ycs; };
+hipError_t upsample2_launch(int f32, const UpsampleParams& p, hipStream_t s);
+struct LayerNormParams {
+  const void* x; int xcs; void* y; int ycs; int M, C, cwrite;
+  const float* gamma; const float* beta; const float* add; int rows; float eps;
+};
+hipError_t layernorm_launch(int f32, const LayerNormParams& p, hipStream_t s);
+struct AttnParams { const void* qkv; int qcs; void* out; int ocs; int N, T, heads; float scale; };
+hipError_t attention_launch(int f32, const AttnParams& p, int head_dim, hipStream_t s);
+// pc_yolo.hip
+struct YoloLetterboxDesc;
+hipError_t yolo_letterbox_launch(int f32, const YoloLetterboxDesc* d_descs, int N, int Hp, int Wp, void* out,
+                                 hipStream_t s);
+struct YoloLevel { const float* out; int H, W, cs, stride; int loc_offset; };
+struct YoloDecodeParams { YoloLevel lv[3]; int nlv, total, nc; float conf; float* cand; int* count; int cap; };
+struct YoloScale;
+hipError_t yolo_decode_launch(const YoloDecodeParams& p, int N, hipStream_t s);
+hipError_t yolo_nms_launch(const float* cand, const int* count, int cap, float iou, int max_det, const YoloScale* sc,
+                           float* dets, int* nkeep, int N, hipStream_t s);
+// pc_clip.hip
+struct ClipPrepDesc {
+  const uint8_t* src; int H, W, row_stride; int kh, kv;
+  const int* hb; const int* hk; const int* vb; const int* vk; int row0, nrows; uint8_t* tmp;
+};
+hipError_t clip_prep_launch(int f32, const ClipPrepDesc* d_descs, int N, int max_rows, void* out, hipStream_t s);
 }  // namespace pc
 
 using namespace pc;
@@ -75,6 +102,8 @@ static_assert(sizeof(pc_letterbox_desc) == 56, "letterbox desc layout");
 static_assert(sizeof(pc_warp_desc) == 96, "warp desc layout");
 static_assert(sizeof(pc_area_tab) == 12, "area tab layout");
 static_assert(sizeof(pc_resize_desc) == 64, "resize desc layout");
+static_assert(sizeof(pc_yolo_letterbox_desc) == 64, "yolo letterbox desc layout");
+static_assert(sizeof(pc_yolo_scale) == 20, "yolo scale layout");
 
 struct pc_ctx {
   int device = 0;
@@ -91,6 +120,13 @@ struct pc_ctx {
   int* cand_count = nullptr;
   float* det_scale = nullptr;
   size_t cand_images = 0;
+  // YOLO candidates
+  float* ycand = nullptr;
+  int* ycount = nullptr;
+  size_t ycand_images = 0;
+  // CLIP preprocessing tables + horizontal-pass scratch
+  void* clip_tmp = nullptr;
+  size_t clip_tmp_bytes = 0;
 };
 
 static int fail(pc_ctx* c, int code, const std::string& msg) {
@@ -155,6 +191,9 @@ extern "C" int pc_ctx_destroy(pc_ctx* c) {
   if (c->cand) hipFree(c->cand);
   if (c->cand_count) hipFree(c->cand_count);
   if (c->det_scale) hipFree(c->det_scale);
+  if (c->ycand) hipFree(c->ycand);
+  if (c->ycount) hipFree(c->ycount);
+  if (c->clip_tmp) hipFree(c->clip_tmp);
   if (c->own_stream) hipStreamDestroy(c->own_stream);
   delete c;
   return PC_OK;
@@ -208,7 +247,7 @@ extern "C" int pc_memset(pc_ctx* c, void* d, int v, size_t n) {
 // ===========================================================================
 // network executor
 // ===========================================================================
-enum { OP_CONV = 1, OP_STEM = 2, OP_MAXPOOL = 3 };
+enum { OP_CONV = 1, OP_STEM = 2, OP_MAXPOOL = 3, OP_UPSAMPLE = 4, OP_LAYERNORM = 5, OP_ATTENTION = 6 };
 
 struct NetBuf { long long elems; int is_f32; void* d = nullptr; };
 struct NetTensor { int buf, H, W, C, cs, coff, is_f32; };
@@ -555,7 +594,8 @@ extern "C" int pc_net_create(pc_ctx* c, const void* prog, size_t nbytes, int pre
         // algorithmic MACs: real output channels x real taps x input channels (padded lanes excluded by the
         // program: w[25+s] carries the true input channel count)
         const int cin_true = op.w[25 + s] > 0 ? op.w[25 + s] : X.C;
-        macs += (double)Y.H * Y.W * op.w[16] * op.w[4 + 5 * s] * op.w[5 + 5 * s] * cin_true;
+        const int cout_true = op.w[27] > 0 ? op.w[27] : op.w[16];
+        macs += (double)Y.H * Y.W * cout_true * op.w[4 + 5 * s] * op.w[5 + 5 * s] * cin_true;
       }
       n->flops_per_image += 2.0 * macs;
       n->plans[i].flops_per_image = 2.0 * macs;
@@ -567,7 +607,12 @@ extern "C" int pc_net_create(pc_ctx* c, const void* prog, size_t nbytes, int pre
       rc = plan_stem(n, op, n->stems[i], stem_col_bytes);
       n->plans[i].flops_per_image = 2.0 * Y.H * Y.W * op.w[8] * op.w[3] * op.w[4] * cin_true;
       n->launches += n->stems[i].use_mfma ? 2 : 1;
-    } else if (op.w[0] == OP_MAXPOOL) {
+    } else if (op.w[0] == OP_MAXPOOL || op.w[0] == OP_UPSAMPLE || op.w[0] == OP_LAYERNORM) {
+      n->launches += 1;
+    } else if (op.w[0] == OP_ATTENTION) {
+      const NetTensor& Q = n->tens[op.w[2]];
+      const double T = (double)Q.H * Q.W;
+      n->flops_per_image += 4.0 * T * T * op.w[3] * op.w[4];
       n->launches += 1;
     } else {
       rc = fail(c, PC_ERR_FORMAT, "unknown op type");
@@ -741,6 +786,35 @@ static int run_ops(pc_net* n, int N) {
       p.y = tensor_ptr(n, w[1]); p.OH = Y.H; p.OW = Y.W; p.ycs = Y.cs;
       p.k = w[3]; p.stride = w[4]; p.pad = w[5];
       HIPCHK(c, maxpool_launch(n->f32, p, s));
+    } else if (w[0] == OP_UPSAMPLE) {
+      UpsampleParams p;
+      const NetTensor& X = n->tens[w[2]];
+      const NetTensor& Y = n->tens[w[1]];
+      p.x = tensor_ptr(n, w[2]); p.N = N; p.H = X.H; p.W = X.W; p.C = std::min(X.C, Y.C); p.xcs = X.cs;
+      p.y = tensor_ptr(n, w[1]); p.ycs = Y.cs;
+      HIPCHK(c, upsample2_launch(n->f32, p, s));
+    } else if (w[0] == OP_LAYERNORM) {
+      LayerNormParams p;
+      const NetTensor& X = n->tens[w[2]];
+      const NetTensor& Y = n->tens[w[1]];
+      p.x = tensor_ptr(n, w[2]); p.xcs = X.cs;
+      p.y = tensor_ptr(n, w[1]); p.ycs = Y.cs;
+      p.M = N * X.H * X.W; p.C = w[8]; p.cwrite = Y.C;
+      p.gamma = (const float*)n->arrays[w[3]];
+      p.beta = (const float*)n->arrays[w[4]];
+      p.add = w[5] >= 0 ? (const float*)n->arrays[w[5]] : nullptr;
+      p.rows = w[5] >= 0 ? w[6] : 1;
+      memcpy(&p.eps, &w[7], 4);
+      HIPCHK(c, layernorm_launch(n->f32, p, s));
+    } else if (w[0] == OP_ATTENTION) {
+      AttnParams p;
+      const NetTensor& Q = n->tens[w[2]];
+      const NetTensor& O = n->tens[w[1]];
+      p.qkv = tensor_ptr(n, w[2]); p.qcs = Q.cs;
+      p.out = tensor_ptr(n, w[1]); p.ocs = O.cs;
+      p.N = N; p.T = Q.H * Q.W; p.heads = w[3];
+      p.scale = 1.0f / sqrtf((float)w[4]);
+      HIPCHK(c, attention_launch(n->f32, p, w[4], s));
     }
     if (prof) {
       int rc = prof_event(n, &rec.b);
@@ -1016,5 +1090,186 @@ extern "C" int pc_scrfd_detect(pc_net* net, const pc_letterbox_desc* h, int n, i
   HIPCHK(c, scrfd_decode_launch(p, n, c->stream));
   HIPCHK(c, scrfd_nms_launch(c->cand, c->cand_count, cap, nms_thresh, max_det, dets, kps, count, n, c->stream));
   if (ncand) HIPCHK(c, hipMemcpyAsync(ncand, c->cand_count, n * 4, hipMemcpyDeviceToDevice, c->stream));
+  return PC_OK;
+}
+
+// ===========================================================================
+// YOLOv8 person detection (PersonDetector.detect, detectors.py:271-296)
+// ===========================================================================
+static int check_yolo_descs(pc_ctx* c, const pc_yolo_letterbox_desc* h, int n, int Hp, int Wp) {
+  for (int i = 0; i < n; ++i) {
+    const pc_yolo_letterbox_desc& d = h[i];
+    if (!d.d_src || d.H <= 0 || d.W <= 0 || d.row_stride < d.W * 3 || d.new_w <= 0 || d.new_h <= 0 || d.top < 0 ||
+        d.left < 0 || d.top + d.new_h > Hp || d.left + d.new_w > Wp || (d.identity && (d.new_w != d.W || d.new_h != d.H)))
+      return fail(c, PC_ERR_ARG, "yolo letterbox job out of range");
+  }
+  return PC_OK;
+}
+
+extern "C" int pc_yolo_letterbox(pc_ctx* c, int prec, const pc_yolo_letterbox_desc* h, int n, int Hp, int Wp,
+                                 void* out) {
+  if (!c || !h || n <= 0 || Hp <= 0 || Wp <= 0 || !out) return fail(c, PC_ERR_ARG, "pc_yolo_letterbox: bad arguments");
+  int rc = check_yolo_descs(c, h, n, Hp, Wp);
+  if (rc) return rc;
+  void* dd;
+  if ((rc = stage_copy(c, h, sizeof(pc_yolo_letterbox_desc) * n, &dd))) return rc;
+  HIPCHK(c, yolo_letterbox_launch(prec == PC_PREC_F32, (const YoloLetterboxDesc*)dd, n, Hp, Wp, out, c->stream));
+  return PC_OK;
+}
+
+extern "C" int pc_yolo_detect(pc_net* net, const pc_yolo_letterbox_desc* h, int n, int Hp, int Wp, float conf,
+                              float iou, const pc_yolo_scale* h_scale, int max_det, float* dets, int32_t* count,
+                              int32_t* ncand) {
+  if (!net || !h || n <= 0 || !h_scale || max_det <= 0 || !dets || !count) return PC_ERR_ARG;
+  pc_ctx* c = net->ctx;
+  if (n > net->max_batch) return fail(c, PC_ERR_ARG, "pc_yolo_detect: batch exceeds max batch");
+  if ((int)net->outs.size() != 3) return fail(c, PC_ERR_FORMAT, "YOLO net must have 3 head outputs");
+  const NetTensor& I = net->tens[net->in_tensor];
+  if (I.H != Hp || I.W != Wp || I.C != 4) return fail(c, PC_ERR_ARG, "pc_yolo_detect: canvas does not match the net input");
+  if (int e = check_yolo_descs(c, h, n, Hp, Wp)) return e;
+  const int cap = 16384;
+  if (c->ycand_images < (size_t)n) {
+    if (c->ycand) hipFree(c->ycand);
+    if (c->ycount) hipFree(c->ycount);
+    HIPCHK(c, hipMalloc((void**)&c->ycand, (size_t)n * cap * 8 * 4));
+    HIPCHK(c, hipMalloc((void**)&c->ycount, (size_t)n * 4));
+    c->ycand_images = n;
+  }
+  const size_t need = (size_t)net->max_batch * Hp * Wp * 4 * (net->f32 ? 4 : 2);
+  if (net->prep_bytes < need) {
+    if (net->prep) HIPCHK(c, hipFree(net->prep));
+    HIPCHK(c, hipMalloc(&net->prep, need));
+    net->prep_bytes = need;
+  }
+  int rc = pc_yolo_letterbox(c, net->f32 ? PC_PREC_F32 : PC_PREC_F16, h, n, Hp, Wp, net->prep);
+  if (rc) return rc;
+  rc = pc_net_run(net, net->prep, n);
+  if (rc) return rc;
+  YoloDecodeParams p;
+  memset(&p, 0, sizeof(p));
+  p.nlv = 3;
+  int loc = 0, nc = -1;
+  for (int l = 0; l < 3; ++l) {
+    const NetTensor& O = net->tens[net->outs[l]];
+    if (!(O.is_f32 || net->f32)) return fail(c, PC_ERR_FORMAT, "YOLO head outputs must be f32");
+    const int ncl = O.C - 64;
+    if (ncl <= 0 || (nc >= 0 && ncl != nc)) return fail(c, PC_ERR_FORMAT, "YOLO head channel layout");
+    nc = ncl;
+    p.lv[l].out = (const float*)tensor_ptr(net, net->outs[l]);
+    p.lv[l].H = O.H; p.lv[l].W = O.W; p.lv[l].cs = O.cs;
+    p.lv[l].stride = Hp / O.H;
+    p.lv[l].loc_offset = loc;
+    loc += O.H * O.W;
+  }
+  if (loc > cap) return fail(c, PC_ERR_CAPACITY, "pc_yolo_detect: more anchors than the NMS capacity");
+  p.total = loc;
+  p.nc = nc;
+  p.conf = conf;
+  p.cand = c->ycand;
+  p.count = c->ycount;
+  p.cap = cap;
+  void* dsc;
+  if ((rc = stage_copy(c, h_scale, sizeof(pc_yolo_scale) * n, &dsc))) return rc;
+  HIPCHK(c, hipMemsetAsync(c->ycount, 0, n * 4, c->stream));
+  HIPCHK(c, yolo_decode_launch(p, n, c->stream));
+  HIPCHK(c, yolo_nms_launch(c->ycand, c->ycount, cap, iou, max_det, (const YoloScale*)dsc, dets, count, n, c->stream));
+  if (ncand) HIPCHK(c, hipMemcpyAsync(ncand, c->ycount, n * 4, hipMemcpyDeviceToDevice, c->stream));
+  return PC_OK;
+}
+
+// ===========================================================================
+// ReID: OpenCLIP ViT-L/14 image tower (ReIDEmbedder.extract, reid_embedder.py:38-57)
+// ===========================================================================
+static const int kClipSide = 224, kClipTok = 257, kClipK = 608, kClipKmax = 64;
+
+extern "C" int pc_clip_prep(pc_ctx* c, int prec, const pc_crop_desc* h, int n, void* out) {
+  if (!c || !h || n <= 0 || !out) return fail(c, PC_ERR_ARG, "pc_clip_prep: bad arguments");
+  // host: geometry + Pillow coefficient tables for the 224 kept columns / rows of each crop
+  struct Tabs { int kh, kv, row0, nrows; std::vector<int32_t> hb, hk, vb, vk; };
+  std::vector<Tabs> T(n);
+  size_t tmp_bytes = 0, tab_ints = 0;
+  int max_rows = 0;
+  for (int i = 0; i < n; ++i) {
+    const pc_crop_desc& d = h[i];
+    if (!d.d_src || d.H <= 0 || d.W <= 0 || d.row_stride < d.W * 3) return fail(c, PC_ERR_ARG, "pc_clip_prep: bad crop");
+    int32_t g[4];
+    pc_clip_geometry(d.H, d.W, kClipSide, g);
+    Tabs& t = T[i];
+    t.hb.resize(2 * kClipSide); t.vb.resize(2 * kClipSide);
+    t.hk.resize((size_t)kClipSide * kClipKmax); t.vk.resize((size_t)kClipSide * kClipKmax);
+    t.kh = pc_pil_bicubic_coeffs(d.W, g[0], g[3], kClipSide, t.hb.data(), t.hk.data(), kClipKmax);
+    t.kv = pc_pil_bicubic_coeffs(d.H, g[1], g[2], kClipSide, t.vb.data(), t.vk.data(), kClipKmax);
+    if (t.kh < 0 || t.kv < 0) return fail(c, PC_ERR_CAPACITY, "pc_clip_prep: crop too large for the resample tables");
+    t.hk.resize((size_t)kClipSide * t.kh); t.vk.resize((size_t)kClipSide * t.kv);
+    int lo = 1 << 30, hi = 0;
+    for (int y = 0; y < kClipSide; ++y) { lo = std::min(lo, t.vb[2 * y]); hi = std::max(hi, t.vb[2 * y] + t.vb[2 * y + 1]); }
+    t.row0 = lo; t.nrows = std::max(hi - lo, 1);
+    for (int y = 0; y < kClipSide; ++y) t.vb[2 * y] -= lo;
+    max_rows = std::max(max_rows, t.nrows);
+    tmp_bytes += (size_t)t.nrows * kClipSide * 3;
+    tab_ints += t.hb.size() + t.hk.size() + t.vb.size() + t.vk.size();
+  }
+  if (c->clip_tmp_bytes < tmp_bytes) {
+    if (c->clip_tmp) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->clip_tmp)); }
+    HIPCHK(c, hipMalloc(&c->clip_tmp, tmp_bytes));
+    c->clip_tmp_bytes = tmp_bytes;
+  }
+  std::vector<int32_t> tabs;
+  tabs.reserve(tab_ints);
+  std::vector<size_t> off(n * 4);
+  for (int i = 0; i < n; ++i) {
+    off[4 * i + 0] = tabs.size(); tabs.insert(tabs.end(), T[i].hb.begin(), T[i].hb.end());
+    off[4 * i + 1] = tabs.size(); tabs.insert(tabs.end(), T[i].hk.begin(), T[i].hk.end());
+    off[4 * i + 2] = tabs.size(); tabs.insert(tabs.end(), T[i].vb.begin(), T[i].vb.end());
+    off[4 * i + 3] = tabs.size(); tabs.insert(tabs.end(), T[i].vk.begin(), T[i].vk.end());
+  }
+  void* dtab;
+  int rc = stage_copy(c, tabs.data(), tabs.size() * 4, &dtab);
+  if (rc) return rc;
+  std::vector<ClipPrepDesc> descs(n);
+  size_t tmp_off = 0;
+  for (int i = 0; i < n; ++i) {
+    ClipPrepDesc& d = descs[i];
+    const int32_t* tb = (const int32_t*)dtab;
+    d.src = h[i].d_src; d.H = h[i].H; d.W = h[i].W; d.row_stride = h[i].row_stride;
+    d.kh = T[i].kh; d.kv = T[i].kv;
+    d.hb = tb + off[4 * i]; d.hk = tb + off[4 * i + 1]; d.vb = tb + off[4 * i + 2]; d.vk = tb + off[4 * i + 3];
+    d.row0 = T[i].row0; d.nrows = T[i].nrows;
+    d.tmp = (uint8_t*)c->clip_tmp + tmp_off;
+    tmp_off += (size_t)T[i].nrows * kClipSide * 3;
+  }
+  void* ddesc;
+  if ((rc = stage_copy(c, descs.data(), sizeof(ClipPrepDesc) * n, &ddesc))) return rc;
+  HIPCHK(c, clip_prep_launch(prec == PC_PREC_F32, (const ClipPrepDesc*)ddesc, n, max_rows, out, c->stream));
+  return PC_OK;
+}
+
+extern "C" int pc_clip_embed(pc_net* net, const pc_crop_desc* h, int n, float* feat) {
+  if (!net || !h || n < 0 || !feat) return PC_ERR_ARG;
+  pc_ctx* c = net->ctx;
+  if (n == 0) return PC_OK;
+  if (n > net->max_batch) return fail(c, PC_ERR_ARG, "pc_clip_embed: batch exceeds max batch");
+  const NetTensor& I = net->tens[net->in_tensor];
+  if (I.H != 1 || I.W != kClipTok || I.C != kClipK) return fail(c, PC_ERR_FORMAT, "CLIP net input must be 1x257x608");
+  const size_t need = (size_t)net->max_batch * kClipTok * kClipK * (net->f32 ? 4 : 2);
+  if (net->prep_bytes < need) {
+    if (net->prep) HIPCHK(c, hipFree(net->prep));
+    HIPCHK(c, hipMalloc(&net->prep, need));
+    net->prep_bytes = need;
+  }
+  int rc = pc_clip_prep(c, net->f32 ? PC_PREC_F32 : PC_PREC_F16, h, n, net->prep);
+  if (rc) return rc;
+  rc = pc_net_run(net, net->prep, n);
+  if (rc) return rc;
+  const NetTensor& O = net->tens[net->outs[0]];
+  if (!(O.is_f32 || net->f32) || O.H * O.W != 1) return fail(c, PC_ERR_FORMAT, "CLIP output must be f32 [1][1][dim]");
+  HIPCHK(c, embed_l2_launch((const float*)tensor_ptr(net, net->outs[0]), O.cs, n, O.C, 1e-12f, feat, c->stream));
+  return PC_OK;
+}
+
+extern "C" int pc_l2_normalize(pc_ctx* c, const float* e, int ld, int n, int dim, float eps, float* out) {
+  if (!c || n < 0 || !e || !out) return fail(c, PC_ERR_ARG, "pc_l2_normalize: bad arguments");
+  if (n == 0) return PC_OK;
+  HIPCHK(c, embed_l2_launch(e, ld, n, dim, eps, out, c->stream));
   return PC_OK;
 }

@@ -13,7 +13,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((address_space(1))) void* gptr_t;
 
-enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_PRELU = 2, ACT_SILU = 3 };
+enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_PRELU = 2, ACT_SILU = 3, ACT_GELU = 4 };
 enum BiasMode { BIAS_NONE = 0, BIAS_CHANNEL = 1, BIAS_BORDER9 = 2 };
 enum ResMode { RES_NONE = 0, RES_SAME = 1, RES_UP2 = 2 };
 

@@ -13,6 +13,7 @@ __device__ __forceinline__ float act_apply(float v, int act, float slope) {
   if (act == ACT_RELU) return v > 0.f ? v : 0.f;
   if (act == ACT_PRELU) return v > 0.f ? v : v * slope;
   if (act == ACT_SILU) return v / (1.0f + __expf(-v));
+  if (act == ACT_GELU) return 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));   // nn.GELU (erf)
   return v;
 }
 

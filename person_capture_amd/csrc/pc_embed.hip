@@ -18,7 +18,8 @@ __device__ __forceinline__ float wave_sum(float v) {
 }
 
 // e: [rows][ld] f32 (rows = 2n when flip), out: [n][dim]
-__global__ void embed_finalize(const float* __restrict__ e, int ld, int n, int dim, int flip, float* __restrict__ out) {
+__global__ void embed_finalize(const float* __restrict__ e, int ld, int n, int dim, int flip, float eps,
+                               float* __restrict__ out) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (row >= n) return;
@@ -37,7 +38,7 @@ __global__ void embed_finalize(const float* __restrict__ e, int ld, int n, int d
   }
   ss = wave_sum(ss);
   float nrm = sqrtf(ss);
-  nrm = fmaxf(nrm, 1e-6f);
+  nrm = fmaxf(nrm, eps);
 #pragma unroll
   for (int j = 0; j < 16; ++j)
     if (j < per) out[(long long)row * dim + lane * per + j] = v[j] / nrm;
@@ -108,7 +109,15 @@ __global__ __launch_bounds__(256) void bank_match(const float* __restrict__ q, i
 hipError_t embed_finalize_launch(const float* e, int ld, int n, int dim, int flip, float* out, hipStream_t s) {
   if (dim % 64 || dim > 1024) return hipErrorInvalidValue;
   dim3 grid((n + 3) / 4);
-  hipLaunchKernelGGL(embed_finalize, grid, dim3(256), 0, s, e, ld, n, dim, flip, out);
+  hipLaunchKernelGGL(embed_finalize, grid, dim3(256), 0, s, e, ld, n, dim, flip, 1e-6f, out);
+  return hipGetLastError();
+}
+
+// torch.nn.functional.normalize(x, dim=1): x / max(||x||, eps) (reid_embedder.py:55, eps 1e-12)
+hipError_t embed_l2_launch(const float* e, int ld, int n, int dim, float eps, float* out, hipStream_t s) {
+  if (dim % 64 || dim > 1024) return hipErrorInvalidValue;
+  dim3 grid((n + 3) / 4);
+  hipLaunchKernelGGL(embed_finalize, grid, dim3(256), 0, s, e, ld, n, dim, 0, eps, out);
   return hipGetLastError();
 }
 

@@ -161,3 +161,74 @@ extern "C" int pc_invert_affine(const double* M, double* iM) {
   iM[3] = A21; iM[4] = A22; iM[5] = -A21 * M[2] - A22 * M[5];
   return PC_OK;
 }
+
+// ---------------------------------------------------------------------------
+// Pillow's BICUBIC resample coefficients (Pillow libImaging/Resample.c:
+// bicubic_filter a=-0.5, support 2; precompute_coeffs; normalize_coeffs_8bpc with
+// PRECISION_BITS = 22), as reached by torchvision Resize on a PIL image inside the
+// OpenCLIP preprocess of ReIDEmbedder.extract (reid_embedder.py:49). Only the output
+// positions [first, first + count) are produced (CenterCrop keeps 224 of them).
+// Returns ksize, or a negative value if kmax is too small / arguments are invalid.
+// ---------------------------------------------------------------------------
+namespace {
+double pil_bicubic(double x) {
+  const double a = -0.5;
+  if (x < 0.0) x = -x;
+  if (x < 1.0) return ((a + 2.0) * x - (a + 3.0)) * x * x + 1;
+  if (x < 2.0) return (((x - 5) * x + 8) * x - 4) * a;
+  return 0.0;
+}
+}  // namespace
+
+extern "C" int pc_pil_bicubic_coeffs(int in_size, int out_size, int first, int count, int32_t* h_bounds, int32_t* h_kk,
+                                     int kmax) {
+  if (in_size <= 0 || out_size <= 0 || first < 0 || count < 0 || first + count > out_size || !h_bounds || !h_kk)
+    return -PC_ERR_ARG;
+  const float in0 = 0.f, in1 = (float)in_size;
+  double filterscale, scale;
+  filterscale = scale = (double)(in1 - in0) / out_size;
+  if (filterscale < 1.0) filterscale = 1.0;
+  const double support = 2.0 * filterscale;
+  const int ksize = (int)ceil(support) * 2 + 1;
+  if (ksize > kmax) return -PC_ERR_CAPACITY;
+  std::vector<double> k(ksize);
+  for (int i = 0; i < count; ++i) {
+    const int xx = first + i;
+    const double center = in0 + (xx + 0.5) * scale;
+    double ww = 0.0;
+    const double ss = 1.0 / filterscale;
+    int xmin = (int)(center - support + 0.5);
+    if (xmin < 0) xmin = 0;
+    int xmax = (int)(center + support + 0.5);
+    if (xmax > in_size) xmax = in_size;
+    xmax -= xmin;
+    int x = 0;
+    for (; x < xmax; ++x) {
+      const double w = pil_bicubic((x + xmin - center + 0.5) * ss);
+      k[x] = w;
+      ww += w;
+    }
+    for (x = 0; x < xmax; ++x)
+      if (ww != 0.0) k[x] /= ww;
+    for (; x < ksize; ++x) k[x] = 0;
+    for (x = 0; x < ksize; ++x)
+      h_kk[(size_t)i * ksize + x] = k[x] < 0 ? (int32_t)(-0.5 + k[x] * (1 << 22)) : (int32_t)(0.5 + k[x] * (1 << 22));
+    h_bounds[2 * i] = xmin;
+    h_bounds[2 * i + 1] = xmax;
+  }
+  return ksize;
+}
+
+// torchvision Resize(224) (shortest edge) + CenterCrop(224) geometry for an h x w image:
+// resized size and the crop's top-left in the resized image.
+extern "C" int pc_clip_geometry(int h, int w, int side, int32_t* h_out4 /* rw, rh, top, left */) {
+  if (h <= 0 || w <= 0 || side <= 0 || !h_out4) return PC_ERR_ARG;
+  const int sh = w <= h ? w : h, lg = w <= h ? h : w;
+  const int new_short = side, new_long = (int)((double)((long long)side * lg) / sh);
+  const int rw = w <= h ? new_short : new_long, rh = w <= h ? new_long : new_short;
+  h_out4[0] = rw;
+  h_out4[1] = rh;
+  h_out4[2] = (int)nearbyint((rh - side) / 2.0);   // Python round(): half to even
+  h_out4[3] = (int)nearbyint((rw - side) / 2.0);
+  return PC_OK;
+}

@@ -23,8 +23,8 @@ from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 
-OP_CONV, OP_STEM, OP_MAXPOOL = 1, 2, 3
-ACT_NONE, ACT_RELU, ACT_PRELU, ACT_SILU = 0, 1, 2, 3
+OP_CONV, OP_STEM, OP_MAXPOOL, OP_UPSAMPLE, OP_LAYERNORM, OP_ATTENTION = 1, 2, 3, 4, 5, 6
+ACT_NONE, ACT_RELU, ACT_PRELU, ACT_SILU, ACT_GELU = 0, 1, 2, 3, 4
 BIAS_NONE, BIAS_CHANNEL, BIAS_BORDER9 = 0, 1, 2
 RES_NONE, RES_SAME, RES_UP2 = 0, 1, 2
 
@@ -59,6 +59,14 @@ class Program:
         self.tensors.append([vb, H, W, C, C, 0, is_f32])
         return t
 
+    def view(self, t: int, coff: int, C: int) -> int:
+        """Channel slice [coff, coff+C) of tensor t (same buffer and pixel stride):
+        concatenations are written and read in place."""
+        vb, H, W, C0, cs, off, f32 = self.tensors[t]
+        assert coff + C <= C0
+        self.tensors.append([vb, H, W, C, cs, off + coff, f32])
+        return len(self.tensors) - 1
+
     def dims(self, t: int) -> Tuple[int, int, int]:
         T = self.tensors[t]
         return T[1], T[2], T[3]
@@ -71,8 +79,11 @@ class Program:
     def conv(self, out: int, segs: Sequence[Tuple[int, int, int, int, int, int]], w_packed: np.ndarray,
              cout: int, bias: Optional[np.ndarray] = None, bias_mode: int = BIAS_CHANNEL,
              slope: Optional[np.ndarray] = None, act: int = ACT_NONE, res: Optional[int] = None,
-             res_mode: int = RES_SAME, act_after_res: int = 0, splitk: int = 1) -> None:
-        """segs: (tensor, KH, KW, stride, pad, cin_true) per K-segment (max 2)."""
+             res_mode: int = RES_SAME, act_after_res: int = 0, splitk: int = 1,
+             flops_cout: Optional[int] = None) -> None:
+        """segs: (tensor, KH, KW, stride, pad, cin_true) per K-segment (max 2).
+        flops_cout: true output channels for the FLOP count when the packed weight rows
+        interleave padding (outputs split into padded channel slices)."""
         assert 1 <= len(segs) <= 2
         npad, ktot = w_packed.shape
         w = [0] * 32
@@ -94,10 +105,12 @@ class Program:
         w[22] = res_mode if res is not None else RES_NONE
         w[23] = act_after_res
         w[24] = splitk
+        w[27] = int(flops_cout) if flops_cout else 0
         self.ops.append(w)
         oh, ow, _ = self.dims(out)
+        fc = flops_cout or cout
         for (t, kh, kw, s, p, cin) in segs:
-            self.flops_per_image += 2.0 * oh * ow * cout * kh * kw * cin
+            self.flops_per_image += 2.0 * oh * ow * fc * kh * kw * cin
 
     def stem(self, out: int, x: int, w: np.ndarray, bias: np.ndarray, stride: int, pad: int,
              slope: Optional[np.ndarray] = None, act: int = ACT_NONE, cin_true: int = 3) -> None:
@@ -117,6 +130,34 @@ class Program:
         ops = [0] * 32
         ops[0:6] = [OP_MAXPOOL, out, x, k, s, p]
         self.ops.append(ops)
+
+    def upsample2(self, out: int, x: int) -> None:
+        """Nearest-neighbour x2 (nn.Upsample(scale_factor=2, mode='nearest')) into out."""
+        ops = [0] * 32
+        ops[0:3] = [OP_UPSAMPLE, out, x]
+        self.ops.append(ops)
+
+    def layernorm(self, out: int, x: int, gamma: np.ndarray, beta: np.ndarray, eps: float = 1e-5,
+                  add: Optional[np.ndarray] = None) -> None:
+        """Per-pixel LayerNorm over the C true channels of x (f32 statistics). `add`
+        ([rows][C], rows = pixels per image) is added to x first (positional table)."""
+        ops = [0] * 32
+        _, _, C = self.dims(x)
+        ops[0:8] = [OP_LAYERNORM, out, x, self.arr(gamma), self.arr(beta),
+                    self.arr(add) if add is not None else -1, int(add.shape[0]) if add is not None else 0,
+                    int(np.float32(eps).view(np.int32))]
+        ops[8] = int(gamma.shape[0])
+        self.ops.append(ops)
+
+    def attention(self, out: int, qkv: int, heads: int, head_dim: int) -> None:
+        """Multi-head self-attention over the W tokens of each image: qkv [T][3*h*d]
+        (q | k | v, head-major inside each) -> out [T][h*d], softmax(q k^T / sqrt(d)) v."""
+        ops = [0] * 32
+        ops[0:5] = [OP_ATTENTION, out, qkv, heads, head_dim]
+        self.ops.append(ops)
+        H, W, _ = self.dims(qkv)
+        T = H * W
+        self.flops_per_image += 4.0 * T * T * heads * head_dim
 
     # ---- serialization --------------------------------------------------
     def _op_io(self, w: List[int]) -> Tuple[List[int], int]:

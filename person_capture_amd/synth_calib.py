@@ -110,3 +110,62 @@ def calibrate_scrfd(p, variant, rng, target_per_image, D=640, n=2):
             q = 1.0 - float(target_per_image[lvl]) / per_img
             thr = float(np.quantile(flat, min(max(q, 0.0), 1.0)))
             p[f"bbox_head.{s}.cls.bias"] = np.full(logits.shape[1], -thr, np.float32)
+
+
+def calibrate_yolo(p, scale, rng, target_per_image, Hp=384, Wp=640, n=2):
+    """YOLOv8: BN statistics from synthetic letterboxed 1080p-like canvases (noise in the
+    middle rows, 114 padding top/bottom, as LetterBox leaves it), then the class-0 logit
+    bias per level so ~target_per_image anchors per canvas pass score 0.5."""
+    from .models_yolo import REG_MAX, YOLO_BN_EPS, yolo_layers
+    torch = _torch()
+    F = torch.nn.functional
+    T = lambda k: torch.from_numpy(p[k])
+    img = np.full((n, Hp, Wp, 3), 114, np.uint8)
+    img[:, 12:Hp - 12] = rng.integers(0, 256, size=(n, Hp - 24, Wp, 3), dtype=np.uint8)
+
+    def bn(name, x):
+        mean = x.mean(dim=(0, 2, 3))
+        var = torch.clamp(x.var(dim=(0, 2, 3), unbiased=False), min=1e-4)
+        p[name + ".running_mean"] = mean.numpy().astype(np.float32)
+        p[name + ".running_var"] = var.numpy().astype(np.float32)
+        return F.batch_norm(x, torch.from_numpy(p[name + ".running_mean"]), torch.from_numpy(p[name + ".running_var"]),
+                            T(name + ".weight"), T(name + ".bias"), False, 0.0, YOLO_BN_EPS)
+
+    def conv(x, name, k, s=1):
+        return F.silu(bn(name + ".bn", F.conv2d(x, T(name + ".conv.weight"), stride=s, padding=k // 2)))
+
+    with torch.no_grad():
+        x = torch.from_numpy(img[..., ::-1].astype(np.float32) / 255.0).permute(0, 3, 1, 2).contiguous()
+        ys = []
+        for L in yolo_layers(scale):
+            t, nm = L["type"], L["name"]
+            xi = ys[L["from"][0]] if L["i"] > 0 else x
+            if t == "Conv":
+                y = conv(xi, nm, L["k"], L["s"])
+            elif t == "C2f":
+                a, b = conv(xi, nm + ".cv1", 1).chunk(2, 1)
+                parts = [a, b]
+                for j in range(L["n"]):
+                    h = conv(conv(parts[-1], f"{nm}.m.{j}.cv1", 3), f"{nm}.m.{j}.cv2", 3)
+                    parts.append(parts[-1] + h if L["shortcut"] else h)
+                y = conv(torch.cat(parts, 1), nm + ".cv2", 1)
+            elif t == "SPPF":
+                parts = [conv(xi, nm + ".cv1", 1)]
+                for _ in range(3):
+                    parts.append(F.max_pool2d(parts[-1], L["k"], 1, L["k"] // 2))
+                y = conv(torch.cat(parts, 1), nm + ".cv2", 1)
+            elif t == "Upsample":
+                y = F.interpolate(xi, scale_factor=2.0, mode="nearest")
+            elif t == "Concat":
+                y = torch.cat([ys[j] for j in L["from"]], 1)
+            else:
+                for lvl, j in enumerate(L["from"]):
+                    h = conv(conv(ys[j], f"{nm}.cv3.{lvl}.0", 3), f"{nm}.cv3.{lvl}.1", 3)
+                    logits = F.conv2d(h, T(f"{nm}.cv3.{lvl}.2.weight"))[:, 0]   # class 0, no bias
+                    flat = logits.reshape(-1).numpy().astype(np.float64)
+                    q = 1.0 - float(target_per_image[lvl]) / (flat.size / n)
+                    thr = float(np.quantile(flat, min(max(q, 0.0), 1.0)))
+                    p[f"{nm}.cv3.{lvl}.2.bias"][0] = np.float32(-thr)
+                    conv(conv(ys[j], f"{nm}.cv2.{lvl}.0", 3), f"{nm}.cv2.{lvl}.1", 3)
+                y = None
+            ys.append(y)

@@ -1,11 +1,12 @@
 """CPU (torch fp32) interpreter of pcgpu programs — test infrastructure.
 
 Executes the serialized op list exactly as the device executor defines it
-(csrc/pc_api.cpp + pc_conv.hip semantics: K-segments, border-class bias,
-activation before/after the residual, nearest-2x residual, split-K, stem,
-max-pool), so the inference-time algebra in person_capture_amd/models.py (BN
-folding, pre-BN border tables, avg-down rewrite, PAFPN fusions) can be checked
-against the literal oracle nets without a GPU.
+(csrc/pc_api.cpp + pc_conv*.hip / pc_ops.hip semantics: K-segments, border-class
+bias, activation before/after the residual, nearest-2x residual, split-K, stem,
+max-pool, upsample, layernorm, attention) over buffer-level tensor views, so the
+inference-time algebra in person_capture_amd/models*.py (BN folding, pre-BN border
+tables, avg-down rewrite, PAFPN fusions, in-place concatenation slices, padded
+channel maps) can be checked against the literal oracle nets without a GPU.
 """
 import numpy as np
 import torch
@@ -21,27 +22,43 @@ def _act(y, act, slope):
         return torch.where(y > 0, y, y * slope.view(1, -1, 1, 1))
     if act == pg.ACT_SILU:
         return F.silu(y)
+    if act == pg.ACT_GELU:
+        return F.gelu(y)
     return y
 
 
 def run_program(P: pg.Program, x_nhwc: np.ndarray):
-    """x_nhwc: [N][H][W][C] input (padded channels). Returns list of outputs NCHW (padded channels)."""
-    T = {}
-    T[P.input] = torch.from_numpy(np.ascontiguousarray(np.transpose(x_nhwc, (0, 3, 1, 2)))).float()
+    """x_nhwc: [N][H][W][C] input (padded channels). Returns list of outputs NCHW (the
+    output tensors' channels)."""
+    N = x_nhwc.shape[0]
+    inp = torch.from_numpy(np.ascontiguousarray(np.transpose(x_nhwc, (0, 3, 1, 2)))).float()
+    bufs = {}
     A = [torch.from_numpy(a.astype(np.float32)) for a in P.arrays]
+
+    def read(t):
+        vb, H, W, C, cs, off, _ = P.tensors[t]
+        if vb < 0:
+            return inp[:, off:off + C]
+        return bufs[vb][:, off:off + C]
+
+    def write(t, y):
+        vb, H, W, C, cs, off, _ = P.tensors[t]
+        if vb not in bufs:
+            bufs[vb] = torch.zeros(N, cs, H, W)
+        bufs[vb][:, off:off + C] = y[:, :C]
+
     for w in P.ops:
         if w[0] == pg.OP_CONV:
-            out = P.tensors[w[1]]
             npad, ktot = w[14], w[15]
-            W = A[w[13]].view(npad, ktot)
+            Wm = A[w[13]].view(npad, ktot)
             acc = None
             k0 = 0
             for s in range(w[2]):
                 t, kh, kw, st, pd = w[3 + 5 * s: 8 + 5 * s]
-                X = T[t]
+                X = read(t)
                 cp = X.shape[1]
                 n = kh * kw * cp
-                ws = W[:, k0:k0 + n].view(npad, kh, kw, cp).permute(0, 3, 1, 2).contiguous()
+                ws = Wm[:, k0:k0 + n].reshape(npad, kh, kw, cp).permute(0, 3, 1, 2).contiguous()
                 k0 += n
                 y = F.conv2d(X, ws, stride=st, padding=pd)
                 acc = y if acc is None else acc + y
@@ -50,7 +67,8 @@ def run_program(P: pg.Program, x_nhwc: np.ndarray):
                 b = A[w[17]]
                 if w[18] == pg.BIAS_BORDER9:
                     t0, kh0, kw0, st0, pd0 = w[3:8]
-                    H, Wd = T[t0].shape[2], T[t0].shape[3]
+                    X0 = read(t0)
+                    H, Wd = X0.shape[2], X0.shape[3]
                     b9 = b.view(3, 3, npad)
                     ih0 = torch.arange(Ho) * st0 - pd0
                     iw0 = torch.arange(Wo) * st0 - pd0
@@ -61,21 +79,25 @@ def run_program(P: pg.Program, x_nhwc: np.ndarray):
                     acc = acc + b.view(1, -1, 1, 1)
             slope = A[w[19]] if w[19] >= 0 else None
             act = w[20]
-            res = T[w[21]] if w[21] >= 0 else None
+            res = read(w[21]) if w[21] >= 0 else None
             if res is not None and w[22] == pg.RES_UP2:
                 res = F.interpolate(res, size=(Ho, Wo), mode="nearest")
             if not w[23]:
                 acc = _act(acc, act, slope)
             if res is not None:
-                acc = acc + res
+                k = min(res.shape[1], acc.shape[1])
+                acc = acc.clone()
+                acc[:, :k] = acc[:, :k] + res[:, :k]
             if w[23]:
                 acc = _act(acc, act, slope)
-            C = out[3]
-            acc = acc[:, :C].clone()
-            acc[:, w[16]:] = 0
-            T[w[1]] = acc
+            C = P.tensors[w[1]][3]
+            out = torch.zeros(N, C, Ho, Wo)
+            k = min(C, npad)
+            out[:, :k] = acc[:, :k]
+            out[:, w[16]:] = 0
+            write(w[1], out)
         elif w[0] == pg.OP_STEM:
-            X = T[w[2]]
+            X = read(w[2])
             cout = w[8]
             wt = A[w[7]].view(cout, 3, 3, 4).permute(0, 3, 1, 2).contiguous()
             y = F.conv2d(X, wt, stride=w[5], padding=w[6]) + A[w[9]].view(1, -1, 1, 1)
@@ -83,7 +105,34 @@ def run_program(P: pg.Program, x_nhwc: np.ndarray):
             cp = P.tensors[w[1]][3]
             out = torch.zeros(y.shape[0], cp, y.shape[2], y.shape[3])
             out[:, :cout] = y
-            T[w[1]] = out
+            write(w[1], out)
         elif w[0] == pg.OP_MAXPOOL:
-            T[w[1]] = F.max_pool2d(T[w[2]], w[3], w[4], w[5])
-    return [T[o] for o in P.outputs]
+            write(w[1], F.max_pool2d(read(w[2]), w[3], w[4], w[5]))
+        elif w[0] == pg.OP_UPSAMPLE:
+            write(w[1], F.interpolate(read(w[2]), scale_factor=2.0, mode="nearest"))
+        elif w[0] == pg.OP_LAYERNORM:
+            X = read(w[2])                           # [N][C][H][W]
+            C = w[8]
+            x = X[:, :C].permute(0, 2, 3, 1).reshape(N, -1, C)
+            if w[5] >= 0:
+                x = x + A[w[5]].view(w[6], C)[None]
+            eps = float(np.int32(w[7]).view(np.float32))
+            y = F.layer_norm(x, (C,), A[w[3]], A[w[4]], eps)
+            H, W = X.shape[2], X.shape[3]
+            Cout = P.tensors[w[1]][3]
+            out = torch.zeros(N, Cout, H, W)
+            out[:, :C] = y.view(N, H, W, C).permute(0, 3, 1, 2)
+            write(w[1], out)
+        elif w[0] == pg.OP_ATTENTION:
+            X = read(w[2])
+            heads, d = w[3], w[4]
+            E = heads * d
+            Tn = X.shape[2] * X.shape[3]
+            x = X.permute(0, 2, 3, 1).reshape(N, Tn, -1)
+            q, k, v = (x[..., i * E:(i + 1) * E].reshape(N, Tn, heads, d).transpose(1, 2) for i in range(3))
+            a = torch.softmax((q * (1.0 / np.sqrt(d))) @ k.transpose(-1, -2), dim=-1) @ v
+            y = a.transpose(1, 2).reshape(N, Tn, E)
+            write(w[1], y.view(N, X.shape[2], X.shape[3], E).permute(0, 3, 1, 2))
+        else:
+            raise ValueError(f"unknown op {w[0]}")
+    return [read(o) for o in P.outputs]
