@@ -313,7 +313,7 @@ static void* tensor_ptr(pc_net* n, int t) {
 // Every activation buffer is followed by kZeroTail zero bytes: a padding tap of the
 // implicit-GEMM loader reads one K-tile row (any channel block of the pixel stride)
 // from there, so the tail covers the widest pixel row a conv reads.
-static const size_t kZeroTail = 16384;
+static const size_t kZeroTail = 65536;
 
 // bytes from a tensor's base to the zero tail of the buffer that holds it
 static unsigned tensor_zero_off(const pc_net* n, int t) {
