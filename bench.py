@@ -246,6 +246,10 @@ def main_other(args):
         from person_capture_amd.detectors import PersonDetector
         from person_capture_amd.reid_embedder import ReIDEmbedder
         det = PersonDetector("yolov8n.pt", device=f"cuda:{local}")
+        # the untrained synthetic SCRFD fires on ~150 anchors of a bilinearly upscaled person crop
+        # at 0.5 (it was calibrated on native-scale frames); 0.75 gives a few faces per crop as a
+        # trained detector would. Real weights need no such knob.
+        fe.conf = 0.75
         reid = ReIDEmbedder(device=f"cuda:{local}")
         dtuples = [(d.ptr, H, W, W * 3) for d in devs]
 
@@ -281,8 +285,12 @@ def main_other(args):
             return faces
         wl = (f"C5: pre-scan 4K frames -> INTER_AREA 416 wide, SCRFD-10G@384, ArcFace-R100 (1 forward), match vs "
               f"{bank_n}-embedding bank, batch {args.batch} frames per GPU")
-    for _ in range(args.warmup):
+    for k in range(args.warmup):
+        t = time.perf_counter()
         step()
+        ctx.sync()
+        print(f"[bench {args.workload}] warmup {k}: {time.perf_counter() - t:.3f} s {stats}", file=sys.stderr,
+              flush=True)
     if args.workload == "c5":
         nets.append(fe._engine(fe._dyn_for(small[0], None)).net)
     for n in nets:

@@ -143,7 +143,19 @@ static int fail(pc_ctx* c, int code, const std::string& msg) {
 
 static int stage_copy(pc_ctx* c, const void* h, size_t nbytes, void** d_out) {
   const size_t bytes = (nbytes + 255) & ~size_t(255);
-  if (bytes > c->stage_cap) return fail(c, PC_ERR_CAPACITY, "staging ring too small");
+  if (bytes > c->stage_cap) {
+    // grow the ring (rare: thousands of descriptors in one call); everything staged so
+    // far must have been consumed before the old buffers go
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    size_t cap = c->stage_cap;
+    while (cap < bytes) cap *= 2;
+    char *h = nullptr, *d = nullptr;
+    if (hipHostMalloc((void**)&h, cap, hipHostMallocDefault) != hipSuccess) return fail(c, PC_ERR_HIP, "staging grow");
+    if (hipMalloc((void**)&d, cap) != hipSuccess) { hipHostFree(h); return fail(c, PC_ERR_HIP, "staging grow"); }
+    hipHostFree(c->stage_h);
+    hipFree(c->stage_d);
+    c->stage_h = h; c->stage_d = d; c->stage_cap = cap; c->stage_off = 0;
+  }
   if (c->stage_off + bytes > c->stage_cap) {
     // wrap: everything previously staged must have been consumed
     HIPCHK(c, hipStreamSynchronize(c->stream));

@@ -218,8 +218,11 @@ class FaceEmbedder:
     def _engine(self, D: int) -> ScrfdEngine:
         e = self._scrfd_engines.get(D)
         if e is None:
+            # heavy fallback sizes (up to 2048) run on single frames: keep their activation
+            # buffers at the footprint of a det_batch x 640 engine
+            mb = max(1, min(self._det_batch, self._det_batch * 640 * 640 // (D * D)))
             e = ScrfdEngine(self._ctx, self._scrfd_params, self.scrfd_variant, D=D, precision=self.precision,
-                            max_batch=self._det_batch, max_det=1024)
+                            max_batch=mb, max_det=1024)
             self._scrfd_engines[D] = e
         return e
 

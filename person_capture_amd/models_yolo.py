@@ -119,7 +119,7 @@ def _conv_init(rng, p: Params, name: str, c1: int, c2: int, k: int) -> None:
     p[name + ".bn.running_var"] = np.ones(c2, np.float32)
 
 
-def synth_yolov8(scale: str = "n", seed: int = 0, calibrate: bool = True, target_per_image=(3.0, 2.0, 1.0)) -> Params:
+def synth_yolov8(scale: str = "n", seed: int = 0, calibrate: bool = True, target_per_image=(1.5, 0.8, 0.4)) -> Params:
     """Seeded YOLOv8 weights (state-dict names of ultralytics' DetectionModel)."""
     rng = np.random.default_rng(np.random.SeedSequence([20260503, ord(scale), seed]))
     p: Params = {}
