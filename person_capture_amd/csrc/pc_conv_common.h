@@ -216,105 +216,163 @@ __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, f32x4 (&a
       });
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < PP * CG; i += NT) {
-      const int pl = i / CG, cg = i & (CG - 1);
-      const int pix = p0 + pbase + pl;
-      const int ch = c0 + cbase + cg * 8;
-      if (pix >= p.M || ch >= p.cwrite) continue;
-      float v[8];
-      {
-        const f32x4 lo = *reinterpret_cast<const f32x4*>(smem + (pl * RS + cg * 8) * 4);
-        const f32x4 hi = *reinterpret_cast<const f32x4*>(smem + (pl * RS + cg * 8 + 4) * 4);
-        v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
-        v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
-      }
+    // A thread keeps one 8-channel group for all its pixel rows (NT % CG == 0), so the
+    // per-channel bias / slopes are loaded once, and every residual row is requested
+    // before the first store: the finishing loop no longer waits on one global load per
+    // row (latency-bound at one workgroup per CU).
+    static_assert((PP * CG) % NT == 0 && NT % CG == 0, "epilogue work split");
+    constexpr int IT = PP * CG / NT;     // pixel rows per thread
+    constexpr int PSTEP = NT / CG;       // pixel-row stride between them
+    const int cg = threadIdx.x & (CG - 1);
+    const int pl0 = threadIdx.x / CG;
+    const int ch = c0 + cbase + cg * 8;
+    if (ch < p.cwrite) {
       const int nv = min(8, p.cwrite - ch);
       const bool full = nv == 8 && vec_ok;
-      int n = 0, oh = 0, ow = 0;
-      if (p.bias_mode == BIAS_BORDER9 || p.res_mode == RES_UP2) {
-        n = pix / hw;
-        const int rem = pix - n * hw;
-        oh = rem / p.OW;
-        ow = rem - oh * p.OW;
+      float bc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (p.bias_mode == BIAS_CHANNEL) {   // bias arrays span npad >= ch + 8
+        const f32x4 b0 = *reinterpret_cast<const f32x4*>(p.bias + ch);
+        const f32x4 b1 = *reinterpret_cast<const f32x4*>(p.bias + ch + 4);
+        bc[0] = b0[0]; bc[1] = b0[1]; bc[2] = b0[2]; bc[3] = b0[3];
+        bc[4] = b1[0]; bc[5] = b1[1]; bc[6] = b1[2]; bc[7] = b1[3];
       }
-      if (p.bias_mode != BIAS_NONE) {
-        int bofs = 0;
-        if (p.bias_mode == BIAS_BORDER9) {
-          const ConvSeg& S = p.seg[0];
-          const int ih0 = oh * S.stride - S.pad, iw0 = ow * S.stride - S.pad;
-          const int rc = ih0 < 0 ? 0 : (ih0 + S.KH - 1 >= S.H ? 2 : 1);
-          const int cc = iw0 < 0 ? 0 : (iw0 + S.KW - 1 >= S.W ? 2 : 1);
-          bofs = (rc * 3 + cc) * p.npad;
-        }
-        const float* bp = p.bias + bofs + ch;   // bias arrays span npad >= ch + 8
-        const f32x4 b0 = *reinterpret_cast<const f32x4*>(bp);
-        const f32x4 b1 = *reinterpret_cast<const f32x4*>(bp + 4);
-        v[0] += b0[0]; v[1] += b0[1]; v[2] += b0[2]; v[3] += b0[3];
-        v[4] += b1[0]; v[5] += b1[1]; v[6] += b1[2]; v[7] += b1[3];
-      }
-      float sl[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      // branch-light finishing: the piecewise-linear activations become one select with a
+      // per-lane negative slope (1 = none, 0 = ReLU, a = PReLU); SiLU / GELU take one
+      // uniform branch per row; channel padding is a per-lane keep mask
+      float sl[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
       if (p.act == ACT_PRELU) {
         const f32x4 s0 = *reinterpret_cast<const f32x4*>(p.slope + ch);
         const f32x4 s1 = *reinterpret_cast<const f32x4*>(p.slope + ch + 4);
         sl[0] = s0[0]; sl[1] = s0[1]; sl[2] = s0[2]; sl[3] = s0[3];
         sl[4] = s1[0]; sl[5] = s1[1]; sl[6] = s1[2]; sl[7] = s1[3];
-      }
-      if (!p.act_after_res) {
+      } else if (p.act == ACT_RELU) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j], p.act, sl[j]);
+        for (int j = 0; j < 8; ++j) sl[j] = 0.f;
       }
+      const bool smooth = p.act == ACT_SILU || p.act == ACT_GELU;
+      const bool has_res = p.res_mode != RES_NONE;
+      const bool pre_act = !p.act_after_res;
+      bool keep[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) keep[j] = ch + j < p.cout;
+      auto act8 = [&](float* v) __attribute__((always_inline)) {
+        if (smooth) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j], p.act, 0.f);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = v[j] > 0.f ? v[j] : v[j] * sl[j];
+        }
+      };
+      // residual rows, requested a group of RG rows at a time before the group's stores
+      // (raw activation-dtype vectors; RG bounded so the second pass's accumulators and
+      // these stay within the 256 registers of a 2-waves-per-SIMD kernel)
+      using RV = typename std::conditional<ESZ == 2, f16x8, f32x4>::type;
+      constexpr int RN = ESZ == 2 ? 1 : 2;
+      constexpr int RG = (NPASS == 2 ? 2 : 4) < IT ? (NPASS == 2 ? 2 : 4) : IT;
+      static_assert(IT % RG == 0, "residual groups");
+#pragma unroll 1
+      for (int kg = 0; kg < IT; kg += RG) {
+      RV rv[RG][RN];
       if (p.res_mode != RES_NONE) {
-        long long rpix = pix;
-        if (p.res_mode == RES_UP2) rpix = ((long long)n * p.rH + (oh >> 1)) * p.rW + (ow >> 1);
-        const T* rp = reinterpret_cast<const T*>(p.res) + rpix * p.rcs + ch;
-        if (full) {
-          if constexpr (ESZ == 2) {
-            const f16x8 r = *reinterpret_cast<const f16x8*>(rp);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] += (float)r[j];
-          } else {
-            const f32x4 r0 = *reinterpret_cast<const f32x4*>(rp);
-            const f32x4 r1 = *reinterpret_cast<const f32x4*>(rp + 4);
-            v[0] += r0[0]; v[1] += r0[1]; v[2] += r0[2]; v[3] += r0[3];
-            v[4] += r1[0]; v[5] += r1[1]; v[6] += r1[2]; v[7] += r1[3];
+        for (int kk = 0; kk < RG; ++kk) {
+          const int k = kk;
+          const int pix = p0 + pbase + pl0 + (kg + kk) * PSTEP;
+#pragma unroll
+          for (int j = 0; j < RN; ++j) rv[k][j] = RV{};
+          if (pix < p.M && full) {
+            long long rpix = pix;
+            if (p.res_mode == RES_UP2) {
+              const int n = pix / hw, rem = pix - (pix / hw) * hw;
+              const int oh = rem / p.OW, ow = rem - (rem / p.OW) * p.OW;
+              rpix = ((long long)n * p.rH + (oh >> 1)) * p.rW + (ow >> 1);
+            }
+            const T* rp = reinterpret_cast<const T*>(p.res) + rpix * p.rcs + ch;
+#pragma unroll
+            for (int j = 0; j < RN; ++j) rv[k][j] = *reinterpret_cast<const RV*>(rp + j * (8 / RN));
           }
-        } else {
-          for (int j = 0; j < nv; ++j) v[j] += (float)rp[j];
         }
       }
-      if (p.act_after_res) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j], p.act, sl[j]);
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (ch + j >= p.cout) v[j] = 0.f;   // keep channel padding exactly zero
-      if (p.out_f32) {
-        float* yp = reinterpret_cast<float*>(p.y) + (long long)pix * p.ycs + ch;
-        if (full) {
-          *reinterpret_cast<f32x4*>(yp) = f32x4{v[0], v[1], v[2], v[3]};
-          *reinterpret_cast<f32x4*>(yp + 4) = f32x4{v[4], v[5], v[6], v[7]};
-        } else {
-          for (int j = 0; j < nv; ++j) yp[j] = v[j];
+      for (int k = 0; k < RG; ++k) {
+        const int pl = pl0 + (kg + k) * PSTEP;
+        const int pix = p0 + pbase + pl;
+        if (pix >= p.M) continue;
+        float v[8];
+        {
+          const f32x4 lo = *reinterpret_cast<const f32x4*>(smem + (pl * RS + cg * 8) * 4);
+          const f32x4 hi = *reinterpret_cast<const f32x4*>(smem + (pl * RS + cg * 8 + 4) * 4);
+          v[0] = lo[0] + bc[0]; v[1] = lo[1] + bc[1]; v[2] = lo[2] + bc[2]; v[3] = lo[3] + bc[3];
+          v[4] = hi[0] + bc[4]; v[5] = hi[1] + bc[5]; v[6] = hi[2] + bc[6]; v[7] = hi[3] + bc[7];
         }
-      } else {
-        T* yp = reinterpret_cast<T*>(p.y) + (long long)pix * p.ycs + ch;
-        if constexpr (ESZ == 2) {
+        int n = 0, oh = 0, ow = 0;
+        if (p.bias_mode == BIAS_BORDER9 || (p.res_mode == RES_UP2 && !full)) {
+          n = pix / hw;
+          const int rem = pix - n * hw;
+          oh = rem / p.OW;
+          ow = rem - oh * p.OW;
+        }
+        if (p.bias_mode == BIAS_BORDER9) {
+          const ConvSeg& S = p.seg[0];
+          const int ih0 = oh * S.stride - S.pad, iw0 = ow * S.stride - S.pad;
+          const int rc = ih0 < 0 ? 0 : (ih0 + S.KH - 1 >= S.H ? 2 : 1);
+          const int cc = iw0 < 0 ? 0 : (iw0 + S.KW - 1 >= S.W ? 2 : 1);
+          const float* bp = p.bias + (rc * 3 + cc) * p.npad + ch;
+          const f32x4 b0 = *reinterpret_cast<const f32x4*>(bp);
+          const f32x4 b1 = *reinterpret_cast<const f32x4*>(bp + 4);
+          v[0] += b0[0]; v[1] += b0[1]; v[2] += b0[2]; v[3] += b0[3];
+          v[4] += b1[0]; v[5] += b1[1]; v[6] += b1[2]; v[7] += b1[3];
+        }
+        if (pre_act) act8(v);
+        if (has_res) {
           if (full) {
-            *reinterpret_cast<f16x8*>(yp) = f16x8{(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3],
-                                                  (f16)v[4], (f16)v[5], (f16)v[6], (f16)v[7]};
+            if constexpr (ESZ == 2) {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) v[j] += (float)rv[k][0][j];
+            } else {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) { v[j] += rv[k][0][j]; v[4 + j] += rv[k][1][j]; }
+            }
           } else {
-            for (int j = 0; j < nv; ++j) yp[j] = (T)v[j];
+            long long rpix = pix;
+            if (p.res_mode == RES_UP2) rpix = ((long long)n * p.rH + (oh >> 1)) * p.rW + (ow >> 1);
+            const T* rp = reinterpret_cast<const T*>(p.res) + rpix * p.rcs + ch;
+            for (int j = 0; j < nv; ++j) v[j] += (float)rp[j];
           }
-        } else {
+        }
+        if (!pre_act) act8(v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = keep[j] ? v[j] : 0.f;   // channel padding stays exactly zero
+        if (p.dbg & 16) continue;   // tuning only: no stores
+        if (p.out_f32) {
+          float* yp = reinterpret_cast<float*>(p.y) + (long long)pix * p.ycs + ch;
           if (full) {
             *reinterpret_cast<f32x4*>(yp) = f32x4{v[0], v[1], v[2], v[3]};
             *reinterpret_cast<f32x4*>(yp + 4) = f32x4{v[4], v[5], v[6], v[7]};
           } else {
             for (int j = 0; j < nv; ++j) yp[j] = v[j];
           }
+        } else {
+          T* yp = reinterpret_cast<T*>(p.y) + (long long)pix * p.ycs + ch;
+          if constexpr (ESZ == 2) {
+            if (full) {
+              *reinterpret_cast<f16x8*>(yp) = f16x8{(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3],
+                                                    (f16)v[4], (f16)v[5], (f16)v[6], (f16)v[7]};
+            } else {
+              for (int j = 0; j < nv; ++j) yp[j] = (T)v[j];
+            }
+          } else {
+            if (full) {
+              *reinterpret_cast<f32x4*>(yp) = f32x4{v[0], v[1], v[2], v[3]};
+              *reinterpret_cast<f32x4*>(yp + 4) = f32x4{v[4], v[5], v[6], v[7]};
+            } else {
+              for (int j = 0; j < nv; ++j) yp[j] = v[j];
+            }
+          }
         }
       }
+      }   // residual groups
     }
     if (pass + 1 < NPASS) __syncthreads();
   }

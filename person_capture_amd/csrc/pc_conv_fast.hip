@@ -211,13 +211,14 @@ __global__ __launch_bounds__(64 * WC * WP, 1) void conv_fast(ConvParams p) {
     constexpr int j = decltype(jc)::value;
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NSTAGE - 2) * NI) : "memory");
     bar();
-    issue(std::integral_constant<int, (j + NSTAGE - 1) % NSTAGE>{}, kiss);
+    if (!(p.dbg & 1)) issue(std::integral_constant<int, (j + NSTAGE - 1) % NSTAGE>{}, kiss);   // dbg: tuning only
     const bool more = kiss + 1 < nk;
     advance(more);
     kiss += more ? 1 : 0;
-    compute(std::integral_constant<int, j>{});
+    if (!(p.dbg & 2)) compute(std::integral_constant<int, j>{});
   };
   int it = 0;
+  if (p.dbg & 8) return;   // tuning only: prologue only
   for (; it + NSTAGE <= nk; it += NSTAGE)
     static_for<NSTAGE>([&](auto jc) __attribute__((always_inline)) { step(jc); });
   static_for<NSTAGE - 1>([&](auto jc) __attribute__((always_inline)) {
@@ -227,6 +228,7 @@ __global__ __launch_bounds__(64 * WC * WP, 1) void conv_fast(ConvParams p) {
   // drain the (dummy) tail DMAs and every wave's last reads before the LDS is reused
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if (p.dbg & 4) return;   // tuning only: skip the epilogue
   if constexpr (((BC / 8) & (BC / 8 - 1)) == 0 && ((BC / 16) & (BC / 16 - 1)) == 0)
     conv_epilogue_lds<T, BC, BP, WC, WP>(p, acc, c0, p0, wr, wc, lane, smem);
   else   // 96 / 224 channel tiles: per-fragment stores

@@ -68,7 +68,7 @@ def _oracle_heads(p, canvas):
 
 
 def test_yolo_net_and_post_f32(gpu_ctx, y8n):
-    fr = _frame(7, 1080, 1920)
+    fr = _frame(100, 1080, 1920)   # 5 oracle detections at conf 0.1 (synthetic weights)
     canvas, (_, _, _, _, Hp, Wp) = ra.yolo_letterbox(fr)
     eng = YoloEngine(gpu_ctx, y8n, "n", Hp, Wp, precision=PC_PREC_F32, max_batch=2)
     x = np.zeros((1, Hp, Wp, 4), np.float32)
@@ -84,8 +84,8 @@ def test_yolo_net_and_post_f32(gpu_ctx, y8n):
         assert np.abs(o - r).max() / max(1.0, np.abs(r).max()) < 1e-4
     # the full device pipeline on this frame: decode + NMS + scale_boxes of the device heads
     dsrc = gpu_ctx.upload(fr)
-    got = eng.read(eng.detect_device([(dsrc.ptr, 1080, 1920, fr.strides[0])], 0.35), 1)[0]
-    want = ra.yolo_postprocess(dev, 0.35, 0.45, 40, Hp, Wp, 1080, 1920)
+    got = eng.read(eng.detect_device([(dsrc.ptr, 1080, 1920, fr.strides[0])], 0.1), 1)[0]
+    want = ra.yolo_postprocess(dev, 0.1, 0.45, 40, Hp, Wp, 1080, 1920)
     assert len(want) > 0
     assert np.array_equal(got, want)
 
