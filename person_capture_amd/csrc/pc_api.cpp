@@ -431,7 +431,7 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl) {
     }
     if ((double)npad * w[15] * esz >= 4294967296.0) ok = false;
     if (ok) {
-      static const double cost[] = {1.0, 1.12, 1.12, 1.3, 1.3, 1.3, 1.15, 1.45, 1.3};
+      static const double cost[] = {1.0, 1.12, 1.12, 1.3, 1.3, 1.3, 1.15, 1.45, 1.3, 1.0};
       int best = -1;
       double best_t = 0;
       for (int k = 0; k < conv_fast_num_cfgs(); ++k) {

@@ -9,11 +9,22 @@
 
 namespace pc {
 
+// erf(x) to 1.5e-7 absolute (Abramowitz & Stegun 7.1.26): a handful of instructions
+// instead of the libm expansion, which matters in epilogues unrolled over 8 x rows
+__device__ __forceinline__ float erf_fast(float x) {
+  const float ax = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(1.0f + 0.3275911f * ax);
+  const float poly = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f +
+                     t * 1.061405429f))));
+  const float r = 1.0f - poly * __expf(-ax * ax);
+  return copysignf(r, x);
+}
+
 __device__ __forceinline__ float act_apply(float v, int act, float slope) {
   if (act == ACT_RELU) return v > 0.f ? v : 0.f;
   if (act == ACT_PRELU) return v > 0.f ? v : v * slope;
-  if (act == ACT_SILU) return v / (1.0f + __expf(-v));
-  if (act == ACT_GELU) return 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));   // nn.GELU (erf)
+  if (act == ACT_SILU) return v * __builtin_amdgcn_rcpf(1.0f + __expf(-v));
+  if (act == ACT_GELU) return 0.5f * v * (1.0f + erf_fast(v * 0.70710678118654752f));   // nn.GELU (erf)
   return v;
 }
 
@@ -257,8 +268,13 @@ __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, f32x4 (&a
       for (int j = 0; j < 8; ++j) keep[j] = ch + j < p.cout;
       auto act8 = [&](float* v) __attribute__((always_inline)) {
         if (smooth) {
+          if (p.act == ACT_SILU) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j], p.act, 0.f);
+            for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j], ACT_SILU, 0.f);
+          } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j], ACT_GELU, 0.f);
+          }
         } else {
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[j] = v[j] > 0.f ? v[j] : v[j] * sl[j];
@@ -324,8 +340,7 @@ __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, f32x4 (&a
           v[0] += b0[0]; v[1] += b0[1]; v[2] += b0[2]; v[3] += b0[3];
           v[4] += b1[0]; v[5] += b1[1]; v[6] += b1[2]; v[7] += b1[3];
         }
-        if (pre_act) act8(v);
-        if (has_res) {
+        if (has_res && !pre_act) {   // act(acc + bias + residual): residual first
           if (full) {
             if constexpr (ESZ == 2) {
 #pragma unroll
@@ -341,7 +356,23 @@ __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, f32x4 (&a
             for (int j = 0; j < nv; ++j) v[j] += (float)rp[j];
           }
         }
-        if (!pre_act) act8(v);
+        act8(v);   // the one activation point
+        if (has_res && pre_act) {
+          if (full) {
+            if constexpr (ESZ == 2) {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) v[j] += (float)rv[k][0][j];
+            } else {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) { v[j] += rv[k][0][j]; v[4 + j] += rv[k][1][j]; }
+            }
+          } else {
+            long long rpix = pix;
+            if (p.res_mode == RES_UP2) rpix = ((long long)n * p.rH + (oh >> 1)) * p.rW + (ow >> 1);
+            const T* rp = reinterpret_cast<const T*>(p.res) + rpix * p.rcs + ch;
+            for (int j = 0; j < nv; ++j) v[j] += (float)rp[j];
+          }
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = keep[j] ? v[j] : 0.f;   // channel padding stays exactly zero
         if (p.dbg & 16) continue;   // tuning only: no stores

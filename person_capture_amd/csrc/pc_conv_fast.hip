@@ -255,6 +255,7 @@ static const FastCfg kFastCfgs[] = {
     {64, 512, 8},    // 6: 1x8 waves, 64x64 per wave, 3 stages
     {32, 256, 4},    // 7: 1x4 waves, 32x64 per wave, 3 stages
     {224, 128, 4},   // 8: 2x2 waves, 112x64 per wave, 2 stages
+    {128, 512, 8},   // 9: 2x4 waves, 64x128 per wave, 2 stages (ROWB 64: 4)
 };
 static const int kNumFastCfgs = sizeof(kFastCfgs) / sizeof(kFastCfgs[0]);
 
@@ -291,6 +292,7 @@ static hipError_t launch_fast_t(const ConvParams& p, int cfg, hipStream_t s) {
     case 6: return launch_fast_cfg<T, 64, 512, ROWB, 1, 8, ROWB == 128 ? 2 : 4>(p, s);
     case 7: return launch_fast_cfg<T, 32, 256, ROWB, 1, 4, S3>(p, s);
     case 8: return launch_fast_cfg<T, 224, 128, ROWB, 2, 2, S3>(p, s);
+    case 9: return launch_fast_cfg<T, 128, 512, ROWB, 2, 4, ROWB == 128 ? 2 : 4>(p, s);
     default: return hipErrorInvalidValue;
   }
 }
