@@ -4,6 +4,7 @@ libpcgpu's pc_host.cpp), warp descriptors."""
 from __future__ import annotations
 
 import ctypes as C
+import functools
 import math
 from typing import List, Optional, Sequence, Tuple
 
@@ -21,8 +22,14 @@ BORDER_REFLECT_101 = 4
 
 def area_tables(ssize: int, dsize: int, scale: float = None):
     """cv::computeResizeAreaTab (cn = 1) as ctypes arrays + per-destination start offsets.
-    scale defaults to ssize/dsize (explicit dsize); cv2.resize(fx=s) uses 1/s."""
+    scale defaults to ssize/dsize (explicit dsize); cv2.resize(fx=s) uses 1/s.
+    Cached per (ssize, dsize, scale): the pre-scan resizes every frame with one geometry."""
     scale = float(ssize) / dsize if scale is None else float(scale)
+    return _area_tables(int(ssize), int(dsize), scale)
+
+
+@functools.lru_cache(maxsize=256)
+def _area_tables(ssize: int, dsize: int, scale: float):
     si: List[int] = []
     di: List[int] = []
     al: List[float] = []

@@ -102,3 +102,18 @@ def test_ctor_errors_mirror_reference():
         fe_mod.FaceEmbedder(ctx="cuda", yolo_model="yolov8l-face.pt")
     with pytest.raises(RuntimeError):
         fe_mod.FaceEmbedder(ctx="cuda", yolo_model="scrfd_10g_bnkps", use_arcface=False)
+
+
+def test_person_reid_ctor_errors_mirror_reference():
+    """No CPU path on this build: device='cpu' raises RuntimeError at construction, like the
+    reference does when its backend is unavailable (detectors.py:28-31, reid_embedder.py:24-27);
+    an OpenCLIP tower this build does not have is refused the same way."""
+    from person_capture_amd.detectors import PersonDetector
+    from person_capture_amd.models_clip import clip_cfg
+    from person_capture_amd.reid_embedder import ReIDEmbedder
+    with pytest.raises(RuntimeError):
+        PersonDetector("yolov8n.pt", device="cpu")
+    with pytest.raises(RuntimeError):
+        ReIDEmbedder(device="cpu")
+    with pytest.raises(RuntimeError):
+        clip_cfg("RN50x64")

@@ -39,7 +39,7 @@ def main():
     for ctr, kern in vals.items():
         for name, v in kern.items():
             per_kernel.setdefault(name, {})[ctr] = (sum(v) / len(v), len(v))
-    conv = {k: v for k, v in per_kernel.items() if "conv_igemm" in k}
+    conv = {k: v for k, v in per_kernel.items() if any(t in k for t in ("conv_igemm", "conv_fast", "conv_halo"))}
     fetch = sum(v.get("FETCH_SIZE", (0, 0))[0] * v.get("FETCH_SIZE", (0, 0))[1] for v in conv.values())
     nf = sum(v.get("FETCH_SIZE", (0, 0))[1] for v in conv.values())
     write = sum(v.get("WRITE_SIZE", (0, 0))[0] * v.get("WRITE_SIZE", (0, 0))[1] for v in conv.values())
