@@ -431,21 +431,23 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl) {
     }
     if ((double)npad * w[15] * esz >= 4294967296.0) ok = false;
     if (ok) {
-      static const double cost[] = {1.0, 1.12, 1.12, 1.3, 1.3, 1.3, 1.15, 1.45, 1.3, 1.0};
-      int best = -1;
+      static const double cost[] = {1.0, 1.12, 1.12, 1.3, 1.3, 1.3, 1.15, 1.45, 1.3, 1.0, 0.9};
+      static const int occ[] = {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2};   // workgroups per CU
+      int best = -1, best_rowb = rowb;
       double best_t = 0;
       for (int k = 0; k < conv_fast_num_cfgs(); ++k) {
         int bc = 0, bp = 0;
         conv_fast_tile(k, &bc, &bp);
-        if (npad % bc || !conv_fast_valid(k, rowb)) continue;
+        const int rb = k == 10 ? 64 : rowb;   // cfg 10 runs on 64-byte K rows only
+        if (npad % bc || !conv_fast_valid(k, rb)) continue;
         if (force > 0 && k != force - 1) continue;
         const long long t = (M + bp - 1) / bp * (npad / bc);
-        const double rounds = (double)((t + 255) / 256);
-        const double est = rounds * bc * bp * cost[k];
-        if (best < 0 || est < best_t) { best = k; best_t = est; }
+        const double rounds = (double)((t + 256 * occ[k] - 1) / (256 * occ[k]));
+        const double est = rounds * bc * bp * occ[k] * cost[k];
+        if (best < 0 || est < best_t) { best = k; best_t = est; best_rowb = rb; }
       }
       pl.fast = best;
-      if (best >= 0) { pl.halo = -1; pl.rowb = rowb; }
+      if (best >= 0) { pl.halo = -1; pl.rowb = best_rowb; }
     }
   }
   if (Y.C > npad) return fail(n->ctx, PC_ERR_FORMAT, "conv output tensor wider than npad");

@@ -189,12 +189,12 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, f32x4 (&acc)[
 // - bias (per channel or border class), activation, residual, zeroed channel
 // padding - and stores them with one 16-byte (f16) or two (f32) stores, so each
 // pixel row of the tile leaves as contiguous bytes and no load waits behind a store.
-template <typename T, int BC, int BP, int WC, int WP>
+template <typename T, int BC, int BP, int WC, int WP, int EPI_MAX = 131072>
 __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, f32x4 (&acc)[BC / WC / 16][BP / WP / 16],
                                                   int c0, int p0, int wr, int wc, int lane, char* smem) {
   constexpr int NW = WC * WP, NT = 64 * NW;
   constexpr int WTC = BC / WC, WTP = BP / WP, TC = WTC / 16, TP = WTP / 16;
-  constexpr bool ONE = BC * BP * 4 <= 131072;
+  constexpr bool ONE = BC * BP * 4 <= EPI_MAX;   // EPI_MAX: LDS the image may use (2 WGs/CU: half)
   constexpr bool SPLIT_C = !ONE && WC >= 2;
   static_assert(ONE || WC >= 2 || WP >= 2, "epilogue split");
   constexpr int PC = ONE ? BC : (SPLIT_C ? BC / 2 : BC);

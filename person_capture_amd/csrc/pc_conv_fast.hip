@@ -26,15 +26,17 @@
 
 namespace pc {
 
-template <int BC, int BP, int WC, int WP>
+template <int BC, int BP, int WC, int WP, int EPI_MAX = 131072>
 __host__ __device__ constexpr int fast_epi_bytes() {
   // LDS image of conv_epilogue_lds (one or two passes)
-  return BC * BP * 4 <= 131072 ? BP * (BC + 4) * 4
+  return BC * BP * 4 <= EPI_MAX ? BP * (BC + 4) * 4
                                : (WC >= 2 ? BP * (BC / 2 + 4) * 4 : (BP / 2) * (BC + 4) * 4);
 }
 
-template <typename T, int BC, int BP, int ROWB, int WC, int WP, int NSTAGE>
-__global__ __launch_bounds__(64 * WC * WP, 1) void conv_fast(ConvParams p) {
+// OCC: workgroups per CU the tile is sized for (LDS <= 160 KiB / OCC); with OCC = 2 one
+// workgroup's epilogue and DMA waits overlap the other's MFMAs.
+template <typename T, int BC, int BP, int ROWB, int WC, int WP, int NSTAGE, int OCC = 1>
+__global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fast(ConvParams p) {
   constexpr int NW = WC * WP;
   constexpr int ESZ = sizeof(T);
   constexpr int CHUNKS = ROWB / 16;
@@ -47,9 +49,10 @@ __global__ __launch_bounds__(64 * WC * WP, 1) void conv_fast(ConvParams p) {
   constexpr int TC = WTC / 16, TP = WTP / 16;
   constexpr int BUF = (BC + BP) * ROWB;
   constexpr int RING = NSTAGE * BUF;
-  constexpr int EPI = fast_epi_bytes<BC, BP, WC, WP>();
+  constexpr int EPI_MAX = OCC == 1 ? 131072 : 65536;
+  constexpr int EPI = fast_epi_bytes<BC, BP, WC, WP, EPI_MAX>();
   constexpr int SMEM = RING > EPI ? RING : EPI;
-  static_assert(SMEM <= 163840, "LDS");
+  static_assert(SMEM * OCC <= 163840, "LDS");
   static_assert(WTC % 16 == 0 && WTP % 16 == 0, "wave tile");
   static_assert(NSTAGE >= 2, "ring depth");
 
@@ -230,7 +233,7 @@ __global__ __launch_bounds__(64 * WC * WP, 1) void conv_fast(ConvParams p) {
   __syncthreads();
   if (p.dbg & 4) return;   // tuning only: skip the epilogue
   if constexpr (((BC / 8) & (BC / 8 - 1)) == 0 && ((BC / 16) & (BC / 16 - 1)) == 0)
-    conv_epilogue_lds<T, BC, BP, WC, WP>(p, acc, c0, p0, wr, wc, lane, smem);
+    conv_epilogue_lds<T, BC, BP, WC, WP, EPI_MAX>(p, acc, c0, p0, wr, wc, lane, smem);
   else   // 96 / 224 channel tiles: per-fragment stores
     conv_epilogue<T, TC, TP, WTC, WTP>(p, acc, c0, p0, wr, wc, lane, 0);
 }
@@ -256,6 +259,7 @@ static const FastCfg kFastCfgs[] = {
     {32, 256, 4},    // 7: 1x4 waves, 32x64 per wave, 3 stages
     {224, 128, 4},   // 8: 2x2 waves, 112x64 per wave, 2 stages
     {128, 512, 8},   // 9: 2x4 waves, 64x128 per wave, 2 stages (ROWB 64: 4)
+    {128, 256, 4},   // 10: 2x2 waves, 64x128 per wave, ROWB 64 only, 3 stages, 2 workgroups per CU
 };
 static const int kNumFastCfgs = sizeof(kFastCfgs) / sizeof(kFastCfgs[0]);
 
@@ -268,13 +272,13 @@ int conv_fast_tile(int cfg, int* bc, int* bp) {
   return 1;
 }
 
-template <typename T, int BC, int BP, int ROWB, int WC, int WP, int NSTAGE>
+template <typename T, int BC, int BP, int ROWB, int WC, int WP, int NSTAGE, int OCC = 1>
 static hipError_t launch_fast_cfg(const ConvParams& p, hipStream_t s) {
   if constexpr (!fast_valid<BC, BP, ROWB, WC * WP>()) {
     return hipErrorInvalidValue;
   } else {
     const int nwg = (p.M + BP - 1) / BP * (p.npad / BC);
-    hipLaunchKernelGGL((conv_fast<T, BC, BP, ROWB, WC, WP, NSTAGE>), dim3(nwg), dim3(64 * WC * WP), 0, s, p);
+    hipLaunchKernelGGL((conv_fast<T, BC, BP, ROWB, WC, WP, NSTAGE, OCC>), dim3(nwg), dim3(64 * WC * WP), 0, s, p);
     return hipGetLastError();
   }
 }
@@ -293,6 +297,9 @@ static hipError_t launch_fast_t(const ConvParams& p, int cfg, hipStream_t s) {
     case 7: return launch_fast_cfg<T, 32, 256, ROWB, 1, 4, S3>(p, s);
     case 8: return launch_fast_cfg<T, 224, 128, ROWB, 2, 2, S3>(p, s);
     case 9: return launch_fast_cfg<T, 128, 512, ROWB, 2, 4, ROWB == 128 ? 2 : 4>(p, s);
+    case 10:
+      if constexpr (ROWB == 64) return launch_fast_cfg<T, 128, 256, 64, 2, 2, 3, 2>(p, s);
+      else return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }
 }
@@ -301,6 +308,7 @@ static hipError_t launch_fast_t(const ConvParams& p, int cfg, hipStream_t s) {
 int conv_fast_valid(int cfg, int rowb) {
   if (cfg < 0 || cfg >= kNumFastCfgs || (rowb != 64 && rowb != 128)) return 0;
   const FastCfg& c = kFastCfgs[cfg];
+  if (cfg == 10 && rowb != 64) return 0;   // sized for 2 workgroups per CU at 64-byte K rows
   const int rpi = 1024 / rowb;
   return (c.bc / rpi) % c.nw == 0 && (c.bp / rpi) % c.nw == 0;
 }
