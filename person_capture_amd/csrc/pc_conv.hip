@@ -374,6 +374,48 @@ __global__ void stem_im2col(StemParams p, int cin_true, T* __restrict__ col) {
   for (int j = 0; j < 8; ++j) dst[j] = v[j];
 }
 
+// The common stem (3x3 window, 3 true channels of an NHWC4 input): one thread per output
+// pixel gathers the nine 4-channel input pixels with one vector load each and writes
+// its 32-element im2col row ([tap][c] order, 27 values + 5 zeros) as full 16-byte
+// stores - the generic gather above issues 8 scalar loads and stores per 8 elements.
+template <typename T>
+__global__ void stem_im2col3(StemParams p, T* __restrict__ col) {
+  const long long pix = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long M = (long long)p.N * p.OH * p.OW;
+  if (pix >= M) return;
+  const int hw = p.OH * p.OW;
+  const int n = (int)(pix / hw);
+  const int rem = (int)(pix - (long long)n * hw);
+  const int oh = rem / p.OW, ow = rem - (rem / p.OW) * p.OW;
+  const T* xb = reinterpret_cast<const T*>(p.x) + (long long)n * p.H * p.W * 4;
+  T v[32];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int ih = oh * p.stride - p.pad + t / 3, iw = ow * p.stride - p.pad + t % 3;
+    float e[4] = {0.f, 0.f, 0.f, 0.f};
+    if ((unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W) load4<T>(xb + ((long long)ih * p.W + iw) * 4, e, 4);
+    v[3 * t] = (T)e[0];
+    v[3 * t + 1] = (T)e[1];
+    v[3 * t + 2] = (T)e[2];
+  }
+#pragma unroll
+  for (int k = 27; k < 32; ++k) v[k] = (T)0.f;
+  T* dst = col + pix * 32;
+  constexpr int VE = 16 / sizeof(T);
+#pragma unroll
+  for (int q = 0; q < 32 / VE; ++q) {
+    if constexpr (sizeof(T) == 2) {
+      f16x8 h;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) h[j] = v[q * 8 + j];
+      *reinterpret_cast<f16x8*>(dst + q * 8) = h;
+    } else {
+      *reinterpret_cast<f32x4*>(dst + q * 4) = f32x4{(float)v[q * 4], (float)v[q * 4 + 1], (float)v[q * 4 + 2],
+                                                     (float)v[q * 4 + 3]};
+    }
+  }
+}
+
 // NHWC max pool (padding = -inf, PyTorch semantics); one thread per pixel x 4 channels.
 template <typename T>
 __global__ void maxpool_nhwc(PoolParams p) {
@@ -471,6 +513,12 @@ hipError_t stem_im2col_launch(int f32, const StemParams& p, int cin_true, void* 
   const long long M = (long long)p.N * p.OH * p.OW;
   dim3 grid((unsigned)((M * 4 + 255) / 256));
   if (p.KH * p.KW * cin_true > 32) return hipErrorInvalidValue;
+  if (p.KH == 3 && p.KW == 3 && cin_true == 3 && p.cin == 4 && p.xcs == 4) {
+    dim3 g3((unsigned)((M + 255) / 256));
+    if (f32) hipLaunchKernelGGL(stem_im2col3<float>, g3, dim3(256), 0, s, p, (float*)col);
+    else hipLaunchKernelGGL(stem_im2col3<f16>, g3, dim3(256), 0, s, p, (f16*)col);
+    return hipGetLastError();
+  }
   if (f32) hipLaunchKernelGGL(stem_im2col<float>, grid, dim3(256), 0, s, p, cin_true, (float*)col);
   else hipLaunchKernelGGL(stem_im2col<f16>, grid, dim3(256), 0, s, p, cin_true, (f16*)col);
   return hipGetLastError();
