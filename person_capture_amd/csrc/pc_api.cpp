@@ -790,7 +790,11 @@ static int run_ops(pc_net* n, int N) {
         q.bias = st.bias; q.bias_mode = BIAS_CHANNEL;
         q.slope = st.slope; q.act = p.act;
         q.kt_total = 1; q.splitk = 1;
-        HIPCHK(c, conv_launch(n->f32, st.rowb, st.cfg, q, s));
+        // the statically scheduled kernel's 64x256 tile when it divides the channels
+        if (st.npad % 64 == 0 && conv_fast_valid(4, st.rowb) && !getenv("PC_STEM_GENERIC"))
+          HIPCHK(c, conv_fast_launch(n->f32, st.rowb, 4, q, s));
+        else
+          HIPCHK(c, conv_launch(n->f32, st.rowb, st.cfg, q, s));
       }
     } else if (w[0] == OP_MAXPOOL) {
       PoolParams p;
