@@ -425,14 +425,17 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl) {
     const char* e = getenv("PC_CONV_FAST");
     const int force = e ? atoi(e) : ((getenv("PC_CONV_CFG") || getenv("PC_CONV_HALO")) ? 0 : -1);
     bool ok = pl.splitk == 1 && force != 0;
+    // odd multiples of 32 channels (96, 160, 224: SCRFD trunks) run faster on the generic
+    // kernel's 96x256 / 32x512 tiles (measured per layer, tools/probe_layers.py scrfd)
+    if (force < 0 && npad > 32 && npad % 64 == 32) ok = false;
     for (int sg = 0; sg < nseg && ok; ++sg) {
       const NetTensor& X = n->tens[w[3 + 5 * sg]];
       if ((double)X.H * X.W * n->max_batch * X.cs * esz + kZeroTail >= 4294967296.0) ok = false;
     }
     if ((double)npad * w[15] * esz >= 4294967296.0) ok = false;
     if (ok) {
-      static const double cost[] = {1.0, 1.12, 1.12, 1.3, 1.3, 1.3, 1.15, 1.45, 1.3, 1.0, 0.9};
-      static const int occ[] = {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2};   // workgroups per CU
+      static const double cost[] = {1.0, 1.12, 1.12, 1.3, 1.3, 1.3, 1.15, 1.45, 1.3, 1.0, 0.9, 1.3, 1.6};
+      static const int occ[] = {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 1, 1};   // workgroups per CU
       int best = -1, best_rowb = rowb;
       double best_t = 0;
       for (int k = 0; k < conv_fast_num_cfgs(); ++k) {

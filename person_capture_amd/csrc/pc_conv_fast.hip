@@ -260,6 +260,8 @@ static const FastCfg kFastCfgs[] = {
     {224, 128, 4},   // 8: 2x2 waves, 112x64 per wave, 2 stages
     {128, 512, 8},   // 9: 2x4 waves, 64x128 per wave, 2 stages (ROWB 64: 4)
     {128, 256, 4},   // 10: 2x2 waves, 64x128 per wave, ROWB 64 only, 3 stages, 2 workgroups per CU
+    {96, 384, 6},    // 11: 1x6 waves, 96x64 per wave (96-channel trunks at 64-byte K rows)
+    {32, 256, 2},    // 12: 1x2 waves, 32x128 per wave (detector heads, npad 32)
 };
 static const int kNumFastCfgs = sizeof(kFastCfgs) / sizeof(kFastCfgs[0]);
 
@@ -300,6 +302,8 @@ static hipError_t launch_fast_t(const ConvParams& p, int cfg, hipStream_t s) {
     case 10:
       if constexpr (ROWB == 64) return launch_fast_cfg<T, 128, 256, 64, 2, 2, 3, 2>(p, s);
       else return hipErrorInvalidValue;
+    case 11: return launch_fast_cfg<T, 96, 384, ROWB, 1, 6, ROWB == 128 ? 2 : 4>(p, s);
+    case 12: return launch_fast_cfg<T, 32, 256, ROWB, 1, 2, ROWB == 128 ? 3 : 4>(p, s);
     default: return hipErrorInvalidValue;
   }
 }
