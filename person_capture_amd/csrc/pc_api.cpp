@@ -434,8 +434,8 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl) {
     }
     if ((double)npad * w[15] * esz >= 4294967296.0) ok = false;
     if (ok) {
-      static const double cost[] = {1.0, 1.12, 1.12, 1.3, 1.3, 1.3, 1.15, 1.45, 1.3, 1.0, 0.9, 1.3, 1.6};
-      static const int occ[] = {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 1, 1};   // workgroups per CU
+      static const double cost[] = {1.0, 1.12, 1.12, 1.3, 1.3, 1.3, 1.15, 1.45, 1.3, 1.0, 0.9, 1.3, 1.6, 1.0};
+      static const int occ[] = {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 1, 1, 1};   // workgroups per CU
       int best = -1, best_rowb = rowb;
       double best_t = 0;
       for (int k = 0; k < conv_fast_num_cfgs(); ++k) {

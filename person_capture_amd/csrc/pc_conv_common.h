@@ -285,7 +285,8 @@ __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, f32x4 (&a
       // these stay within the 256 registers of a 2-waves-per-SIMD kernel)
       using RV = typename std::conditional<ESZ == 2, f16x8, f32x4>::type;
       constexpr int RN = ESZ == 2 ? 1 : 2;
-      constexpr int RG = (NPASS == 2 ? 2 : 4) < IT ? (NPASS == 2 ? 2 : 4) : IT;
+      constexpr int RG0 = (NPASS == 2 ? 2 : 4) < IT ? (NPASS == 2 ? 2 : 4) : IT;
+      constexpr int RG = IT % RG0 == 0 ? RG0 : (IT % 2 == 0 ? 2 : 1);
       static_assert(IT % RG == 0, "residual groups");
 #pragma unroll 1
       for (int kg = 0; kg < IT; kg += RG) {

@@ -43,15 +43,18 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
   constexpr int BKE = ROWB / ESZ;             // K elements per tile
   constexpr int RPI = 1024 / ROWB;            // LDS rows per DMA wave-instruction
   constexpr int NA = BC / RPI, NB = BP / RPI; // DMA instructions per tile (weights, im2col)
-  static_assert(NA % NW == 0 && NB % NW == 0, "every wave must issue the same DMA count");
-  constexpr int NIA = NA / NW, NIB = NB / NW, NI = NIA + NIB;
+  static_assert(NA % NW == 0, "every wave must issue the same weight DMA count");
+  // im2col rows: when NB is not a multiple of the wave count, the last round of DMAs of
+  // the waves past NB goes to a trash area, so every wave still issues NIB (static vmcnt)
+  constexpr int NIA = NA / NW, NIB = (NB + NW - 1) / NW, NI = NIA + NIB;
   constexpr int WTC = BC / WC, WTP = BP / WP;
   constexpr int TC = WTC / 16, TP = WTP / 16;
   constexpr int BUF = (BC + BP) * ROWB;
   constexpr int RING = NSTAGE * BUF;
   constexpr int EPI_MAX = OCC == 1 ? 131072 : 65536;
   constexpr int EPI = fast_epi_bytes<BC, BP, WC, WP, EPI_MAX>();
-  constexpr int SMEM = RING > EPI ? RING : EPI;
+  constexpr int TRASH = NB % NW ? NW * 1024 : 0;
+  constexpr int SMEM = RING + TRASH > EPI ? RING + TRASH : EPI;
   static_assert(SMEM * OCC <= 163840, "LDS");
   static_assert(WTC % 16 == 0 && WTP % 16 == 0, "wave tile");
   static_assert(NSTAGE >= 2, "ring depth");
@@ -126,8 +129,9 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
       const bool ok = (unsigned)(b_ih[i] + ith) < (unsigned)sH && (unsigned)(b_iw[i] + itw) < (unsigned)sW;
       unsigned off = ok ? b_base[i] + tapoff : b_zero;
       asm volatile("" : "+v"(off));
-      __builtin_amdgcn_global_load_lds((gptr_t)(xb + off),
-                                       (lds_ptr_t)(smem + slot * BUF + BC * ROWB + (i * NW + wave) * 1024), 16, 0, 0);
+      const int dst = (NB % NW == 0 || i * NW + wave < NB) ? slot * BUF + BC * ROWB + (i * NW + wave) * 1024
+                                                           : RING + wave * 1024;
+      __builtin_amdgcn_global_load_lds((gptr_t)(xb + off), (lds_ptr_t)(smem + dst), 16, 0, 0);
     });
   };
   // advance the issue iterator by one K-tile (no-op once the last tile was issued)
@@ -241,7 +245,7 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
 // tile shapes whose DMA count divides evenly over the waves at this row width
 template <int BC, int BP, int ROWB, int NW>
 constexpr bool fast_valid() {
-  return (BC / (1024 / ROWB)) % NW == 0 && (BP / (1024 / ROWB)) % NW == 0;
+  return (BC / (1024 / ROWB)) % NW == 0 && BP % (1024 / ROWB) == 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -262,6 +266,7 @@ static const FastCfg kFastCfgs[] = {
     {128, 256, 4},   // 10: 2x2 waves, 64x128 per wave, ROWB 64 only, 3 stages, 2 workgroups per CU
     {96, 384, 6},    // 11: 1x6 waves, 96x64 per wave (96-channel trunks at 64-byte K rows)
     {32, 256, 2},    // 12: 1x2 waves, 32x128 per wave (detector heads, npad 32)
+    {256, 224, 8},   // 13: 4x2 waves, 64x112 per wave: 50176-pixel layers (b256 14x14) fill 224 CUs
 };
 static const int kNumFastCfgs = sizeof(kFastCfgs) / sizeof(kFastCfgs[0]);
 
@@ -304,6 +309,7 @@ static hipError_t launch_fast_t(const ConvParams& p, int cfg, hipStream_t s) {
       else return hipErrorInvalidValue;
     case 11: return launch_fast_cfg<T, 96, 384, ROWB, 1, 6, ROWB == 128 ? 2 : 4>(p, s);
     case 12: return launch_fast_cfg<T, 32, 256, ROWB, 1, 2, ROWB == 128 ? 3 : 4>(p, s);
+    case 13: return launch_fast_cfg<T, 256, 224, ROWB, 4, 2, ROWB == 128 ? 2 : 4>(p, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -314,7 +320,7 @@ int conv_fast_valid(int cfg, int rowb) {
   const FastCfg& c = kFastCfgs[cfg];
   if (cfg == 10 && rowb != 64) return 0;   // sized for 2 workgroups per CU at 64-byte K rows
   const int rpi = 1024 / rowb;
-  return (c.bc / rpi) % c.nw == 0 && (c.bp / rpi) % c.nw == 0;
+  return (c.bc / rpi) % c.nw == 0 && c.bp % rpi == 0;
 }
 
 hipError_t conv_fast_launch(int f32, int rowb, int cfg, const ConvParams& p, hipStream_t s) {
