@@ -194,7 +194,7 @@ def main():
                    "parallelism": f"frame-shard x{world} (no collective)"},
         "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": traffic,
-                     "kernel": "conv_igemm (SCRFD + ArcFace implicit-GEMM convs)",
+                     "kernel": "implicit-GEMM MFMA convs (conv_fast / conv_igemm, SCRFD + ArcFace)",
                      "launches": conv_launches, "avg_launch_us": round(conv_ms * 1e3 / max(1, conv_launches), 2),
                      "flops_per_launch": round(conv_flops / max(1, conv_launches)),
                      "conv_share_of_step": round(conv_ms * 1e-3 / (t1 - t0), 4)},
@@ -316,7 +316,7 @@ def main_other(args):
                    **{k: v for k, v in stats.items()}, "parallelism": f"frame-shard x{world} (no collective)"},
         "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": None,
-                     "kernel": "conv_igemm (all nets' implicit-GEMM convs / 1x1 linears)", "launches": conv_launches,
+                     "kernel": "implicit-GEMM MFMA convs (all nets, ViT linears as 1x1)", "launches": conv_launches,
                      "avg_launch_us": round(conv_ms * 1e3 / max(1, conv_launches), 2),
                      "conv_share_of_step": round(conv_ms * 1e-3 / local_dt, 4)},
         "cpu_baseline": None,
