@@ -146,8 +146,11 @@ def main():
     nfaces = sum(len(r) for r in res)
     accept = sum(1 for r in res for f in r if f["fd"] <= 0.45)
     nets = [fe._engine(640).net, fe._arc.net]
-    for n in nets:
-        n.profile(True)
+    if not os.getenv("PC_BENCH_NOPROF"):
+        for n in nets:
+            n.profile(True)
+    if fe.host_times is not None:
+        fe.host_times.clear()
     _barrier(world)
     ctx.sync()
     t0 = time.perf_counter()
@@ -160,6 +163,9 @@ def main():
     prof = [n.profile_read() for n in nets]
     for n in nets:
         n.profile(False)
+    if fe.host_times is not None:
+        print("host phases ms/step: " + ", ".join(f"{k} {v * 1e3 / args.steps:.2f}" for k, v in fe.host_times.items()),
+              file=sys.stderr)
     conv_ms = sum(p["conv_ms"] for p in prof)
     conv_launches = sum(p["conv_launches"] for p in prof)
     conv_flops = sum(p["conv_flops"] for p in prof)

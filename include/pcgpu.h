@@ -148,6 +148,17 @@ int pc_copy_h2d(pc_ctx* ctx, void* d_dst, const void* h_src, size_t bytes); /* s
 int pc_copy_d2h(pc_ctx* ctx, void* h_dst, const void* d_src, size_t bytes); /* stream-ordered */
 int pc_copy_d2d(pc_ctx* ctx, void* d_dst, const void* d_src, size_t bytes);
 int pc_memset(pc_ctx* ctx, void* d_dst, int value, size_t bytes);
+/* Pinned host memory (page-locked: D2H copies into it stay asynchronous) and stream
+ * fences. A fence is a HIP event recorded on the context stream; pc_fence_wait blocks
+ * the host until everything enqueued before the record has finished. Used to overlap
+ * the host-side detector policy of one chunk of frames with device work of the next
+ * (FaceEmbedder.extract_batch). */
+int pc_host_alloc(pc_ctx* ctx, size_t bytes, void** h_out);
+int pc_host_free(pc_ctx* ctx, void* h_ptr);
+int pc_fence_create(pc_ctx* ctx, void** fence_out);
+int pc_fence_record(pc_ctx* ctx, void* fence);
+int pc_fence_wait(pc_ctx* ctx, void* fence);
+int pc_fence_destroy(pc_ctx* ctx, void* fence);
 
 /* ---- networks (serialized program produced by person_capture_amd.netdef) ---- */
 int pc_net_create(pc_ctx* ctx, const void* h_program, size_t program_bytes, int precision, int max_batch,

@@ -80,6 +80,12 @@ SIGNATURES = {
     "pc_copy_d2h": ([_P, _P, _P, _SZ], _I),
     "pc_copy_d2d": ([_P, _P, _P, _SZ], _I),
     "pc_memset": ([_P, _P, _I, _SZ], _I),
+    "pc_host_alloc": ([_P, _SZ, C.POINTER(_P)], _I),
+    "pc_host_free": ([_P, _P], _I),
+    "pc_fence_create": ([_P, C.POINTER(_P)], _I),
+    "pc_fence_record": ([_P, _P], _I),
+    "pc_fence_wait": ([_P, _P], _I),
+    "pc_fence_destroy": ([_P, _P], _I),
     "pc_net_create": ([_P, _P, _SZ, _I, _I, C.POINTER(_P)], _I),
     "pc_net_destroy": ([_P], _I),
     "pc_net_run": ([_P, _P, _I], _I),

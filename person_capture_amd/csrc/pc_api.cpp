@@ -235,6 +235,40 @@ extern "C" int pc_device_free(pc_ctx* c, void* d) {
   if (d) HIPCHK(c, hipFree(d));
   return PC_OK;
 }
+extern "C" int pc_host_alloc(pc_ctx* c, size_t bytes, void** h) {
+  if (!c || !h) return PC_ERR_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipHostMalloc(h, bytes ? bytes : 16, hipHostMallocDefault));
+  return PC_OK;
+}
+extern "C" int pc_host_free(pc_ctx* c, void* h) {
+  if (!c) return PC_ERR_ARG;
+  if (h) HIPCHK(c, hipHostFree(h));
+  return PC_OK;
+}
+extern "C" int pc_fence_create(pc_ctx* c, void** f) {
+  if (!c || !f) return PC_ERR_ARG;
+  hipEvent_t e = nullptr;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  *f = (void*)e;
+  return PC_OK;
+}
+extern "C" int pc_fence_record(pc_ctx* c, void* f) {
+  if (!c || !f) return PC_ERR_ARG;
+  HIPCHK(c, hipEventRecord((hipEvent_t)f, c->stream));
+  return PC_OK;
+}
+extern "C" int pc_fence_wait(pc_ctx* c, void* f) {
+  if (!c || !f) return PC_ERR_ARG;
+  HIPCHK(c, hipEventSynchronize((hipEvent_t)f));
+  return PC_OK;
+}
+extern "C" int pc_fence_destroy(pc_ctx* c, void* f) {
+  if (!c) return PC_ERR_ARG;
+  if (f) HIPCHK(c, hipEventDestroy((hipEvent_t)f));
+  return PC_OK;
+}
 extern "C" int pc_copy_h2d(pc_ctx* c, void* d, const void* h, size_t n) {
   if (!c) return PC_ERR_ARG;
   if (n) HIPCHK(c, hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, c->stream));

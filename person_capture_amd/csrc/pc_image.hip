@@ -150,12 +150,13 @@ struct WarpDesc {
 __device__ __forceinline__ int border_interp(int p, int len, int border) {
   if ((unsigned)p < (unsigned)len) return p;
   if (len == 1) return 0;
+  // OpenCV's reflect loop in closed form (the pattern has period 2*len for REFLECT and
+  // 2*len-2 for REFLECT_101), so a far-out coordinate costs O(1), not O(|p|/len)
   const int delta = border == 4 ? 1 : 0;
-  do {
-    if (p < 0) p = -p - 1 + delta;
-    else p = len - 1 - (p - len) - delta;
-  } while ((unsigned)p >= (unsigned)len);
-  return p;
+  const long long T = 2LL * len - 2 * delta;
+  long long q = (long long)p % T;
+  if (q < 0) q += T;
+  return (int)(q < len ? q : T - 1 + delta - q);
 }
 
 __device__ __forceinline__ void bilinear_wtab(int fx, int fy, int w[4]) {

@@ -172,6 +172,43 @@ class ScrfdEngine:
             out.append((dets[i, :k].copy(), kps[i, :k].reshape(k, 5, 2).copy()))
         return out
 
+    def detect_async(self, d_frames: Sequence[Tuple[int, int, int, int]], thresh: float, slot: str,
+                     nms_thresh: float = 0.4) -> list:
+        """Enqueue detection of up to max_batch frames and the readback of its results
+        into pinned memory; collect() waits for them. slot names the pinned buffers and
+        fence (one per in-flight call)."""
+        n = len(d_frames)
+        if n > self.max_batch:
+            raise ValueError(f"detect_async: {n} frames exceed max_batch {self.max_batch}")
+        descs, scales = [], []
+        for (ptr, H, W, rs) in d_frames:
+            d, s = make_letterbox_desc(ptr, H, W, rs, self.D)
+            descs.append(d)
+            scales.append(s)
+        dd, dk, dc, dn = self.detect_device(descs, scales, thresh, nms_thresh)
+        md = self.max_det
+        sizes = [n * 4, n * 4, n * md * 5 * 4, n * md * 10 * 4]
+        pin = self.ctx.pinned(f"scrfd{self.D}_{slot}", sum(sizes))
+        off = 0
+        views = []
+        for (buf, shape, dt), sz in zip(((dc, (n,), np.int32), (dn, (n,), np.int32), (dd, (n, md, 5), np.float32),
+                                         (dk, (n, md, 10), np.float32)), sizes):
+            views.append(self.ctx.download_async(buf.ptr, pin, off, shape, dt))
+            off += sz
+        fence = self.ctx.fence(f"scrfd{self.D}_{slot}")
+        return [fence, n] + views
+
+    def collect(self, pending) -> List[Tuple[np.ndarray, np.ndarray]]:
+        fence, n, cnt, ncand, dets, kps = pending
+        fence.wait()
+        if np.any(ncand > 8192):
+            raise RuntimeError("SCRFD candidate capacity (8192 per frame) exceeded; raise det_thresh")
+        out = []
+        for i in range(n):
+            k = min(int(cnt[i]), self.max_det)
+            out.append((dets[i, :k].copy(), kps[i, :k].reshape(k, 5, 2).copy()))
+        return out
+
     def detect_frames(self, d_frames: Sequence[Tuple[int, int, int, int]], thresh: float,
                       nms_thresh: float = 0.4) -> List[Tuple[np.ndarray, np.ndarray]]:
         """d_frames: (device ptr, H, W, row_stride) per frame (BGR u8)."""

@@ -28,8 +28,10 @@ as the reference does for unavailable backends.
 """
 from __future__ import annotations
 
+import ctypes as C
 import math
 import os
+import time
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -143,6 +145,11 @@ class FaceEmbedder:
         self._arc_depth = int(arc_kind[len("iresnet"):])
         self._det_batch = int(os.getenv("PERSON_CAPTURE_AMD_DET_BATCH", "8"))
         self._arc_batch = int(os.getenv("PERSON_CAPTURE_AMD_ARC_BATCH", "256"))
+        # frames per detection chunk of extract_batch: the host policy of chunk c runs
+        # while the device works on chunk c+1 (0 = one chunk, no overlap)
+        self._pipe_chunk = int(os.getenv("PERSON_CAPTURE_AMD_PIPE_CHUNK", "16"))
+        # host phase timers of extract_batch (diagnostics; bench.py prints them)
+        self.host_times: Optional[Dict[str, float]] = {} if os.getenv("PERSON_CAPTURE_AMD_HOST_TIMING") else None
         self._scrfd_engines: Dict[int, ScrfdEngine] = {}
         self._arc = ArcFaceEngine(self._ctx, self._arc_params, self._arc_depth, precision=self.precision,
                                   max_batch=self._arc_batch)
@@ -324,28 +331,77 @@ class FaceEmbedder:
             else:
                 f = frames[i]
                 imgs.append(None if f is None or f.size == 0 else self._upload(f, key=f"frame{i}"))
-        # speculative 0-degree pass for every frame at the det size implied by the current state
+        # speculative 0-degree pass for every frame at the det size implied by the current
+        # state, enqueued chunk by chunk with its readback into pinned memory; the policy of
+        # chunk c (host) then overlaps the device work of the later chunks, and ArcFace
+        # launches as soon as a full batch of faces is known.
+        ht = self.host_times
+        tick = time.perf_counter
+        t_prev = tick()
+
+        def lap(key):
+            nonlocal t_prev
+            if ht is not None:
+                t = tick()
+                ht[key] = ht.get(key, 0.0) + (t - t_prev)
+                t_prev = t
         spec_dyn = [self._dyn_for(im, imgsz) if im is not None else None for im in imgs]
         spec: List[Optional[tuple]] = [None] * n
-        by_dyn: Dict[int, List[int]] = {}
-        for i, d in enumerate(spec_dyn):
-            if d is not None:
-                by_dyn.setdefault(d, []).append(i)
-        for d, idx in by_dyn.items():
-            res = self._detect_batch([imgs[i] for i in idx], d, float(self.conf))
-            for i, r in zip(idx, res):
-                spec[i] = r
-        faces_per_frame: List[list] = []
-        for i in range(n):
-            im = imgs[i]
-            if im is None:
-                faces_per_frame.append([])
-                continue
-            self._frame_idx += 1
-            dyn = self._dyn_for(im, imgsz)
-            first = spec[i] if dyn == spec_dyn[i] else self._detect_once(im, dyn, float(self.conf))
-            faces_per_frame.append(self._scrfd_policy(im, dyn, first))
-        return self._embed_faces(imgs, faces_per_frame)
+        chunk = self._pipe_chunk if self._pipe_chunk > 0 else max(1, n)
+        chunks = [list(range(c0, min(n, c0 + chunk))) for c0 in range(0, n, chunk)]
+        det_pending: List[list] = [[] for _ in chunks]
+        slot = 0
+        for ci, frames_c in enumerate(chunks):
+            by_dyn: Dict[int, List[int]] = {}
+            for i in frames_c:
+                if spec_dyn[i] is not None:
+                    by_dyn.setdefault(spec_dyn[i], []).append(i)
+            for d, idx in by_dyn.items():
+                eng = self._engine(int(d))
+                for s0 in range(0, len(idx), eng.max_batch):
+                    sub = idx[s0:s0 + eng.max_batch]
+                    pend = eng.detect_async([(imgs[i].ptr, imgs[i].H, imgs[i].W, imgs[i].stride) for i in sub],
+                                            float(self.conf), slot=str(slot))
+                    det_pending[ci].append((sub, eng, pend))
+                    slot += 1
+        lap("det_launch")
+        faces_per_frame: List[list] = [[] for _ in range(n)]
+        jobs: List[tuple] = []       # (frame index, (xi1, yi1, xi2, yi2), kps) not yet launched
+        emb_pending: List[tuple] = []
+        for ci, frames_c in enumerate(chunks):
+            lap("host_other")
+            for sub, eng, pend in det_pending[ci]:
+                for i, r in zip(sub, eng.collect(pend)):
+                    spec[i] = r
+            lap("det_wait")
+            for i in frames_c:
+                im = imgs[i]
+                if im is None:
+                    continue
+                self._frame_idx += 1
+                dyn = self._dyn_for(im, imgsz)
+                first = spec[i] if dyn == spec_dyn[i] else self._detect_once(im, dyn, float(self.conf))
+                kept = self._scrfd_policy(im, dyn, first)
+                faces_per_frame[i] = kept
+                jobs.extend(self._face_jobs(im, i, kept))
+            lap("policy")
+            per = self._embed_per()
+            while len(jobs) >= per:
+                emb_pending.append(self._embed_launch(imgs, jobs[:per], len(emb_pending)))
+                jobs = jobs[per:]
+            lap("embed_launch")
+        if jobs:
+            emb_pending.append(self._embed_launch(imgs, jobs, len(emb_pending)))
+        lap("embed_launch")
+        out: List[list] = [[] for _ in range(n)]
+        for pend in emb_pending:
+            self._embed_collect(pend, out)
+        self._ctx.sync()
+        lap("embed_wait_collect")
+        for lst in out:
+            lst.sort(key=lambda f: (f['quality'], (f['bbox'][2] - f['bbox'][0]) * (f['bbox'][3] - f['bbox'][1])),
+                     reverse=True)
+        return out
 
     # ------------------------------------------------------------------ detector policy
     def _dyn_for(self, im: _DevImage, imgsz: Optional[int]) -> int:
@@ -372,6 +428,25 @@ class FaceEmbedder:
         if deg == 270:
             return W0 - 1 - yr, xr
         return xr, yr
+
+    @staticmethod
+    def _accumulate0(bb: np.ndarray, kp: np.ndarray, W0: int, H0: int) -> List[tuple]:
+        """The 0-degree _accumulate (face_embedder.py:2214-2239) of _scrfd_policy over all boxes of one SCRFD result
+        at once (same truncation, clamping, size gate and crop-local f32 landmarks)."""
+        if len(bb) == 0:
+            return []
+        xy = bb[:, :4].astype(np.int64)              # int(v): truncation toward zero
+        xa1 = np.clip(np.minimum(xy[:, 0], xy[:, 2]), 0, W0 - 1)
+        ya1 = np.clip(np.minimum(xy[:, 1], xy[:, 3]), 0, H0 - 1)
+        xa2 = np.maximum(xa1 + 1, np.minimum(W0, np.maximum(xy[:, 0], xy[:, 2])))
+        ya2 = np.maximum(ya1 + 1, np.minimum(H0, np.maximum(xy[:, 1], xy[:, 3])))
+        keep = np.nonzero((xa2 - xa1 > 2) & (ya2 - ya1 > 2))[0]
+        if keep.size == 0:
+            return []
+        off = np.stack([xa1, ya1], axis=1).astype(np.float64)[:, None, :]
+        pts = (kp.astype(np.float64) - off).astype(np.float32)
+        sc = bb[:, 4].astype(np.float64)
+        return [((int(xa1[i]), int(ya1[i]), int(xa2[i]), int(ya2[i])), pts[i], float(sc[i])) for i in keep]
 
     def _scrfd_policy(self, im: _DevImage, dyn: int, first) -> List[tuple]:
         """face_embedder.py:2205-2443: from the 0-degree result through fallbacks to the
@@ -405,8 +480,12 @@ class FaceEmbedder:
             dets.append(((xa1, ya1, xa2, ya2), pts, score))
 
         bboxes, kpss = first
-        for i, bb in enumerate(bboxes):
-            accumulate(bb, None if kpss is None or i >= len(kpss) else kpss[i], 0)
+        if kpss is not None and len(kpss) == len(bboxes) and np.ndim(kpss) == 3 and np.shape(kpss)[1:] == (5, 2) \
+                and np.ndim(bboxes) == 2 and np.shape(bboxes)[1] >= 5:
+            dets.extend(self._accumulate0(np.asarray(bboxes), np.asarray(kpss, np.float32), W0, H0))
+        else:
+            for i, bb in enumerate(bboxes):
+                accumulate(bb, None if kpss is None or i >= len(kpss) else kpss[i], 0)
 
         tta_scales = ()
         if not dets and not self._fast_prescan:
@@ -549,52 +628,71 @@ class FaceEmbedder:
         return kept
 
     # ------------------------------------------------------------------ align + embed
-    def _embed_faces(self, imgs: Sequence[Optional[_DevImage]], faces_per_frame: List[list]) -> List[list]:
-        """face_embedder.py:2445-2482 for every kept face of every frame: crop, canonical
-        5-point align (or eye-roll / resize fallback), quality, ArcFace with flip-TTA."""
-        jobs = []   # (frame index, (xi1, yi1, xi2, yi2), kps)
-        for fi, kept in enumerate(faces_per_frame):
-            im = imgs[fi]
-            if im is None:
-                continue
-            H0, W0 = im.H, im.W
-            for (x1, y1, x2, y2), kps, _sc in kept:
-                xi1 = max(0, min(W0 - 1, int(round(x1))))
-                yi1 = max(0, min(H0 - 1, int(round(y1))))
-                xi2 = max(xi1 + 1, min(W0, int(round(x2))))
-                yi2 = max(yi1 + 1, min(H0, int(round(y2))))
-                jobs.append((fi, (xi1, yi1, xi2, yi2), kps))
-        out: List[list] = [[] for _ in faces_per_frame]
+    @staticmethod
+    def _face_jobs(im: _DevImage, fi: int, kept: list) -> List[tuple]:
+        """Integer crop boxes of the kept detections (face_embedder.py:2445-2452)."""
+        H0, W0 = im.H, im.W
+        out = []
+        for (x1, y1, x2, y2), kps, _sc in kept:
+            xi1 = max(0, min(W0 - 1, int(round(x1))))
+            yi1 = max(0, min(H0 - 1, int(round(y1))))
+            xi2 = max(xi1 + 1, min(W0, int(round(x2))))
+            yi2 = max(yi1 + 1, min(H0, int(round(y2))))
+            out.append((fi, (xi1, yi1, xi2, yi2), kps))
+        return out
+
+    def _do_flip(self) -> bool:
+        return (not getattr(self, "_fast_prescan", False)) or getattr(self, "_prescan_escalate", False)
+
+    def _embed_per(self) -> int:
+        return self._arc.max_batch // 2 if self._do_flip() else self._arc.max_batch
+
+    def _embed_launch(self, imgs: Sequence[Optional[_DevImage]], jobs: List[tuple], slot: int) -> tuple:
+        """Enqueue crop + align/resize + quality + ArcFace (+ bank match) of at most one
+        ArcFace batch of faces, and the readback into pinned memory."""
         m = len(jobs)
-        if m == 0:
-            return out
         chips = self._ctx.scratch("chips", m * _ARC_SIDE * _ARC_SIDE * 3)
         chip_sz = _ARC_SIDE * _ARC_SIDE * 3
-        canon = [imageops.canon_5pts(k) if k is not None else None for (_, _, k) in jobs]
-        aligned_idx = [j for j in range(m) if canon[j] is not None]
+        has_k = [j for j in range(m) if jobs[j][2] is not None]
+        valid = np.zeros((m,), bool)
+        descs = []
         warps: List[WarpDesc] = []
         resize_jobs = []
-        if aligned_idx:
-            M, ok = imageops.align_matrices(np.stack([canon[j] for j in aligned_idx]).astype(np.float32))
-            for t, j in enumerate(aligned_idx):
-                fi, (xi1, yi1, xi2, yi2), _ = jobs[j]
-                im = imgs[fi]
-                src = im.ptr + yi1 * im.stride + xi1 * 3
-                if ok[t]:
-                    warps.append(imageops.warp_desc(src, im.stride, xi2 - xi1, yi2 - yi1, M[t].reshape(-1),
-                                                    chips.ptr + j * chip_sz))
-                else:
-                    resize_jobs.append(j)
+        if has_k:
+            cs, okc = imageops.canon_5pts_batch(np.stack([np.asarray(jobs[j][2], np.float32).reshape(5, 2)
+                                                          if np.asarray(jobs[j][2]).shape == (5, 2)
+                                                          else np.full((5, 2), np.nan, np.float32) for j in has_k]))
+            aligned_idx = [j for j, o in zip(has_k, okc) if o]
+            valid[aligned_idx] = True
+            if aligned_idx:
+                M, ok = imageops.align_matrices(cs[okc])
+                sel = np.asarray(aligned_idx)[ok]
+                if sel.size:
+                    geo = np.array([(imgs[jobs[j][0]].ptr + jobs[j][1][1] * imgs[jobs[j][0]].stride + jobs[j][1][0] * 3,
+                                     imgs[jobs[j][0]].stride, jobs[j][1][2] - jobs[j][1][0],
+                                     jobs[j][1][3] - jobs[j][1][1]) for j in sel], dtype=np.int64).reshape(-1, 4)
+                    descs.append(imageops.warp_descs(geo[:, 0], geo[:, 1], geo[:, 2], geo[:, 3], M[ok],
+                                                     chips.ptr + sel.astype(np.int64) * chip_sz))
+                resize_jobs.extend(int(j) for j in np.asarray(aligned_idx)[~ok])
         for j in range(m):
-            if canon[j] is None:
+            if not valid[j]:
                 fi, box, kps = jobs[j]
                 if kps is not None:
                     self._upright_by_eye_roll(imgs[fi], box, kps, chips.ptr + j * chip_sz, warps, resize_jobs, j)
                 else:
                     resize_jobs.append(j)
         if warps:
-            arr = (WarpDesc * len(warps))(*warps)
-            check(self._ctx.lib.pc_warp_affine(self._ctx.handle, arr, len(warps)), self._ctx.handle, "warp_affine")
+            descs.append(np.frombuffer(b"".join(bytes(w) for w in warps), imageops.WARP_DESC_DTYPE))
+        if descs:
+            # (np.concatenate would canonicalise the padded record dtype: fill one array)
+            arr = np.zeros(sum(len(d) for d in descs), imageops.WARP_DESC_DTYPE)
+            o = 0
+            for d in descs:
+                arr[o:o + len(d)] = d
+                o += len(d)
+            assert arr.dtype.itemsize == 96
+            check(self._ctx.lib.pc_warp_affine(self._ctx.handle, arr.ctypes.data_as(C.POINTER(WarpDesc)), len(arr)),
+                  self._ctx.handle, "warp_affine")
         for j in resize_jobs:
             fi, (xi1, yi1, xi2, yi2), _ = jobs[j]
             im = imgs[fi]
@@ -603,34 +701,42 @@ class FaceEmbedder:
         qbuf = self._ctx.scratch("quality", m * 8)
         check(self._ctx.lib.pc_face_quality(self._ctx.handle, chips.ptr, m, _ARC_SIDE, qbuf.ptr), self._ctx.handle,
               "face_quality")
-        do_flip = (not getattr(self, "_fast_prescan", False)) or getattr(self, "_prescan_escalate", False)
+        do_flip = self._do_flip()
         fbuf = self._ctx.scratch("feats", m * self._arc_feat_dim * 4)
-        per = self._arc.max_batch // 2 if do_flip else self._arc.max_batch
-        for s in range(0, m, per):
-            k = min(per, m - s)
-            self._arc.embed_device(chips.ptr + s * chip_sz, k, do_flip, fbuf.ptr + s * self._arc_feat_dim * 4)
+        if (2 * m if do_flip else m) > self._arc.max_batch:
+            raise ValueError("embed launch larger than one ArcFace batch")
+        self._arc.embed_device(chips.ptr, m, do_flip, fbuf.ptr)
         bank = getattr(self, "_bank", None)
+        dbg = bool(getattr(self, "debug_chips", False))
+        fd_bytes = m * 4 if bank is not None else 0
+        sizes = [m * 8, m * self._arc_feat_dim * 4, fd_bytes, m * chip_sz if dbg else 0]
+        pin = self._ctx.pinned(f"emb{slot}", sum(sizes))
+        q = self._ctx.download_async(qbuf.ptr, pin, 0, (m,), np.float64)
+        feats = self._ctx.download_async(fbuf.ptr, pin, sizes[0], (m, self._arc_feat_dim), np.float32)
         fd = None
         if bank is not None:
             dfd = self._ctx.scratch("fd", m * 4)
             didx = self._ctx.scratch("fd_idx", m * 4)
             bank.match_device(fbuf.ptr, m, dfd.ptr, didx.ptr)
-            fd = self._ctx.download(dfd.ptr, (m,), np.float32)
-        q = self._ctx.download(qbuf.ptr, (m,), np.float64)
-        feats = self._ctx.download(fbuf.ptr, (m, self._arc_feat_dim), np.float32)
-        for j, (fi, (x1, y1, x2, y2), _) in enumerate(jobs):
+            fd = self._ctx.download_async(dfd.ptr, pin, sizes[0] + sizes[1], (m,), np.float32)
+        chip_h = None
+        if dbg:
+            chip_h = self._ctx.download_async(chips.ptr, pin, sizes[0] + sizes[1] + sizes[2],
+                                              (m, _ARC_SIDE, _ARC_SIDE, 3), np.uint8)
+        return self._ctx.fence(f"emb{slot}"), jobs, q, feats, fd, chip_h
+
+    def _embed_collect(self, pend: tuple, out: List[list]) -> None:
+        fence, jobs, q, feats, fd, chip_h = pend
+        fence.wait()
+        for j, (fi, (x1, y1, x2, y2), kps) in enumerate(jobs):
             face = {'bbox': np.array([x1, y1, x2, y2], dtype=np.int32), 'feat': feats[j].copy(),
                     'quality': float(q[j])}
             if fd is not None:
                 face['fd'] = float(fd[j])
-            if getattr(self, "debug_chips", False):   # parity tests: the aligned chip and its landmarks
-                face['chip'] = self._ctx.download(chips.ptr + j * chip_sz, (_ARC_SIDE, _ARC_SIDE, 3), np.uint8)
-                face['kps5'] = None if jobs[j][2] is None else np.asarray(jobs[j][2], np.float32).copy()
+            if chip_h is not None:   # parity tests: the aligned chip and its landmarks
+                face['chip'] = chip_h[j].copy()
+                face['kps5'] = None if kps is None else np.asarray(kps, np.float32).copy()
             out[fi].append(face)
-        for lst in out:
-            lst.sort(key=lambda f: (f['quality'], (f['bbox'][2] - f['bbox'][0]) * (f['bbox'][3] - f['bbox'][1])),
-                     reverse=True)
-        return out
 
     def _resize_chip(self, crop: _DevImage, d_dst: int) -> None:
         """cv2.resize(face, (112,112), INTER_AREA if max(h,w) > 112 else INTER_LINEAR) (:2458-2460)."""

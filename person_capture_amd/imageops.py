@@ -80,6 +80,61 @@ def canon_5pts(pts) -> Optional[np.ndarray]:
     return np.stack([le, ri, nose, lm, rm], axis=0)
 
 
+def canon_5pts_batch(pts: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+    """canon_5pts over a stack [m][5][2] -> (ordered [m][5][2] float32, valid [m]).
+    Stable sorts on 5 keys equal numpy's default (insertion sort below 16 elements),
+    so every valid row is exactly canon_5pts of that row."""
+    a = np.asarray(pts, dtype=np.float32).reshape(-1, 5, 2)
+    m = a.shape[0]
+    if m == 0:
+        return a.copy(), np.zeros((0,), bool)
+    finite = np.isfinite(a).all(axis=(1, 2))
+    a = np.where(finite[:, None, None], a, np.float32(0))
+    r = np.arange(m)[:, None]
+    by_y = np.argsort(a[:, :, 1], axis=1, kind="stable")
+    s = a[r, by_y]                                   # rows sorted by y
+    eyes, nose, mouth = s[:, :2], s[:, 2], s[:, 3:]
+    eyes = eyes[r, np.argsort(eyes[:, :, 0], axis=1, kind="stable")]
+    mouth = mouth[r, np.argsort(mouth[:, :, 0], axis=1, kind="stable")]
+    le, ri, lm, rm = eyes[:, 0], eyes[:, 1], mouth[:, 0], mouth[:, 1]
+    ok = finite & (le[:, 0] < ri[:, 0]) & (lm[:, 0] < rm[:, 0])
+    ok &= (np.maximum(le[:, 1], ri[:, 1]) < nose[:, 1]) & (nose[:, 1] < np.minimum(lm[:, 1], rm[:, 1]))
+    return np.stack([le, ri, nose, lm, rm], axis=1), ok
+
+
+# pc_warp_desc (include/pcgpu.h) as a numpy record, for building descriptor arrays in bulk
+WARP_DESC_DTYPE = np.dtype({"names": ["d_src", "row_stride", "w", "h", "M", "d_dst", "out_w", "out_h", "border"],
+                            "formats": [np.uint64, np.int32, np.int32, np.int32, (np.float64, 6), np.uint64,
+                                        np.int32, np.int32, np.int32],
+                            "offsets": [0, 8, 12, 16, 24, 72, 80, 84, 88], "itemsize": 96})
+
+
+def invert_affine_batch(M: np.ndarray) -> np.ndarray:
+    """pc_invert_affine (cv2.invertAffineTransform) over [n][6], same operation order."""
+    M = np.asarray(M, np.float64).reshape(-1, 6)
+    D = M[:, 0] * M[:, 4] - M[:, 1] * M[:, 3]
+    nz = D != 0
+    D = np.where(nz, 1.0 / np.where(nz, D, 1.0), 0.0)
+    A11, A22, A12, A21 = M[:, 4] * D, M[:, 0] * D, -M[:, 1] * D, -M[:, 3] * D
+    out = np.empty_like(M)
+    out[:, 0], out[:, 1], out[:, 2] = A11, A12, -A11 * M[:, 2] - A12 * M[:, 5]
+    out[:, 3], out[:, 4], out[:, 5] = A21, A22, -A21 * M[:, 2] - A22 * M[:, 5]
+    return out
+
+
+def warp_descs(d_src, row_stride, w, h, M_fwd, d_dst, out_w: int = 112, out_h: int = 112,
+               border: int = BORDER_REFLECT) -> np.ndarray:
+    """warp_desc over arrays (one descriptor per row of M_fwd [n][6])."""
+    M_fwd = np.asarray(M_fwd, np.float64).reshape(-1, 6)
+    d = np.zeros(M_fwd.shape[0], WARP_DESC_DTYPE)
+    d["d_src"] = np.asarray(d_src, np.uint64)
+    d["row_stride"], d["w"], d["h"] = row_stride, w, h
+    d["M"] = invert_affine_batch(M_fwd)
+    d["d_dst"] = np.asarray(d_dst, np.uint64)
+    d["out_w"], d["out_h"], d["border"] = out_w, out_h, border
+    return d
+
+
 def estimate_affine_partial(src_sets: np.ndarray, dst: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
     """Batched cv2.estimateAffinePartial2D(src, dst, method=LMEDS) (native).
     src_sets [n][k][2] float32, dst [k][2] -> (M [n][2][3] float64, ok [n] bool)."""

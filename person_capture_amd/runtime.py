@@ -34,6 +34,60 @@ class DeviceBuffer:
             pass
 
 
+class PinnedBuffer:
+    """Page-locked host memory (hipHostMalloc) viewed as a flat uint8 numpy array."""
+
+    def __init__(self, ctx: "GpuContext", nbytes: int):
+        self.ctx = ctx
+        self.nbytes = int(nbytes)
+        p = C.c_void_p()
+        check(ctx.lib.pc_host_alloc(ctx.handle, max(self.nbytes, 16), C.byref(p)), ctx.handle, "host_alloc")
+        self.ptr = int(p.value)
+        self.array = np.ctypeslib.as_array((C.c_uint8 * self.nbytes).from_address(self.ptr))
+
+    def view(self, shape, dtype, offset: int = 0) -> np.ndarray:
+        n = int(np.prod(shape)) * np.dtype(dtype).itemsize
+        if offset + n > self.nbytes:
+            raise ValueError("pinned view out of range")
+        return self.array[offset:offset + n].view(dtype).reshape(shape)
+
+    def free(self) -> None:
+        if self.ptr and self.ctx.handle:
+            self.array = None
+            self.ctx.lib.pc_host_free(self.ctx.handle, C.c_void_p(self.ptr))
+        self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Fence:
+    """A HIP event recorded on the context stream (host waits for the work before it)."""
+
+    def __init__(self, ctx: "GpuContext"):
+        self.ctx = ctx
+        h = C.c_void_p()
+        check(ctx.lib.pc_fence_create(ctx.handle, C.byref(h)), ctx.handle, "fence_create")
+        self.handle = h
+
+    def record(self) -> "Fence":
+        check(self.ctx.lib.pc_fence_record(self.ctx.handle, self.handle), self.ctx.handle, "fence_record")
+        return self
+
+    def wait(self) -> None:
+        check(self.ctx.lib.pc_fence_wait(self.ctx.handle, self.handle), self.ctx.handle, "fence_wait")
+
+    def __del__(self):
+        try:
+            if self.handle and self.ctx.handle:
+                self.ctx.lib.pc_fence_destroy(self.ctx.handle, self.handle)
+        except Exception:
+            pass
+
+
 class GpuContext:
     """One context per (GPU, consumer): stream, zero page, staging ring."""
 
@@ -47,10 +101,14 @@ class GpuContext:
         self.handle = h
         self._keep = []   # host arrays referenced by in-flight async copies
         self._bufs: Dict[str, DeviceBuffer] = {}
+        self._pinned: Dict[str, PinnedBuffer] = {}
+        self._fences: Dict[str, Fence] = {}
 
     def close(self) -> None:
         if self.handle:
             self._bufs.clear()
+            self._pinned.clear()
+            self._fences.clear()
             self.lib.pc_ctx_destroy(self.handle)
             self.handle = None
 
@@ -73,6 +131,33 @@ class GpuContext:
             b = DeviceBuffer(self, max(int(nbytes), 256))
             self._bufs[key] = b
         return b
+
+    def pinned(self, key: str, nbytes: int) -> PinnedBuffer:
+        """A named, growable pinned host buffer. The caller owns the ordering: a buffer
+        may only be reused once the fence covering its last copy has been waited on."""
+        b = self._pinned.get(key)
+        if b is None or b.nbytes < nbytes:
+            if b is not None:
+                self.sync()
+            b = PinnedBuffer(self, max(int(nbytes), 4096))
+            self._pinned[key] = b
+        return b
+
+    def fence(self, key: str) -> Fence:
+        """Record (and return) the named fence on the context stream."""
+        f = self._fences.get(key)
+        if f is None:
+            f = self._fences[key] = Fence(self)
+        return f.record()
+
+    def download_async(self, ptr: int, pin: PinnedBuffer, offset: int, shape, dtype) -> np.ndarray:
+        """Stream-ordered D2H into pinned memory; the returned view is valid after a
+        later fence on this context has been waited on."""
+        out = pin.view(shape, dtype, offset)
+        if out.nbytes:
+            check(self.lib.pc_copy_d2h(self.handle, C.c_void_p(pin.ptr + offset), C.c_void_p(int(ptr)), out.nbytes),
+                  self.handle, "d2h")
+        return out
 
     def upload(self, arr: np.ndarray, dst: Optional[DeviceBuffer] = None, offset: int = 0) -> DeviceBuffer:
         a = np.ascontiguousarray(arr)
