@@ -723,10 +723,19 @@ static int run_ops(pc_net* n, int N) {
   const bool prof = n->prof && !n->use_graph;
   if (n->in_copy)
     HIPCHK(c, hipMemcpyAsync(n->in_copy, n->cur_input, n->in_img_bytes * N, hipMemcpyDeviceToDevice, s));
+  // one event per op boundary: an op's end event is the next op's start event
+  int open_ev = -1;
   for (size_t i = 0; i < n->ops.size(); ++i) {
     const int* w = n->ops[i].w;
     ProfRec rec{-1, -1, w[0], w[0] == OP_CONV ? n->plans[i].flops_per_image * N : 0.0, (int)i};
-    if (prof) { int rc = prof_event(n, &rec.a); if (rc) return rc; }
+    if (prof) {
+      if (open_ev >= 0) {
+        rec.a = open_ev;
+      } else {
+        int rc = prof_event(n, &rec.a);
+        if (rc) return rc;
+      }
+    }
     if (w[0] == OP_CONV) {
       const ConvPlan& pl = n->plans[i];
       ConvParams p;
@@ -807,9 +816,8 @@ static int run_ops(pc_net* n, int N) {
           int rc = prof_event(n, &rec.b);
           if (rc) return rc;
           n->recs.push_back(rec);
-          rec = ProfRec{-1, -1, OP_CONV, n->plans[i].flops_per_image * N, (int)i};
-          rc = prof_event(n, &rec.a);
-          if (rc) return rc;
+          const int b = rec.b;
+          rec = ProfRec{b, -1, OP_CONV, n->plans[i].flops_per_image * N, (int)i};
         }
         ConvParams q;
         memset(&q, 0, sizeof(q));
@@ -875,6 +883,7 @@ static int run_ops(pc_net* n, int N) {
       int rc = prof_event(n, &rec.b);
       if (rc) return rc;
       n->recs.push_back(rec);
+      open_ev = rec.b;
     }
   }
   return PC_OK;

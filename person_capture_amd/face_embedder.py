@@ -148,6 +148,7 @@ class FaceEmbedder:
         # frames per detection chunk of extract_batch: the host policy of chunk c runs
         # while the device works on chunk c+1 (0 = one chunk, no overlap)
         self._pipe_chunk = int(os.getenv("PERSON_CAPTURE_AMD_PIPE_CHUNK", "16"))
+        self._pipe_ahead = int(os.getenv("PERSON_CAPTURE_AMD_PIPE_AHEAD", "2"))
         # host phase timers of extract_batch (diagnostics; bench.py prints them)
         self.host_times: Optional[Dict[str, float]] = {} if os.getenv("PERSON_CAPTURE_AMD_HOST_TIMING") else None
         self._scrfd_engines: Dict[int, ScrfdEngine] = {}
@@ -351,9 +352,13 @@ class FaceEmbedder:
         chunks = [list(range(c0, min(n, c0 + chunk))) for c0 in range(0, n, chunk)]
         det_pending: List[list] = [[] for _ in chunks]
         slot = 0
-        for ci, frames_c in enumerate(chunks):
+
+        def launch_det(ci: int) -> None:
+            nonlocal slot
+            if ci >= len(chunks):
+                return
             by_dyn: Dict[int, List[int]] = {}
-            for i in frames_c:
+            for i in chunks[ci]:
                 if spec_dyn[i] is not None:
                     by_dyn.setdefault(spec_dyn[i], []).append(i)
             for d, idx in by_dyn.items():
@@ -364,6 +369,11 @@ class FaceEmbedder:
                                             float(self.conf), slot=str(slot))
                     det_pending[ci].append((sub, eng, pend))
                     slot += 1
+        # keep `ahead` detection chunks queued in front of the host so ArcFace batches
+        # enqueued by the policy interleave with the remaining detection work
+        ahead = max(1, self._pipe_ahead)
+        for ci in range(ahead):
+            launch_det(ci)
         lap("det_launch")
         faces_per_frame: List[list] = [[] for _ in range(n)]
         jobs: List[tuple] = []       # (frame index, (xi1, yi1, xi2, yi2), kps) not yet launched
@@ -374,6 +384,8 @@ class FaceEmbedder:
                 for i, r in zip(sub, eng.collect(pend)):
                     spec[i] = r
             lap("det_wait")
+            launch_det(ci + ahead)
+            lap("det_launch")
             for i in frames_c:
                 im = imgs[i]
                 if im is None:
