@@ -147,7 +147,7 @@ class FaceEmbedder:
         self._arc_batch = int(os.getenv("PERSON_CAPTURE_AMD_ARC_BATCH", "256"))
         # frames per detection chunk of extract_batch: the host policy of chunk c runs
         # while the device works on chunk c+1 (0 = one chunk, no overlap)
-        self._pipe_chunk = int(os.getenv("PERSON_CAPTURE_AMD_PIPE_CHUNK", "16"))
+        self._pipe_chunk = int(os.getenv("PERSON_CAPTURE_AMD_PIPE_CHUNK", "32"))
         self._pipe_ahead = int(os.getenv("PERSON_CAPTURE_AMD_PIPE_AHEAD", "2"))
         # host phase timers of extract_batch (diagnostics; bench.py prints them)
         self.host_times: Optional[Dict[str, float]] = {} if os.getenv("PERSON_CAPTURE_AMD_HOST_TIMING") else None
