@@ -43,6 +43,11 @@ def _dist_init():
     return world, rank, local
 
 
+def _device(local: int) -> int:
+    from person_capture_amd.shard import device_for_rank
+    return device_for_rank(local)
+
+
 def _barrier(world):
     if world > 1:
         import torch.distributed as dist
@@ -115,11 +120,21 @@ def main():
                     help="c3: BASELINE configs[2] (the metric's config, default); c4: full path with YOLOv8n "
                          "persons + per-crop SCRFD/ArcFace + CLIP ReID; c5: 4K pre-scan (INTER_AREA 416 wide, "
                          "SCRFD @384, 1 ArcFace forward, 1024-entry bank)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: exercise the rank launcher, dist init and the timing/reduction protocol only")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # --gpus N without torch.distributed.run: start N fresh rank processes (this process has not
+        # touched the GPU) and exit with their status
+        from person_capture_amd.shard import spawn_local_ranks
+        sys.exit(spawn_local_ranks([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], args.gpus))
+    if args.dry_run:
+        return main_dry(args)
     if args.workload != "c3":
         return main_other(args)
 
     world, rank, local = _dist_init()
+    local = _device(local)
     os.environ.setdefault("PERSON_CAPTURE_AMD_PRECISION", args.precision)
     os.environ.setdefault("PERSON_CAPTURE_AMD_DET_BATCH", str(args.batch))
     os.environ.setdefault("PERSON_CAPTURE_AMD_ARC_BATCH", "512")
@@ -227,9 +242,35 @@ def _timed(world, ctx, steps, step):
     return _max_over_ranks(world, t1 - t0), t1 - t0
 
 
+def main_dry(args):
+    """The multi-rank protocol without a GPU (CPU test of the launcher): every rank
+    'processes' its contiguous share of a batch with a host stand-in, then the same
+    barrier / max-over-ranks time / sum-over-ranks frames reduction as the real run."""
+    from person_capture_amd.shard import shard_indices
+    world, rank, local = _dist_init()
+    total = args.batch * max(1, world)
+    mine = shard_indices(total, rank, world)
+    _barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        sum(i * i for i in mine)
+    t1 = time.perf_counter()
+    _barrier(world)
+    elapsed = max(_max_over_ranks(world, t1 - t0), 1e-9)
+    frames = _sum_over_ranks(world, len(mine) * args.steps)
+    if rank == 0:
+        print(json.dumps({"metric": "dry-run", "value": frames / elapsed, "unit": "frames/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup, "frames": frames, "local_rank": local}),
+              flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
 def main_other(args):
     """C4 (full path) and C5 (4K pre-scan): secondary workloads, same JSON contract."""
     world, rank, local = _dist_init()
+    local = _device(local)
     os.environ.setdefault("PERSON_CAPTURE_AMD_PRECISION", args.precision)
     os.environ.setdefault("PERSON_CAPTURE_AMD_DET_BATCH", str(args.batch))
     os.environ.setdefault("PERSON_CAPTURE_AMD_ARC_BATCH", "512")

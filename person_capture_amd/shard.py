@@ -1,13 +1,19 @@
-"""Frame-shard runner: one process per GPU, frames dealt round-robin by index, no
-device collective (SURVEY.md §8e — detect/align/embed/match has no cross-frame
-reduction). Results come back to rank 0 in frame order over a host (gloo) gather.
+"""Frame-shard runner: one process per GPU, each rank takes one contiguous run of
+frames, no device collective (SURVEY.md §8e — detect/align/embed/match has no
+cross-frame reduction). Results come back to rank 0 in frame order over a host
+(gloo) gather.
 
-Launch with `python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ...`;
-each rank binds `cuda:LOCAL_RANK` and builds its own FaceEmbedder (context, stream,
-weights). Sequential policy state of the reference (the adaptive rotation gate's
-no-face streak, pre-scan bank growth, lock-ROI) is per instance: callers that need
-single-stream semantics replay match.stream_ref_bank_update / span hysteresis on
-rank 0 over the gathered, frame-ordered results.
+Contiguous runs (not round-robin) so that the per-instance sequential state of the
+reference's FaceEmbedder — the no-face streak that shrinks the det size
+(face_embedder.py:2190-2204), the adaptive rotation gate over _frame_idx /
+_last_face_idx (:2330-2347) — sees the same consecutive frames inside a run as a
+single stream does; only the first frames of each run start from a fresh state.
+
+Launch with `python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ...`
+(or `bench.py --gpus N`, which spawns the ranks itself); each rank binds
+`cuda:LOCAL_RANK` and builds its own FaceEmbedder (context, stream, weights).
+Sequential caller policy (pre-scan bank growth, lock-ROI) is replayed on rank 0 over
+the gathered, frame-ordered results (match.stream_ref_bank_update is host code).
 """
 from __future__ import annotations
 
@@ -15,17 +21,22 @@ import os
 from typing import Callable, List, Optional, Sequence
 
 
+def shard_bounds(n: int, rank: int, world: int) -> range:
+    """Rank r gets frames [r*n//world, (r+1)*n//world): contiguous, sizes differ by <= 1."""
+    return range(rank * n // world, (rank + 1) * n // world)
+
+
 def shard_indices(n: int, rank: int, world: int) -> List[int]:
-    """Frame i goes to rank i mod world."""
-    return list(range(rank, n, world))
+    return list(shard_bounds(n, rank, world))
 
 
 def merge_in_order(n: int, world: int, per_rank: Sequence[Sequence]) -> list:
-    """Inverse of shard_indices: per_rank[r][k] is the result of frame r + k*world."""
-    out = [None] * n
+    """Inverse of shard_indices: rank results concatenated in rank order."""
+    out: list = []
     for r, res in enumerate(per_rank):
-        for k, v in enumerate(res):
-            out[r + k * world] = v
+        if len(res) != len(shard_bounds(n, r, world)):
+            raise ValueError(f"rank {r} returned {len(res)} results for {len(shard_bounds(n, r, world))} frames")
+        out.extend(res)
     return out
 
 
@@ -51,6 +62,40 @@ class FrameShardRunner:
         if self.rank != 0:
             return None
         return merge_in_order(n, self.world, gathered)
+
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_local_ranks(cmd: Sequence[str], world: int, env: Optional[dict] = None) -> int:
+    """Start `world` rank processes of `cmd` on this node with the torch.distributed.run
+    environment (RANK, LOCAL_RANK, WORLD_SIZE, LOCAL_WORLD_SIZE, MASTER_ADDR=127.0.0.1,
+    MASTER_PORT). The caller must not have touched the GPU: the ranks are fresh
+    processes (no exec of the caller). Returns the first non-zero exit code, else 0."""
+    import subprocess
+    port = _free_port()
+    base = dict(os.environ if env is None else env)
+    procs = []
+    for r in range(world):
+        e = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+                 GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(list(cmd), env=e))
+    rcs = [p.wait() for p in procs]
+    return next((rc for rc in rcs if rc != 0), 0)
+
+
+def device_for_rank(local_rank: int) -> int:
+    """cuda:LOCAL_RANK, folded onto the visible devices when ranks outnumber them (a
+    rehearsal of N ranks on a smaller box shares GPUs; the driver's N-GPU node does not)."""
+    import torch
+    n = torch.cuda.device_count()   # counts devices without initialising HIP
+    return local_rank % n if n > 0 else local_rank
 
 
 def face_runner(device_index: Optional[int] = None, **face_kwargs) -> FrameShardRunner:

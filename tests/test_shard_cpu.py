@@ -1,6 +1,6 @@
 """Multi-process (gloo, world_size 2, CPU) coverage of the frame-shard runner:
-round-robin assignment and frame-ordered gather on rank 0; and the bench's
-max-over-ranks timing reduction."""
+contiguous assignment and frame-ordered gather on rank 0; the bench's
+max-over-ranks timing reduction; and the rank launcher bench.py --gpus N uses."""
 import os
 import socket
 
@@ -53,11 +53,12 @@ def test_frame_shard_gloo_world2(n):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert res[0][0] == [f"frame{i}" for i in range(0, n, 2)]
-    assert res[1][0] == [f"frame{i}" for i in range(1, n, 2)]
+    h = n // 2
+    assert res[0][0] == [f"frame{i}" for i in range(0, h)]
+    assert res[1][0] == [f"frame{i}" for i in range(h, n)]
     assert res[1][1] is None
     assert [d["frame"] for d in res[0][1]] == [f"frame{i}" for i in range(n)]
-    assert all(d["rank"] == i % 2 for i, d in enumerate(res[0][1]))
+    assert all(d["rank"] == (0 if i < h else 1) for i, d in enumerate(res[0][1]))
     assert res[0][2] == res[1][2] == 2.0
 
 
@@ -65,5 +66,24 @@ def test_shard_helpers():
     for n in range(0, 20):
         for w in (1, 2, 3, 8):
             parts = [shard_indices(n, r, w) for r in range(w)]
-            assert sorted(i for p in parts for i in p) == list(range(n))
+            assert [i for p in parts for i in p] == list(range(n))   # contiguous, in rank order
+            assert max(map(len, parts)) - min(map(len, parts)) <= 1
             assert merge_in_order(n, w, parts) == list(range(n))
+
+
+def test_bench_launcher_world2():
+    """bench.py --gpus 2 (no torch.distributed.run) spawns two rank processes with the
+    launcher environment; they init gloo, split the frames contiguously and rank 0 prints
+    ONE JSON line with n_gpus 2 and the frames of both ranks."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run", "--steps", "3",
+                        "--batch", "5"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["frames"] == 2 * 5 * 3 and out["local_rank"] == 0
