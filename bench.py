@@ -326,7 +326,7 @@ def main_other(args):
         def step():
             for i, d in enumerate(devs):   # gui_app.py:1505-1507
                 nh = int(round(H * (Wmax / float(W))))
-                small[i] = fe._dev_resize(d, Wmax, nh, True, key=f"prescan{i}")
+                small[i] = fe._dev_resize(d, f"prescan{i}", dsize=(Wmax, nh), area=True)
             faces = fe.extract_batch([None] * len(small), dev_frames=small, bank=bank)
             stats["faces"] = sum(len(f) for f in faces)
             return faces

@@ -31,6 +31,7 @@
  *                                      (face_embedder.py:2165-2169, 2292-2294, 2394)
  *   pc_resize_area                     cv2.resize(..., INTER_AREA) (gui_app.py:1505-1507)
  *   pc_resize_linear                   cv2.resize(..., INTER_LINEAR) (face_embedder.py:2264, 2460)
+ *   pc_resize_area_fast                cv2.resize(..., INTER_AREA) at integer ratios (face_embedder.py:2460)
  *   pc_yolo_detect                     PersonDetector.detect -> [ext] ultralytics YOLO.predict(conf, iou=0.45,
  *                                      classes=[0], max_det=40, imgsz=640) (detectors.py:271-296)
  *   pc_clip_prep / pc_clip_embed       ReIDEmbedder.extract: BGR2RGB + open_clip preprocess + encode_image +
@@ -91,15 +92,17 @@ typedef struct pc_warp_desc {
   int32_t pad1_;
 } pc_warp_desc;
 
-/* One u8 -> u8 INTER_LINEAR resize job (cv2.resize semantics, BGR). */
+/* One u8 -> u8 bilinear resize job (cv2.resize semantics, BGR): INTER_LINEAR, or INTER_AREA
+ * when not both axes downscale (area_mode = 1: OpenCV's area-mode linear coefficients). */
 typedef struct pc_resize_desc {
   const uint8_t* d_src;
   int32_t H, W, row_stride;
   int32_t new_w, new_h;
-  double scale_x, scale_y;
+  double scale_x, scale_y; /* 1 / inv_scale */
   int32_t simd_end;
-  int32_t pad_;
+  int32_t area_mode;
   uint8_t* d_dst; /* new_h x new_w x 3 contiguous */
+  double inv_x, inv_y; /* dsize / ssize, or the fx / fy given */
 } pc_resize_desc;
 
 /* One INTER_AREA coefficient: source index, destination index, weight. */
@@ -148,6 +151,9 @@ int pc_copy_h2d(pc_ctx* ctx, void* d_dst, const void* h_src, size_t bytes); /* s
 int pc_copy_d2h(pc_ctx* ctx, void* h_dst, const void* d_src, size_t bytes); /* stream-ordered */
 int pc_copy_d2d(pc_ctx* ctx, void* d_dst, const void* d_src, size_t bytes);
 int pc_memset(pc_ctx* ctx, void* d_dst, int value, size_t bytes);
+/* device -> device pitched copy (cv2.resize to the same size copies, resize.cpp) */
+int pc_copy_2d(pc_ctx* ctx, void* d_dst, size_t dst_pitch, const void* d_src, size_t src_pitch, size_t width_bytes,
+               size_t rows);
 /* Pinned host memory (page-locked: D2H copies into it stay asynchronous) and stream
  * fences. A fence is a HIP event recorded on the context stream; pc_fence_wait blocks
  * the host until everything enqueued before the record has finished. Used to overlap
@@ -188,6 +194,9 @@ int pc_resize_linear(pc_ctx* ctx, const pc_resize_desc* h_descs, int n);
 int pc_face_quality(pc_ctx* ctx, const uint8_t* d_chips, int n, int side, double* d_out);
 int pc_arcface_prep(pc_ctx* ctx, int precision, const uint8_t* d_chips, int n, int side, int flip, void* d_out);
 int pc_rotate_pad(pc_ctx* ctx, const uint8_t* d_src, int H, int W, int row_stride, int deg, int pad, uint8_t* d_dst);
+/* cv2.resize INTER_AREA at an exact integer ratio isx x isy (OpenCV resizeAreaFast). */
+int pc_resize_area_fast(pc_ctx* ctx, const uint8_t* d_src, int row_stride, int isx, int isy, uint8_t* d_dst, int OH,
+                        int OW);
 int pc_resize_area(pc_ctx* ctx, const uint8_t* d_src, int row_stride, const pc_area_tab* h_xtab,
                    const int32_t* h_xstart, int n_x, const pc_area_tab* h_ytab, const int32_t* h_ystart, int n_y,
                    uint8_t* d_dst, int OH, int OW);
@@ -195,8 +204,9 @@ int pc_resize_area(pc_ctx* ctx, const uint8_t* d_src, int row_stride, const pc_a
 /* ---- detection ---- */
 /* Runs letterbox -> SCRFD net -> decode(score >= det_thresh) -> NMS(nms_thresh) for n frames.
  * Outputs (device): d_dets [n][max_det][5], d_kps [n][max_det][10], d_count [n] (number kept,
- * may exceed max_det: then only the first max_det rows are written), d_ncand [n] candidates
- * above threshold (capacity 8192 per frame; more is PC_ERR_CAPACITY on the next call). */
+ * may exceed max_det: then only the first max_det rows are written; call again with a larger
+ * max_det for the full list), d_ncand [n] candidates above threshold. No candidate cap: every
+ * anchor of the net has a slot, as the reference keeps every candidate >= det_thresh. */
 int pc_scrfd_detect(pc_net* net, const pc_letterbox_desc* h_descs, int n, int D, float det_thresh,
                     float nms_thresh, const float* h_det_scale, int max_det, float* d_dets, float* d_kps,
                     int32_t* d_count, int32_t* d_ncand);

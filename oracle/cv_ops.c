@@ -33,11 +33,22 @@ static int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v
 static int round_f(float v) { return (int)lrintf(v); }
 static int round_d(double v) { return (int)lrint(v); }
 
-static void linear_coefs(int dsize, int ssize, double scale, int* ofs, short* c0, short* c1) {
+/* resize.cpp coefficient loop (ksize 2). area_mode: INTER_AREA requested but not both axes
+ * downscale -> sx = cvFloor(dx*scale), fx = (float)((dx+1) - (sx+1)*inv_scale) wrapped to [0,1). */
+static void linear_coefs2(int dsize, int ssize, double scale, double inv_scale, int area_mode, int* ofs, short* c0,
+                          short* c1) {
   for (int d = 0; d < dsize; ++d) {
-    float f = (float)((d + 0.5) * scale - 0.5);
-    int s = (int)floorf(f);
-    f -= (float)s;
+    float f;
+    int s;
+    if (!area_mode) {
+      f = (float)((d + 0.5) * scale - 0.5);
+      s = (int)floorf(f);
+      f -= (float)s;
+    } else {
+      s = (int)floor(d * scale);
+      f = (float)((d + 1) - (s + 1) * inv_scale);
+      f = f <= 0 ? 0.f : f - (float)(int)floorf(f);
+    }
     if (s < 0) { f = 0.f; s = 0; }
     if (s >= ssize - 1) { f = 0.f; s = ssize - 1; }
     ofs[d] = s;
@@ -46,9 +57,20 @@ static void linear_coefs(int dsize, int ssize, double scale, int* ofs, short* c0
   }
 }
 
+static void linear_coefs(int dsize, int ssize, double scale, int* ofs, short* c0, short* c1) {
+  linear_coefs2(dsize, ssize, scale, 0.0, 0, ofs, c0, c1);
+}
+
 /* dst: new_h x new_w x 3 contiguous */
+void cv_resize_linear2_u8(const uint8_t* src, int H, int W, int row_stride, uint8_t* dst, int new_w, int new_h,
+                          double scale_x, double scale_y, double inv_x, double inv_y, int area_mode, int simd_end);
 void cv_resize_linear_u8(const uint8_t* src, int H, int W, int row_stride, uint8_t* dst, int new_w, int new_h,
                          double scale_x, double scale_y, int simd_end) {
+  cv_resize_linear2_u8(src, H, W, row_stride, dst, new_w, new_h, scale_x, scale_y, 0.0, 0.0, 0, simd_end);
+}
+
+void cv_resize_linear2_u8(const uint8_t* src, int H, int W, int row_stride, uint8_t* dst, int new_w, int new_h,
+                          double scale_x, double scale_y, double inv_x, double inv_y, int area_mode, int simd_end) {
   int* xo = (int*)malloc(sizeof(int) * new_w);
   short* a0 = (short*)malloc(sizeof(short) * new_w);
   short* a1 = (short*)malloc(sizeof(short) * new_w);
@@ -57,8 +79,8 @@ void cv_resize_linear_u8(const uint8_t* src, int H, int W, int row_stride, uint8
   short* b1 = (short*)malloc(sizeof(short) * new_h);
   int* S0 = (int*)malloc(sizeof(int) * new_w * 3);
   int* S1 = (int*)malloc(sizeof(int) * new_w * 3);
-  linear_coefs(new_w, W, scale_x, xo, a0, a1);
-  linear_coefs(new_h, H, scale_y, yo, b0, b1);
+  linear_coefs2(new_w, W, scale_x, inv_x, area_mode, xo, a0, a1);
+  linear_coefs2(new_h, H, scale_y, inv_y, area_mode, yo, b0, b1);
   for (int dy = 0; dy < new_h; ++dy) {
     const int sy0 = yo[dy];
     const int sy1 = sy0 + 1 < H ? sy0 + 1 : H - 1;
@@ -205,10 +227,31 @@ int cv_area_tab(int ssize, int dsize, double scale, int* si, int* di, float* alp
   return k;
 }
 
+/* INTER_AREA at an exact integer ratio (resizeAreaFast_Invoker, CV_8UC3): 2x2 goes through
+ * ResizeAreaFastVec, (a+b+c+d+2)>>2 for every byte; other ratios saturate_cast<uchar>(sum * (1.f/area)). */
+void cv_resize_area_fast_u8(const uint8_t* src, int row_stride, int isx, int isy, uint8_t* dst, int OH, int OW) {
+  const float scale = 1.f / (float)(isx * isy);
+  for (int dy = 0; dy < OH; ++dy)
+    for (int dx = 0; dx < OW; ++dx)
+      for (int c = 0; c < 3; ++c) {
+        int sum = 0;
+        for (int j = 0; j < isy; ++j)
+          for (int i = 0; i < isx; ++i) sum += src[(size_t)(dy * isy + j) * row_stride + (dx * isx + i) * 3 + c];
+        const int v = (isx == 2 && isy == 2) ? ((sum + 2) >> 2) : round_f((float)sum * scale);
+        dst[((size_t)dy * OW + dx) * 3 + c] = (uint8_t)clampi(v, 0, 255);
+      }
+}
+
 /* INTER_AREA generic path, CV_8UC3. Row buffer accumulated per source row in table
  * order, then beta-weighted into the destination row sum (float), saturate_cast at the end. */
+void cv_resize_area2_u8(const uint8_t* src, int H, int W, int row_stride, uint8_t* dst, int OH, int OW, double sx,
+                        double sy);
 void cv_resize_area_u8(const uint8_t* src, int H, int W, int row_stride, uint8_t* dst, int OH, int OW) {
-  const double sx = (double)W / OW, sy = (double)H / OH;
+  cv_resize_area2_u8(src, H, W, row_stride, dst, OH, OW, 1.0 / ((double)OW / W), 1.0 / ((double)OH / H));
+}
+
+void cv_resize_area2_u8(const uint8_t* src, int H, int W, int row_stride, uint8_t* dst, int OH, int OW, double sx,
+                        double sy) {
   int* xs = (int*)malloc(sizeof(int) * W * 2); int* xd = (int*)malloc(sizeof(int) * W * 2);
   float* xa = (float*)malloc(sizeof(float) * W * 2);
   int* ys = (int*)malloc(sizeof(int) * H * 2); int* yd = (int*)malloc(sizeof(int) * H * 2);

@@ -31,6 +31,9 @@ def lib():
         _lib.cv_area_tab.argtypes = [I, I, D, P, P, P]
         _lib.cv_area_tab.restype = I
         _lib.cv_resize_area_u8.argtypes = [P, I, I, I, P, I, I]
+        _lib.cv_resize_area2_u8.argtypes = [P, I, I, I, P, I, I, D, D]
+        _lib.cv_resize_area_fast_u8.argtypes = [P, I, I, I, P, I, I]
+        _lib.cv_resize_linear2_u8.argtypes = [P, I, I, I, P, I, I, D, D, D, D, I, I]
     return _lib
 
 
@@ -101,3 +104,50 @@ def face_quality(chip_bgr: np.ndarray) -> float:
     p = np.pad(g, 1, mode="reflect")     # numpy 'reflect' == OpenCV BORDER_REFLECT_101
     lap = p[1:-1, :-2] + p[1:-1, 2:] + p[:-2, 1:-1] + p[2:, 1:-1] - 4.0 * g
     return float(lap.var())
+
+
+INTER_LINEAR = 1
+INTER_AREA = 3
+_DBL_EPSILON = 2.220446049250313e-16
+
+
+def simd_end(width_bytes: int) -> int:
+    """Byte index where OpenCV's 128-bit vertical linear pass stops (16-byte, then 8-byte steps)."""
+    x = (width_bytes // 16) * 16 if width_bytes >= 16 else 0
+    while x < width_bytes - 8:
+        x += 8
+    return x
+
+
+def resize(img: np.ndarray, dsize=None, fx: float = 0.0, fy: float = 0.0,
+           interpolation: int = INTER_LINEAR) -> np.ndarray:
+    """cv2.resize for u8 BGR with OpenCV 4.9's dispatch (imgproc/src/resize.cpp, cv::resize and
+    hal::resize): dsize from fx/fy by cvRound, copy when the size is unchanged, scale = 1/inv_scale,
+    INTER_LINEAR at exactly 2x2 down -> area fast, INTER_AREA with both axes downscaling -> the area
+    paths (integer ratio: resizeAreaFast; else the generic tables), INTER_AREA otherwise -> the
+    linear kernel with area-mode coefficients."""
+    img = np.ascontiguousarray(img, np.uint8)
+    H, W = img.shape[:2]
+    if dsize is None or tuple(dsize) == (0, 0):
+        inv_x, inv_y = float(fx), float(fy)
+        new_w, new_h = int(round(W * inv_x)), int(round(H * inv_y))
+    else:
+        new_w, new_h = int(dsize[0]), int(dsize[1])
+        inv_x, inv_y = float(new_w) / W, float(new_h) / H
+    if (new_w, new_h) == (W, H):
+        return img.copy()
+    sx, sy = 1.0 / inv_x, 1.0 / inv_y
+    isx, isy = int(round(sx)), int(round(sy))
+    fast = abs(sx - isx) < _DBL_EPSILON and abs(sy - isy) < _DBL_EPSILON
+    if interpolation == INTER_LINEAR and fast and isx == 2 and isy == 2:
+        interpolation = INTER_AREA
+    out = np.empty((new_h, new_w, 3), np.uint8)
+    if interpolation == INTER_AREA and sx >= 1 and sy >= 1:
+        if fast:
+            lib().cv_resize_area_fast_u8(_p(img), img.strides[0], isx, isy, _p(out), new_h, new_w)
+        else:
+            lib().cv_resize_area2_u8(_p(img), H, W, img.strides[0], _p(out), new_h, new_w, sx, sy)
+        return out
+    lib().cv_resize_linear2_u8(_p(img), H, W, img.strides[0], _p(out), new_w, new_h, sx, sy, inv_x, inv_y,
+                               1 if interpolation == INTER_AREA else 0, simd_end(new_w * 3))
+    return out

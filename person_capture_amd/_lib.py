@@ -35,7 +35,8 @@ class WarpDesc(C.Structure):
 class ResizeDesc(C.Structure):
     _fields_ = [("d_src", C.c_void_p), ("H", C.c_int32), ("W", C.c_int32), ("row_stride", C.c_int32),
                 ("new_w", C.c_int32), ("new_h", C.c_int32), ("scale_x", C.c_double), ("scale_y", C.c_double),
-                ("simd_end", C.c_int32), ("pad_", C.c_int32), ("d_dst", C.c_void_p)]
+                ("simd_end", C.c_int32), ("area_mode", C.c_int32), ("d_dst", C.c_void_p),
+                ("inv_x", C.c_double), ("inv_y", C.c_double)]
 
 
 class AreaTab(C.Structure):
@@ -59,7 +60,7 @@ class CropDesc(C.Structure):
 
 
 assert C.sizeof(YoloLetterboxDesc) == 64 and C.sizeof(YoloScale) == 20 and C.sizeof(CropDesc) == 24
-assert C.sizeof(ResizeDesc) == 64 and C.sizeof(LetterboxDesc) == 56 and C.sizeof(WarpDesc) == 96 and C.sizeof(AreaTab) == 12
+assert C.sizeof(ResizeDesc) == 80 and C.sizeof(LetterboxDesc) == 56 and C.sizeof(WarpDesc) == 96 and C.sizeof(AreaTab) == 12
 
 _P = C.c_void_p
 _I = C.c_int
@@ -80,6 +81,7 @@ SIGNATURES = {
     "pc_copy_d2h": ([_P, _P, _P, _SZ], _I),
     "pc_copy_d2d": ([_P, _P, _P, _SZ], _I),
     "pc_memset": ([_P, _P, _I, _SZ], _I),
+    "pc_copy_2d": ([_P, _P, _SZ, _P, _SZ, _SZ, _SZ], _I),
     "pc_host_alloc": ([_P, _SZ, C.POINTER(_P)], _I),
     "pc_host_free": ([_P, _P], _I),
     "pc_fence_create": ([_P, C.POINTER(_P)], _I),
@@ -103,6 +105,7 @@ SIGNATURES = {
     "pc_face_quality": ([_P, _P, _I, _I, _P], _I),
     "pc_arcface_prep": ([_P, _I, _P, _I, _I, _I, _P], _I),
     "pc_rotate_pad": ([_P, _P, _I, _I, _I, _I, _I, _P], _I),
+    "pc_resize_area_fast": ([_P, _P, _I, _I, _I, _P, _I, _I], _I),
     "pc_resize_area": ([_P, _P, _I, C.POINTER(AreaTab), C.POINTER(C.c_int32), _I, C.POINTER(AreaTab),
                         C.POINTER(C.c_int32), _I, _P, _I, _I], _I),
     "pc_scrfd_detect": ([_P, C.POINTER(LetterboxDesc), _I, _I, _F, _F, C.POINTER(_F), _I, _P, _P, _P, _P], _I),

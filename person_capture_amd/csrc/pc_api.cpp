@@ -43,6 +43,8 @@ hipError_t quality_launch(const uint8_t* chips, int N, int side, double* out, hi
 hipError_t arcprep_launch(int f32, const uint8_t* chips, int N, int side, int flip, void* out, hipStream_t s);
 hipError_t rotate_pad_launch(const uint8_t* src, int H, int W, int row_stride, int deg, int pad, uint8_t* dst, int OH,
                              int OW, hipStream_t s);
+hipError_t resize_area_fast_launch(const uint8_t* src, int row_stride, int isx, int isy, uint8_t* dst, int OH, int OW,
+                                   hipStream_t s);
 hipError_t resize_area_launch(const uint8_t* src, int row_stride, const AreaTab* xtab, const int* xstart,
                               const AreaTab* ytab, const int* ystart, uint8_t* dst, int OH, int OW, hipStream_t s);
 hipError_t embed_finalize_launch(const float* e, int ld, int n, int dim, int flip, float* out, hipStream_t s);
@@ -65,6 +67,9 @@ struct DecodeParams {
   int cap;
 };
 hipError_t scrfd_decode_launch(const DecodeParams& p, int N, hipStream_t s);
+hipError_t scrfd_nms_big_launch(const float* cand, const int* count, int cap, int pcap, unsigned long long* keys,
+                                int* slot_of, float* kept, float nms_thresh, int max_det, float* dets, float* kps,
+                                int* nkeep, int N, hipStream_t s);
 hipError_t scrfd_nms_launch(const float* cand, const int* count, int cap, float nms_thresh, int max_det, float* dets,
                             float* kps, int* nkeep, int N, hipStream_t s);
 hipError_t embed_l2_launch(const float* e, int ld, int n, int dim, float eps, float* out, hipStream_t s);
@@ -101,7 +106,7 @@ using namespace pc;
 static_assert(sizeof(pc_letterbox_desc) == 56, "letterbox desc layout");
 static_assert(sizeof(pc_warp_desc) == 96, "warp desc layout");
 static_assert(sizeof(pc_area_tab) == 12, "area tab layout");
-static_assert(sizeof(pc_resize_desc) == 64, "resize desc layout");
+static_assert(sizeof(pc_resize_desc) == 80, "resize desc layout");
 static_assert(sizeof(pc_yolo_letterbox_desc) == 64, "yolo letterbox desc layout");
 static_assert(sizeof(pc_yolo_scale) == 20, "yolo scale layout");
 
@@ -119,7 +124,10 @@ struct pc_ctx {
   float* cand = nullptr;
   int* cand_count = nullptr;
   float* det_scale = nullptr;
-  size_t cand_images = 0;
+  size_t cand_bytes = 0;
+  // large-candidate NMS scratch (scrfd_nms_big): sort keys, anchor -> slot map, kept boxes
+  void* nms_big = nullptr;
+  size_t nms_big_bytes = 0;
   // YOLO candidates
   float* ycand = nullptr;
   int* ycount = nullptr;
@@ -202,6 +210,7 @@ extern "C" int pc_ctx_destroy(pc_ctx* c) {
   if (c->stage_d) hipFree(c->stage_d);
   if (c->cand) hipFree(c->cand);
   if (c->cand_count) hipFree(c->cand_count);
+  if (c->nms_big) hipFree(c->nms_big);
   if (c->det_scale) hipFree(c->det_scale);
   if (c->ycand) hipFree(c->ycand);
   if (c->ycount) hipFree(c->ycount);
@@ -284,6 +293,16 @@ extern "C" int pc_copy_d2d(pc_ctx* c, void* d, const void* s, size_t n) {
   if (n) HIPCHK(c, hipMemcpyAsync(d, s, n, hipMemcpyDeviceToDevice, c->stream));
   return PC_OK;
 }
+extern "C" int pc_copy_2d(pc_ctx* c, void* d_dst, size_t dst_pitch, const void* d_src, size_t src_pitch,
+                          size_t width_bytes, size_t rows) {
+  if (!c || !d_dst || !d_src || width_bytes > dst_pitch || width_bytes > src_pitch)
+    return fail(c, PC_ERR_ARG, "pc_copy_2d: bad arguments");
+  if (!width_bytes || !rows) return PC_OK;
+  HIPCHK(c, hipMemcpy2DAsync(d_dst, dst_pitch, d_src, src_pitch, width_bytes, rows, hipMemcpyDeviceToDevice,
+                             c->stream));
+  return PC_OK;
+}
+
 extern "C" int pc_memset(pc_ctx* c, void* d, int v, size_t n) {
   if (!c) return PC_ERR_ARG;
   if (n) HIPCHK(c, hipMemsetAsync(d, v, n, c->stream));
@@ -1060,6 +1079,14 @@ extern "C" int pc_resize_area(pc_ctx* c, const uint8_t* src, int row_stride, con
   return PC_OK;
 }
 
+extern "C" int pc_resize_area_fast(pc_ctx* c, const uint8_t* src, int row_stride, int isx, int isy, uint8_t* dst,
+                                   int OH, int OW) {
+  if (!c || !src || !dst || isx < 1 || isy < 1 || OH <= 0 || OW <= 0)
+    return fail(c, PC_ERR_ARG, "pc_resize_area_fast: bad arguments");
+  HIPCHK(c, resize_area_fast_launch(src, row_stride, isx, isy, dst, OH, OW, c->stream));
+  return PC_OK;
+}
+
 extern "C" int pc_embed_finalize(pc_ctx* c, const float* e, int ld, int n, int dim, int flip, float* out) {
   if (!c || n < 0) return fail(c, PC_ERR_ARG, "pc_embed_finalize: bad arguments");
   if (n == 0) return PC_OK;
@@ -1107,15 +1134,27 @@ extern "C" int pc_scrfd_detect(pc_net* net, const pc_letterbox_desc* h, int n, i
   if ((int)net->outs.size() != 3) return fail(c, PC_ERR_FORMAT, "SCRFD net must have 3 outputs");
   const NetTensor& I = net->tens[net->in_tensor];
   if (I.H != D || I.W != D) return fail(c, PC_ERR_ARG, "pc_scrfd_detect: D does not match the net input size");
-  const int cap = 8192;
-  if (c->cand_images < (size_t)n) {
+  // candidate capacity = every anchor of the net (no cap: the reference keeps all
+  // candidates >= det_thresh); images with more than 8192 go through scrfd_nms_big
+  int cap = 0;
+  for (int l = 0; l < 3; ++l) cap += net->tens[net->outs[l]].H * net->tens[net->outs[l]].W * 2;
+  int pcap = 8192;
+  while (pcap < cap) pcap <<= 1;
+  const size_t cand_need = (size_t)n * cap * 16 * 4;
+  if (c->cand_bytes < cand_need) {
     if (c->cand) hipFree(c->cand);
     if (c->cand_count) hipFree(c->cand_count);
     if (c->det_scale) hipFree(c->det_scale);
-    HIPCHK(c, hipMalloc((void**)&c->cand, (size_t)n * cap * 16 * 4));
-    HIPCHK(c, hipMalloc((void**)&c->cand_count, (size_t)n * 4));
-    HIPCHK(c, hipMalloc((void**)&c->det_scale, (size_t)n * 4));
-    c->cand_images = n;
+    HIPCHK(c, hipMalloc((void**)&c->cand, cand_need));
+    HIPCHK(c, hipMalloc((void**)&c->cand_count, (size_t)n * 4 + 256));
+    HIPCHK(c, hipMalloc((void**)&c->det_scale, (size_t)n * 4 + 256));
+    c->cand_bytes = cand_need;
+  }
+  const size_t keys_b = (size_t)n * pcap * 8, map_b = (size_t)n * cap * 4, kept_b = (size_t)n * cap * 16;
+  if (c->nms_big_bytes < keys_b + map_b + kept_b) {
+    if (c->nms_big) hipFree(c->nms_big);
+    HIPCHK(c, hipMalloc(&c->nms_big, keys_b + map_b + kept_b));
+    c->nms_big_bytes = keys_b + map_b + kept_b;
   }
   // letterbox into the net's own input staging area (reuse prep scratch)
   const size_t need = (size_t)net->max_batch * D * D * 4 * (net->f32 ? 4 : 2);
@@ -1153,6 +1192,12 @@ extern "C" int pc_scrfd_detect(pc_net* net, const pc_letterbox_desc* h, int n, i
   p.cap = cap;
   HIPCHK(c, scrfd_decode_launch(p, n, c->stream));
   HIPCHK(c, scrfd_nms_launch(c->cand, c->cand_count, cap, nms_thresh, max_det, dets, kps, count, n, c->stream));
+  {
+    char* big = (char*)c->nms_big;
+    HIPCHK(c, scrfd_nms_big_launch(c->cand, c->cand_count, cap, pcap, (unsigned long long*)big, (int*)(big + keys_b),
+                                   (float*)(big + keys_b + map_b), nms_thresh, max_det, dets, kps, count, n,
+                                   c->stream));
+  }
   if (ncand) HIPCHK(c, hipMemcpyAsync(ncand, c->cand_count, n * 4, hipMemcpyDeviceToDevice, c->stream));
   return PC_OK;
 }

@@ -83,6 +83,7 @@ __global__ __launch_bounds__(1024) void scrfd_nms(const float* __restrict__ cand
   const int n = blockIdx.x;
   const int tid = threadIdx.x;
   const int K = min(count[n], cap);
+  if (K > NMS_CAP) return;   // scrfd_nms_big handles this image
   const float* cb = cand + (long long)n * cap * 16;
   int P = 1;
   while (P < K) P <<= 1;
@@ -151,6 +152,161 @@ __global__ __launch_bounds__(1024) void scrfd_nms(const float* __restrict__ cand
   if (tid == 0) nkeep[n] = kept;
 }
 
+// The same greedy NMS for an image with more than NMS_CAP candidates (low thresholds at
+// the heavy rotation sizes, up to 2*(D/8)^2*(1+1/4+1/16) anchors): keys live in global
+// memory, sorted by a single-workgroup bitonic network whose strides below BIG_TILE run
+// in LDS; then the greedy pass walks the sorted order in blocks of 1024: every
+// candidate of a block is first tested against all boxes kept so far (in parallel),
+// then the block is resolved in order (one barrier round per kept box). Same keys (score
+// desc, anchor index asc), same IoU arithmetic, same suppression test as scrfd_nms.
+constexpr int BIG_TILE = 8192;
+
+__device__ inline void cmpswap(unsigned long long& a, unsigned long long& b, bool up) {
+  if ((a > b) == up) { const unsigned long long t = a; a = b; b = t; }
+}
+
+__global__ __launch_bounds__(1024) void scrfd_nms_big(const float* __restrict__ cand, const int* __restrict__ count,
+                                                      int cap, int pcap, unsigned long long* __restrict__ keys_g,
+                                                      int* __restrict__ slot_of, float* __restrict__ kept_g,
+                                                      float nms_thresh, int max_det, float* __restrict__ dets,
+                                                      float* __restrict__ kps, int* __restrict__ nkeep) {
+  __shared__ unsigned long long tile[BIG_TILE];
+  __shared__ float sbox[1024][4];
+  __shared__ unsigned char ssup[1024];
+  __shared__ int s_next;
+  const int n = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int K = min(count[n], cap);
+  if (K <= NMS_CAP) return;
+  const float* cb = cand + (long long)n * cap * 16;
+  unsigned long long* keys = keys_g + (long long)n * pcap;
+  int* smap = slot_of + (long long)n * cap;
+  float* kept_box = kept_g + (long long)n * cap * 4;
+  int P = BIG_TILE;
+  while (P < K) P <<= 1;
+  for (int i = tid; i < P; i += 1024) {
+    unsigned long long key = ~0ull;
+    if (i < K) {
+      const unsigned u = __float_as_uint(cb[i * 16 + 4]);
+      const unsigned ord = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+      const unsigned aidx = __float_as_uint(cb[i * 16 + 15]);
+      key = ((unsigned long long)(~ord) << 32) | aidx;   // anchor indices are unique per image
+      smap[aidx] = i;
+    }
+    keys[i] = key;
+  }
+  __syncthreads();
+  // bitonic sort ascending; all stages with k <= BIG_TILE in one LDS visit per tile
+  for (int t0 = 0; t0 < P; t0 += BIG_TILE) {
+    for (int i = tid; i < BIG_TILE; i += 1024) tile[i] = keys[t0 + i];
+    __syncthreads();
+    for (int k = 2; k <= BIG_TILE; k <<= 1)
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int li = tid; li < BIG_TILE; li += 1024) {
+          const int lx = li ^ j;
+          if (lx > li) cmpswap(tile[li], tile[lx], ((t0 + li) & k) == 0);
+        }
+        __syncthreads();
+      }
+    for (int i = tid; i < BIG_TILE; i += 1024) keys[t0 + i] = tile[i];
+    __syncthreads();
+  }
+  for (int k = 2 * BIG_TILE; k <= P; k <<= 1) {
+    int j = k >> 1;
+    for (; j >= BIG_TILE; j >>= 1) {
+      for (int i = tid; i < P; i += 1024) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          unsigned long long a = keys[i], b = keys[ixj];
+          cmpswap(a, b, (i & k) == 0);
+          keys[i] = a; keys[ixj] = b;
+        }
+      }
+      __syncthreads();
+    }
+    for (int t0 = 0; t0 < P; t0 += BIG_TILE) {
+      for (int i = tid; i < BIG_TILE; i += 1024) tile[i] = keys[t0 + i];
+      __syncthreads();
+      for (int jj = j; jj > 0; jj >>= 1) {
+        for (int li = tid; li < BIG_TILE; li += 1024) {
+          const int lx = li ^ jj;
+          if (lx > li) cmpswap(tile[li], tile[lx], ((t0 + li) & k) == 0);
+        }
+        __syncthreads();
+      }
+      for (int i = tid; i < BIG_TILE; i += 1024) keys[t0 + i] = tile[i];
+      __syncthreads();
+    }
+  }
+  // blocked greedy pass
+  int nk = 0;
+  for (int b0 = 0; b0 < K; b0 += 1024) {
+    const int i = b0 + tid;
+    bool sup = i >= K;
+    float x1 = 0.f, y1 = 0.f, x2 = 0.f, y2 = 0.f, area = 0.f;
+    int si = 0;
+    if (!sup) {
+      si = smap[(unsigned)(keys[i] & 0xFFFFFFFFull)];
+      const float* bj = cb + si * 16;
+      x1 = bj[0]; y1 = bj[1]; x2 = bj[2]; y2 = bj[3];
+      area = (x2 - x1 + 1.0f) * (y2 - y1 + 1.0f);
+      for (int q = 0; q < nk; ++q) {
+        const float* kb = kept_box + q * 4;
+        const float kx1 = kb[0], ky1 = kb[1], kx2 = kb[2], ky2 = kb[3];
+        const float area_k = (kx2 - kx1 + 1.0f) * (ky2 - ky1 + 1.0f);
+        const float w = fmaxf(0.0f, fminf(kx2, x2) - fmaxf(kx1, x1) + 1.0f);
+        const float h = fmaxf(0.0f, fminf(ky2, y2) - fmaxf(ky1, y1) + 1.0f);
+        const float inter = w * h;
+        const float ovr = inter / (area_k + area - inter);
+        if (!(ovr <= nms_thresh)) { sup = true; break; }
+      }
+    }
+    sbox[tid][0] = x1; sbox[tid][1] = y1; sbox[tid][2] = x2; sbox[tid][3] = y2;
+    ssup[tid] = sup ? 1 : 0;
+    __syncthreads();
+    int cur = 0;
+    while (true) {
+      if (tid == 0) s_next = 1024;
+      __syncthreads();
+      if (tid >= cur && !ssup[tid]) atomicMin(&s_next, tid);
+      __syncthreads();
+      const int c = s_next;
+      if (c >= 1024) break;
+      if (tid == c) {
+        float* kb = kept_box + nk * 4;
+        kb[0] = x1; kb[1] = y1; kb[2] = x2; kb[3] = y2;
+        if (nk < max_det) {
+          const float* src = cb + si * 16;
+          for (int e = 0; e < 5; ++e) dets[((long long)n * max_det + nk) * 5 + e] = src[e];
+          for (int e = 0; e < 10; ++e) kps[((long long)n * max_det + nk) * 10 + e] = src[5 + e];
+        }
+      }
+      if (tid > c && !ssup[tid]) {
+        const float cx1 = sbox[c][0], cy1 = sbox[c][1], cx2 = sbox[c][2], cy2 = sbox[c][3];
+        const float area_c = (cx2 - cx1 + 1.0f) * (cy2 - cy1 + 1.0f);
+        const float w = fmaxf(0.0f, fminf(cx2, x2) - fmaxf(cx1, x1) + 1.0f);
+        const float h = fmaxf(0.0f, fminf(cy2, y2) - fmaxf(cy1, y1) + 1.0f);
+        const float inter = w * h;
+        const float ovr = inter / (area_c + area - inter);
+        if (!(ovr <= nms_thresh)) ssup[tid] = 1;
+      }
+      ++nk;
+      cur = c + 1;
+      __syncthreads();
+    }
+    __syncthreads();
+  }
+  if (tid == 0) nkeep[n] = nk;
+}
+
+hipError_t scrfd_nms_big_launch(const float* cand, const int* count, int cap, int pcap, unsigned long long* keys,
+                                int* slot_of, float* kept, float nms_thresh, int max_det, float* dets, float* kps,
+                                int* nkeep, int N, hipStream_t s) {
+  hipLaunchKernelGGL(scrfd_nms_big, dim3(N), dim3(1024), 0, s, cand, count, cap, pcap, keys, slot_of, kept,
+                     nms_thresh, max_det, dets, kps, nkeep);
+  return hipGetLastError();
+}
+
 hipError_t scrfd_decode_launch(const DecodeParams& p, int N, hipStream_t s) {
   dim3 grid((p.total_loc + 255) / 256, N);
   hipLaunchKernelGGL(scrfd_decode, grid, dim3(256), 0, s, p);
@@ -159,7 +315,6 @@ hipError_t scrfd_decode_launch(const DecodeParams& p, int N, hipStream_t s) {
 
 hipError_t scrfd_nms_launch(const float* cand, const int* count, int cap, float nms_thresh, int max_det, float* dets,
                             float* kps, int* nkeep, int N, hipStream_t s) {
-  if (cap > NMS_CAP) return hipErrorInvalidValue;
   hipLaunchKernelGGL(scrfd_nms, dim3(N), dim3(1024), 0, s, cand, count, cap, nms_thresh, max_det, dets, kps, nkeep);
   return hipGetLastError();
 }

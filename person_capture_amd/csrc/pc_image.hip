@@ -94,15 +94,31 @@ __global__ void letterbox_blob(const LetterboxDesc* __restrict__ descs, int D, T
 
 // Plain u8 -> u8 INTER_LINEAR resize of a (crop of a) BGR frame, same fixed point
 // as the letterbox (TTA rescales face_embedder.py:2264, chip resize fallback :2460).
+// area_mode: cv::resize was asked for INTER_AREA but not both axes downscale, so OpenCV
+// runs the linear kernel with its "area mode" coefficients (resize.cpp: sx = floor(dx *
+// scale), fx = (dx+1) - (sx+1) * inv_scale, wrapped into [0,1)), on both axes.
 struct ResizeDesc {
   const uint8_t* src;
   int H, W, row_stride;
   int new_w, new_h;
-  double scale_x, scale_y;
+  double scale_x, scale_y;  // 1 / inv_scale, as hal::resize computes them
   int simd_end;
-  int pad_;
+  int area_mode;
   uint8_t* dst;  // new_h x new_w x 3 contiguous
+  double inv_x, inv_y;      // dsize/ssize, or the fx/fy the caller gave
 };
+
+__device__ __forceinline__ void lin_coef_area(int d, double scale, double inv, int src_len, int& s0, short& a0,
+                                              short& a1) {
+  int s = (int)floor(d * scale);
+  float f = (float)((d + 1) - (s + 1) * inv);
+  f = f <= 0.f ? 0.f : f - (float)(int)floorf(f);
+  if (s < 0) { f = 0.f; s = 0; }
+  if (s >= src_len - 1) { f = 0.f; s = src_len - 1; }
+  s0 = s;
+  a0 = (short)__float2int_rn((1.f - f) * 2048.f);
+  a1 = (short)__float2int_rn(f * 2048.f);
+}
 
 __global__ void resize_linear_u8(const ResizeDesc* __restrict__ descs) {
   const ResizeDesc d = descs[blockIdx.y];
@@ -111,8 +127,13 @@ __global__ void resize_linear_u8(const ResizeDesc* __restrict__ descs) {
   const int y = pix / d.new_w, x = pix - (pix / d.new_w) * d.new_w;
   int sx, sy;
   short a0, a1, b0, b1;
-  lin_coef(x, d.scale_x, d.W, sx, a0, a1);
-  lin_coef(y, d.scale_y, d.H, sy, b0, b1);
+  if (d.area_mode) {
+    lin_coef_area(x, d.scale_x, d.inv_x, d.W, sx, a0, a1);
+    lin_coef_area(y, d.scale_y, d.inv_y, d.H, sy, b0, b1);
+  } else {
+    lin_coef(x, d.scale_x, d.W, sx, a0, a1);
+    lin_coef(y, d.scale_y, d.H, sy, b0, b1);
+  }
   const int sx1 = sx + 1 < d.W ? sx + 1 : sx;
   const int sy1 = sy + 1 < d.H ? sy + 1 : sy;
   const uint8_t* r0 = d.src + (long long)sy * d.row_stride;
@@ -352,7 +373,36 @@ __global__ void resize_area_u8(const uint8_t* __restrict__ src, int row_stride,
   }
 }
 
+// cv2.resize INTER_AREA at an exact integer ratio (hal::resize "is_area_fast"):
+// resizeAreaFast_Invoker. 2x2 takes ResizeAreaFastVec ((sum + 2) >> 2 for every byte);
+// other ratios saturate_cast<uchar>(sum * (1.f / area)) (round half to even).
+__global__ void resize_area_fast_u8(const uint8_t* __restrict__ src, int row_stride, int isx, int isy,
+                                    uint8_t* __restrict__ dst, int OH, int OW) {
+  const int pix = blockIdx.x * blockDim.x + threadIdx.x;
+  if (pix >= OH * OW) return;
+  const int dy = pix / OW, dx = pix - (pix / OW) * OW;
+  const float scale = 1.f / (float)(isx * isy);
+  uint8_t* o = dst + (long long)pix * 3;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    int sum = 0;
+    for (int j = 0; j < isy; ++j) {
+      const uint8_t* row = src + (long long)(dy * isy + j) * row_stride + (dx * isx) * 3 + c;
+      for (int i = 0; i < isx; ++i) sum += row[i * 3];
+    }
+    int v = (isx == 2 && isy == 2) ? ((sum + 2) >> 2) : __float2int_rn((float)sum * scale);
+    o[c] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+  }
+}
+
 // ---------------------------------------------------------------------------
+hipError_t resize_area_fast_launch(const uint8_t* src, int row_stride, int isx, int isy, uint8_t* dst, int OH, int OW,
+                                   hipStream_t s) {
+  hipLaunchKernelGGL(resize_area_fast_u8, dim3((OH * OW + 255) / 256), dim3(256), 0, s, src, row_stride, isx, isy,
+                     dst, OH, OW);
+  return hipGetLastError();
+}
+
 hipError_t letterbox_launch(int f32, const LetterboxDesc* d_descs, int N, int D, void* out, hipStream_t s) {
   dim3 grid((D * D + 255) / 256, N);
   if (f32) hipLaunchKernelGGL(letterbox_blob<float>, grid, dim3(256), 0, s, d_descs, D, (float*)out);

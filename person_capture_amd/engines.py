@@ -161,16 +161,17 @@ class ScrfdEngine:
     def read_results(self, bufs, n: int) -> List[Tuple[np.ndarray, np.ndarray]]:
         dd, dk, dc, dn = bufs
         cnt = self.ctx.download(dc.ptr, (n,), np.int32)
-        ncand = self.ctx.download(dn.ptr, (n,), np.int32)
-        if np.any(ncand > 8192):
-            raise RuntimeError("SCRFD candidate capacity (8192 per frame) exceeded; raise det_thresh")
         dets = self.ctx.download(dd.ptr, (n, self.max_det, 5), np.float32)
         kps = self.ctx.download(dk.ptr, (n, self.max_det, 10), np.float32)
-        out = []
-        for i in range(n):
-            k = min(int(cnt[i]), self.max_det)
-            out.append((dets[i, :k].copy(), kps[i, :k].reshape(k, 5, 2).copy()))
-        return out
+        return self._unpack(cnt, dets, kps)
+
+    def _unpack(self, cnt, dets, kps) -> List[Tuple[np.ndarray, np.ndarray]]:
+        if np.any(cnt > self.max_det):
+            raise _MaxDetOverflow(int(cnt.max()))
+        return [(dets[i, :int(cnt[i])].copy(), kps[i, :int(cnt[i])].reshape(-1, 5, 2).copy()) for i in range(len(cnt))]
+
+    def _grow(self, need: int) -> None:
+        self.max_det = max(need, 2 * self.max_det)
 
     def detect_async(self, d_frames: Sequence[Tuple[int, int, int, int]], thresh: float, slot: str,
                      nms_thresh: float = 0.4) -> list:
@@ -196,18 +197,18 @@ class ScrfdEngine:
             views.append(self.ctx.download_async(buf.ptr, pin, off, shape, dt))
             off += sz
         fence = self.ctx.fence(f"scrfd{self.D}_{slot}")
-        return [fence, n] + views
+        return [fence, n] + views + [(thresh, nms_thresh), list(d_frames)]
 
     def collect(self, pending) -> List[Tuple[np.ndarray, np.ndarray]]:
-        fence, n, cnt, ncand, dets, kps = pending
+        fence, n, cnt, ncand, dets, kps = pending[:6]
         fence.wait()
-        if np.any(ncand > 8192):
-            raise RuntimeError("SCRFD candidate capacity (8192 per frame) exceeded; raise det_thresh")
-        out = []
-        for i in range(n):
-            k = min(int(cnt[i]), self.max_det)
-            out.append((dets[i, :k].copy(), kps[i, :k].reshape(k, 5, 2).copy()))
-        return out
+        try:
+            return self._unpack(cnt, dets, kps)
+        except _MaxDetOverflow as e:
+            # more faces kept than result rows: the device list is cut, so redo these frames
+            # with room for all of them (the reference has no cap)
+            self._grow(e.need)
+            return self.detect_frames(pending[-1], thresh=pending[-2][0], nms_thresh=pending[-2][1])
 
     def detect_frames(self, d_frames: Sequence[Tuple[int, int, int, int]], thresh: float,
                       nms_thresh: float = 0.4) -> List[Tuple[np.ndarray, np.ndarray]]:
@@ -219,6 +220,18 @@ class ScrfdEngine:
             scales.append(s)
         res = []
         for s0 in range(0, len(descs), self.max_batch):
-            b = self.detect_device(descs[s0:s0 + self.max_batch], scales[s0:s0 + self.max_batch], thresh, nms_thresh)
-            res.extend(self.read_results(b, len(descs[s0:s0 + self.max_batch])))
+            while True:
+                b = self.detect_device(descs[s0:s0 + self.max_batch], scales[s0:s0 + self.max_batch], thresh,
+                                       nms_thresh)
+                try:
+                    res.extend(self.read_results(b, len(descs[s0:s0 + self.max_batch])))
+                    break
+                except _MaxDetOverflow as e:
+                    self._grow(e.need)
         return res
+
+
+class _MaxDetOverflow(Exception):
+    def __init__(self, need: int):
+        super().__init__(f"{need} detections kept")
+        self.need = need

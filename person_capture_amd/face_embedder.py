@@ -257,25 +257,37 @@ class FaceEmbedder:
                                           buf.ptr), self._ctx.handle, "rotate_pad")
         return _DevImage(buf.ptr, OH, OW, OW * 3, buf)
 
-    def _dev_resize(self, img: _DevImage, new_w: int, new_h: int, area: bool, key: str,
-                    scale_x: Optional[float] = None, scale_y: Optional[float] = None) -> _DevImage:
-        """cv2.resize semantics: scale = 1/fx when fx was given, else old/new."""
-        sx = float(img.W) / new_w if scale_x is None else float(scale_x)
-        sy = float(img.H) / new_h if scale_y is None else float(scale_y)
-        buf = self._ctx.scratch(key, new_w * new_h * 3)
-        if area and sx >= 1.0 and sy >= 1.0:
-            (xt, xs), (yt, ys) = imageops.area_tables(img.W, new_w, sx), imageops.area_tables(img.H, new_h, sy)
-            check(self._ctx.lib.pc_resize_area(self._ctx.handle, img.ptr, img.stride, xt, xs, len(xt), yt, ys, len(yt),
-                                               buf.ptr, new_h, new_w), self._ctx.handle, "resize_area")
+    def _dev_resize(self, img: _DevImage, key: str, dsize: Optional[Tuple[int, int]] = None, fx: float = 0.0,
+                    fy: float = 0.0, area: bool = False) -> _DevImage:
+        """cv2.resize(img, dsize or None, fx, fy, INTER_AREA if area else INTER_LINEAR) on the device."""
+        p = imageops.resize_plan(img.H, img.W, dsize, fx, fy, area)
+        buf = self._ctx.scratch(key, p["new_w"] * p["new_h"] * 3)
+        self._cv_resize(img, p, buf.ptr)
+        return _DevImage(buf.ptr, p["new_h"], p["new_w"], p["new_w"] * 3, buf)
+
+    def _cv_resize(self, img: _DevImage, p: dict, d_dst: int) -> None:
+        """Run the kernel imageops.resize_plan chose, writing new_h x new_w x 3 contiguous at d_dst."""
+        lib, h = self._ctx.lib, self._ctx.handle
+        nw, nh = p["new_w"], p["new_h"]
+        kind = p["kind"]
+        if kind == "copy":
+            check(lib.pc_copy_2d(h, C.c_void_p(d_dst), nw * 3, C.c_void_p(img.ptr), img.stride, nw * 3, nh), h,
+                  "copy_2d")
+        elif kind == "area_fast":
+            check(lib.pc_resize_area_fast(h, img.ptr, img.stride, p["isx"], p["isy"], d_dst, nh, nw), h,
+                  "resize_area_fast")
+        elif kind == "area":
+            (xt, xs), (yt, ys) = imageops.area_tables(img.W, nw, p["scale_x"]), imageops.area_tables(img.H, nh, p["scale_y"])
+            check(lib.pc_resize_area(h, img.ptr, img.stride, xt, xs, len(xt), yt, ys, len(yt), d_dst, nh, nw), h,
+                  "resize_area")
         else:
             d = ResizeDesc()
             d.d_src, d.H, d.W, d.row_stride = img.ptr, img.H, img.W, img.stride
-            d.new_w, d.new_h, d.scale_x, d.scale_y = new_w, new_h, sx, sy
-            d.simd_end = opencv_vresize_simd_end(new_w * 3)
-            d.d_dst = buf.ptr
-            arr = (ResizeDesc * 1)(d)
-            check(self._ctx.lib.pc_resize_linear(self._ctx.handle, arr, 1), self._ctx.handle, "resize_linear")
-        return _DevImage(buf.ptr, new_h, new_w, new_w * 3, buf)
+            d.new_w, d.new_h, d.scale_x, d.scale_y = nw, nh, p["scale_x"], p["scale_y"]
+            d.inv_x, d.inv_y, d.area_mode = p["inv_x"], p["inv_y"], p["area_mode"]
+            d.simd_end = opencv_vresize_simd_end(nw * 3)
+            d.d_dst = d_dst
+            check(lib.pc_resize_linear(h, (ResizeDesc * 1)(d), 1), h, "resize_linear")
 
     # ------------------------------------------------------------------ static helpers (reference API)
     _ARC_DST = imageops.ARC_DST
@@ -507,8 +519,7 @@ class FaceEmbedder:
                 if s == 1.0:
                     continue
                 try:
-                    nw, nh = int(round(W0 * s)), int(round(H0 * s))
-                    img_s = self._dev_resize(im, nw, nh, area=s < 1.0, key="tta", scale_x=1.0 / s, scale_y=1.0 / s)
+                    img_s = self._dev_resize(im, "tta", fx=s, fy=s, area=s < 1.0)
                     dyn_s = _round32(min(self._heavy_cap, max(320, int(dyn * s))))
                     bb_s, kp_s = self._detect_once(img_s, dyn_s, probe_conf)
                 except Exception:
@@ -752,21 +763,8 @@ class FaceEmbedder:
 
     def _resize_chip(self, crop: _DevImage, d_dst: int) -> None:
         """cv2.resize(face, (112,112), INTER_AREA if max(h,w) > 112 else INTER_LINEAR) (:2458-2460)."""
-        area = max(crop.H, crop.W) > _ARC_SIDE
-        sx, sy = float(crop.W) / _ARC_SIDE, float(crop.H) / _ARC_SIDE
-        if area and sx >= 1.0 and sy >= 1.0:
-            (xt, xs), (yt, ys) = imageops.area_tables(crop.W, _ARC_SIDE), imageops.area_tables(crop.H, _ARC_SIDE)
-            check(self._ctx.lib.pc_resize_area(self._ctx.handle, crop.ptr, crop.stride, xt, xs, len(xt), yt, ys,
-                                               len(yt), d_dst, _ARC_SIDE, _ARC_SIDE), self._ctx.handle, "resize_area")
-        else:
-            d = ResizeDesc()
-            d.d_src, d.H, d.W, d.row_stride = crop.ptr, crop.H, crop.W, crop.stride
-            d.new_w = d.new_h = _ARC_SIDE
-            d.scale_x, d.scale_y = sx, sy
-            d.simd_end = opencv_vresize_simd_end(_ARC_SIDE * 3)
-            d.d_dst = d_dst
-            check(self._ctx.lib.pc_resize_linear(self._ctx.handle, (ResizeDesc * 1)(d), 1), self._ctx.handle,
-                  "resize_linear")
+        p = imageops.resize_plan(crop.H, crop.W, (_ARC_SIDE, _ARC_SIDE), area=max(crop.H, crop.W) > _ARC_SIDE)
+        self._cv_resize(crop, p, d_dst)
 
     def _upright_by_eye_roll(self, im: _DevImage, box, pts5, d_dst: int, warps: list, resize_jobs: list,
                              j: int) -> None:

@@ -18,13 +18,48 @@ ARC_DST = np.array([[38.2946, 51.6963], [73.5318, 51.5014], [56.0252, 71.7366], 
                     [70.7299, 92.2041]], dtype=np.float32)
 BORDER_REFLECT = 2
 BORDER_REFLECT_101 = 4
+_DBL_EPSILON = 2.220446049250313e-16
+
+
+def resize_plan(H: int, W: int, dsize: Optional[Tuple[int, int]] = None, fx: float = 0.0, fy: float = 0.0,
+                area: bool = False) -> dict:
+    """Which cv2.resize kernel OpenCV 4.9 runs for a u8 image (imgproc/src/resize.cpp: cv::resize
+    then hal::resize) and its exact parameters:
+      'copy'       dsize == source size
+      'area_fast'  INTER_AREA (or INTER_LINEAR at exactly 2x2 down) at integer ratios (isx, isy)
+      'area'       INTER_AREA, both axes downscale, generic tables at (scale_x, scale_y)
+      'linear'     bilinear fixed point; area_mode when INTER_AREA was asked but an axis upscales
+    dsize = (new_w, new_h) sets inv_scale = new/old; else new = cvRound(old * f), inv_scale = f.
+    scale = 1 / inv_scale (not old/new: they can differ in the last bit)."""
+    if dsize is None or tuple(dsize) == (0, 0):
+        inv_x, inv_y = float(fx), float(fy)
+        new_w, new_h = int(round(W * inv_x)), int(round(H * inv_y))
+    else:
+        new_w, new_h = int(dsize[0]), int(dsize[1])
+        inv_x, inv_y = float(new_w) / W, float(new_h) / H
+    p = {"new_w": new_w, "new_h": new_h, "inv_x": inv_x, "inv_y": inv_y}
+    if (new_w, new_h) == (W, H):
+        p["kind"] = "copy"
+        return p
+    sx, sy = 1.0 / inv_x, 1.0 / inv_y
+    isx, isy = int(round(sx)), int(round(sy))
+    fast = abs(sx - isx) < _DBL_EPSILON and abs(sy - isy) < _DBL_EPSILON
+    p.update(scale_x=sx, scale_y=sy, isx=isx, isy=isy, area_mode=0)
+    if not area and fast and isx == 2 and isy == 2:
+        area = True
+    if area and sx >= 1 and sy >= 1:
+        p["kind"] = "area_fast" if fast else "area"
+    else:
+        p["kind"] = "linear"
+        p["area_mode"] = 1 if area else 0
+    return p
 
 
 def area_tables(ssize: int, dsize: int, scale: float = None):
     """cv::computeResizeAreaTab (cn = 1) as ctypes arrays + per-destination start offsets.
-    scale defaults to ssize/dsize (explicit dsize); cv2.resize(fx=s) uses 1/s.
+    scale defaults to 1/(dsize/ssize) as hal::resize computes it (explicit dsize); cv2.resize(fx=s) uses 1/s.
     Cached per (ssize, dsize, scale): the pre-scan resizes every frame with one geometry."""
-    scale = float(ssize) / dsize if scale is None else float(scale)
+    scale = 1.0 / (float(dsize) / ssize) if scale is None else float(scale)
     return _area_tables(int(ssize), int(dsize), scale)
 
 

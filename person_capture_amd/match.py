@@ -90,14 +90,23 @@ class DeviceBank:
             self.set(bank)
 
     def set(self, bank: np.ndarray) -> None:
+        """bank: [B][D] unit rows, or one 1-D row (the reference's _fd_min then takes 1 - dot).
+        A 1-D empty bank is rejected: the reference's np.dot((D,), (0,)) raises there."""
         b = np.ascontiguousarray(bank, dtype=np.float32)
         if b.ndim == 1:
+            if b.size == 0:
+                raise ValueError("1-D empty reference bank (shapes not aligned)")
             b = b.reshape(1, -1)
+        if b.ndim != 2:
+            raise ValueError(f"reference bank must be 1-D or 2-D, got shape {b.shape}")
         self.rows, self.dim = b.shape
         self._buf = self.ctx.alloc(max(b.nbytes, 16))
         if b.size:
             self.ctx.upload(b, self._buf)
 
-    def match_device(self, d_feats: int, n: int, d_fd: int, d_idx: int) -> None:
+    def match_device(self, d_feats: int, n: int, d_fd: int, d_idx: int, feat_dim: int = 512) -> None:
+        """fd[i] = Processor._fd_min(feats[i], bank) for n device feature rows of feat_dim f32."""
+        if self.rows and self.dim != feat_dim:
+            raise ValueError(f"bank rows have {self.dim} dims, features {feat_dim} (shapes not aligned)")
         check(self.ctx.lib.pc_bank_match(self.ctx.handle, d_feats, int(n), self._buf.ptr, int(self.rows),
-                                         int(self.dim), d_fd, d_idx), self.ctx.handle, "bank_match")
+                                         int(feat_dim), d_fd, d_idx), self.ctx.handle, "bank_match")

@@ -158,3 +158,59 @@ def test_fallback_paths_run(gpu_ctx):
     fe.set_prescan_fast(True)
     out2 = fe.extract(flat)
     assert isinstance(out2, list)
+
+
+def _pipe_frames():
+    fr = []
+    for i in range(11):
+        if i in (2, 3, 4, 8):
+            # blank and wider than 1920 (no 1.25 TTA scale, face_embedder.py:2252-2254): no face
+            # before the rotation passes, so the no-face streak counts it
+            fr.append(np.zeros((64, 1984, 3), np.uint8))
+        else:
+            fr.append(np.random.default_rng(70 + i).integers(0, 256, (480, 640, 3), dtype=np.uint8))
+    return fr
+
+
+@pytest.mark.parametrize("env", [{"PIPE_CHUNK": "2", "PIPE_AHEAD": "2", "ARC_BATCH": "8"},
+                                 {"PIPE_CHUNK": "32", "PIPE_AHEAD": "2", "ARC_BATCH": "512", "DET_BATCH": "64"}])
+def test_pipelined_batch_equals_sequential(gpu_ctx, monkeypatch, env):
+    """extract_batch's software pipeline (detection chunks queued ahead of the host policy,
+    many ArcFace launches sharing the chips/feats/fd scratch, per-launch pinned readbacks)
+    returns exactly what frame-by-frame extract() on a fresh instance returns. Three blank
+    frames push the no-face streak to 3, so the next frame's det size (512) differs from
+    the speculative one (640) and takes the synchronous re-detect between queued chunks;
+    the blank frames also run the rotation fallback (adaptive gating off, TTA and edge pad
+    off so the streak counts them)."""
+    monkeypatch.setenv("PERSON_CAPTURE_AMD_PRECISION", "f32")
+    for k, v in env.items():
+        monkeypatch.setenv("PERSON_CAPTURE_AMD_" + k, v)
+
+    def make():
+        fe = fe_mod.FaceEmbedder(ctx="cuda:0", yolo_model="scrfd_10g_bnkps", conf=0.5)
+        fe.configure_rotation_strategy(adaptive=False)
+        fe.scrfd_tta_scales = ()
+        fe.scrfd_edge_pad_frac = 0.0
+        return fe
+    frames = _pipe_frames()
+    bank = _bank(6, seed=9)
+    fb = make()
+    got = fb.extract_batch(frames, bank=DeviceBank(fb._ctx, bank))
+    fs = make()
+    streaks = []
+    ref = []
+    for f in frames:
+        ref.append(fs.extract_batch([f], bank=DeviceBank(fs._ctx, bank))[0])
+        streaks.append(fs._no_face_streak)
+    assert max(streaks) >= 3, streaks          # the det-size switch happened
+    assert fb._no_face_streak == fs._no_face_streak and fb._frame_idx == fs._frame_idx
+    assert fb._last_face_idx == fs._last_face_idx
+    n = 0
+    for a_list, b_list in zip(got, ref):
+        assert len(a_list) == len(b_list)
+        for a, b in zip(a_list, b_list):
+            assert np.array_equal(a["bbox"], b["bbox"])
+            assert np.array_equal(a["feat"], b["feat"])
+            assert a["fd"] == b["fd"] and a["quality"] == b["quality"]
+            n += 1
+    assert n >= 10

@@ -131,3 +131,34 @@ def test_resize_area_bit_exact(gpu_ctx, HW, OW):
     got = gpu_ctx.download(out.ptr, (OH, OW, 3), np.uint8)
     ref = cv_ops.resize_area(img, OW, OH)
     assert np.array_equal(got, ref)
+
+
+# (H, W, dsize, fx, area): chip resize fallbacks (face_embedder.py:2458-2460, 1579-1582) with
+# mixed axes (one down, one up -> area-mode linear), exact 2x/3x (resizeAreaFast), same size
+# (copy), pure up/down; TTA rescales by fx (:2264); the pre-scan downscale (gui_app.py:1505-1507)
+_RESIZE_CASES = [
+    (130, 100, (112, 112), 0, True), (100, 130, (112, 112), 0, True), (224, 224, (112, 112), 0, True),
+    (336, 224, (112, 112), 0, True), (336, 336, (112, 112), 0, True), (112, 200, (112, 112), 0, True),
+    (60, 50, (112, 112), 0, False), (113, 90, (112, 112), 0, True), (112, 112, (112, 112), 0, True),
+    (720, 1280, None, 0.75, True), (720, 1280, None, 0.6, True), (480, 640, None, 1.25, False),
+    (360, 640, None, 0.5, False), (2160, 3840, (416, 234), 0, True), (150, 77, (112, 112), 0, False),
+]
+
+
+@pytest.mark.parametrize("H,W,dsize,fx,area", _RESIZE_CASES)
+def test_cv_resize_dispatch_bit_exact(gpu_ctx, H, W, dsize, fx, area):
+    """Every cv2.resize the path makes, through the same OpenCV 4.9 dispatch (copy / area fast /
+    area / linear with area-mode coefficients) as oracle/cv_ops.resize: bit-exact."""
+    from person_capture_amd.face_embedder import FaceEmbedder, _DevImage
+    fe = FaceEmbedder.__new__(FaceEmbedder)
+    fe._ctx = gpu_ctx
+    rng = np.random.default_rng(H * 7 + W)
+    big = _frame(rng, H + 3, W + 5)
+    img = big[1:H + 1, 2:W + 2]                       # a non-contiguous crop, as the callers pass
+    d = gpu_ctx.upload(big)
+    src = _DevImage(d.ptr + 1 * big.strides[0] + 2 * 3, H, W, big.strides[0])
+    out = fe._dev_resize(src, "t_resize", dsize=dsize, fx=fx, fy=fx, area=area)
+    got = gpu_ctx.download(out.ptr, (out.H, out.W, 3), np.uint8)
+    ref = cv_ops.resize(img, dsize, fx, fx, cv_ops.INTER_AREA if area else cv_ops.INTER_LINEAR)
+    assert got.shape == ref.shape
+    assert np.array_equal(got, ref)

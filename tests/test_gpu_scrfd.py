@@ -90,3 +90,29 @@ def test_scrfd_end_to_end_f32(gpu_ctx, s10g):
     a, b = keep(det), keep(det_ref)
     assert a.shape == b.shape and a.shape[0] > 0
     assert np.abs(a - b).max() < 1e-2
+
+
+@pytest.mark.parametrize("D,thresh,max_det", [(1536, 0.1, 64), (1280, 0.02, 4096), (640, 0.0, 16)])
+def test_scrfd_nms_uncapped_bit_exact(gpu_ctx, s10g, D, thresh, max_det):
+    """No candidate cap (the reference keeps every candidate >= det_thresh): at the heavy
+    rotation sizes with low thresholds an image has far more than the 8192 candidates the
+    LDS NMS holds; the global-memory NMS must give the same boxes in the same order, and a
+    kept count above max_det grows the result rows instead of cutting the list."""
+    eng = ScrfdEngine(gpu_ctx, s10g, "10g", D=D, precision=PC_PREC_F16, max_batch=2, max_det=max_det)
+    frames = [_frame(30, 720, 1280), _frame(31, 500, 400)]
+    devs = [gpu_ctx.upload(f) for f in frames]
+    res = eng.detect_frames([(d.ptr, f.shape[0], f.shape[1], f.strides[0]) for d, f in zip(devs, frames)],
+                            thresh=thresh)
+    heads = [eng.net.read_output(l, 2) for l in range(3)]
+    ncand = 0
+    for i, f in enumerate(frames):
+        _, _, det_scale = ra.scrfd_letterbox_geometry(f.shape[0], f.shape[1], D)
+        hs = [h[i, ..., :30] for h in heads]
+        ncand = max(ncand, sum(int((1.0 / (1.0 + np.exp(-h[..., :2].astype(np.float64))) >= thresh).sum())
+                               for h in hs))
+        det_ref, kps_ref = ra.scrfd_detect_post(hs, thresh, det_scale)
+        det, kps = res[i]
+        assert det.shape == det_ref.shape, (det.shape, det_ref.shape)
+        assert np.array_equal(det, det_ref)
+        assert np.array_equal(kps, kps_ref)
+    assert ncand > 8192   # the big path ran

@@ -71,3 +71,18 @@ def test_accumulate0_matches_scalar_policy_step():
         for a, b in zip(got, ref):
             assert a[0] == b[0] and all(type(v) is int for v in a[0])
             assert np.array_equal(a[1], b[1]) and a[2] == b[2]
+
+
+def test_resize_plan_dispatch():
+    """imageops.resize_plan picks OpenCV 4.9's kernel (resize.cpp dispatch)."""
+    from person_capture_amd.imageops import resize_plan
+    assert resize_plan(224, 224, (112, 112), area=True)["kind"] == "area_fast"
+    assert resize_plan(224, 224, (112, 112), area=False)["kind"] == "area_fast"     # LINEAR at exactly 2x2
+    assert resize_plan(336, 336, (112, 112), area=False)["kind"] == "linear"        # LINEAR 3x stays linear
+    p = resize_plan(130, 100, (112, 112), area=True)
+    assert p["kind"] == "linear" and p["area_mode"] == 1
+    assert resize_plan(112, 112, (112, 112), area=True)["kind"] == "copy"
+    p = resize_plan(720, 1280, None, 0.75, 0.75, area=True)
+    assert p["kind"] == "area" and (p["new_w"], p["new_h"]) == (960, 540) and p["scale_x"] == 1 / 0.75
+    # scale is 1/(new/old), which can differ from old/new in the last bit
+    assert resize_plan(130, 130, (112, 112), area=True)["scale_x"] == 1.0 / (112 / 130)
