@@ -87,23 +87,50 @@ def synth_bank(n: int, dim: int = 512) -> np.ndarray:
     return b / np.linalg.norm(b, axis=1, keepdims=True)
 
 
-def cpu_baseline(frames: np.ndarray, fe, bank: np.ndarray, n_sample: int):
-    """The oracle port of the same pipeline on the host cores, bounded sample."""
+def cpu_baseline(frames: np.ndarray, fe, bank: np.ndarray, n_sample: int, n_sample_1t: int):
+    """The oracle port of the same pipeline on the host cores, bounded sample: all-core
+    (16 threads, the box's CPU share) and single-thread (the reference CLI pins torch and
+    OpenCV to one thread, main.py:3-6,14)."""
     import torch
     from oracle import pipeline as op
+
+    def run(threads, n):
+        torch.set_num_threads(threads)
+        t0 = time.perf_counter()
+        faces = 0
+        for i in range(n):
+            r = op.extract_frame(frames[i], fe._scrfd_params, fe.scrfd_variant, fe._arc_params, fe._arc_depth,
+                                 conf=fe.conf, D=640, bank=bank)
+            faces += 0 if r == op.NEEDS_FALLBACK else len(r)
+        return n / (time.perf_counter() - t0), faces, time.perf_counter() - t0
+
     threads = min(16, os.cpu_count() or 1)
+    v, faces, dt = run(threads, n_sample)
+    out = {"value": round(v, 4), "unit": "frames/s", "cores": threads, "kind": "port",
+           "host_cpu_count": os.cpu_count(),
+           "sample": f"{n_sample} of the bench's 1080p frames through oracle/pipeline.extract_frame "
+                     f"(fp32 torch-CPU SCRFD-10G + ArcFace-R100 flip-TTA, numpy/C post), {faces} faces, "
+                     f"{dt:.1f} s at {threads} threads"}
+    if n_sample_1t > 0:
+        v1, faces1, dt1 = run(1, n_sample_1t)
+        out["value_1_thread"] = round(v1, 4)
+        out["sample_1_thread"] = f"first {n_sample_1t} frames, {faces1} faces, {dt1:.1f} s at 1 thread"
     torch.set_num_threads(threads)
-    t0 = time.perf_counter()
-    faces = 0
-    for i in range(n_sample):
-        r = op.extract_frame(frames[i], fe._scrfd_params, fe.scrfd_variant, fe._arc_params, fe._arc_depth,
-                             conf=fe.conf, D=640, bank=bank)
-        faces += 0 if r == op.NEEDS_FALLBACK else len(r)
-    dt = time.perf_counter() - t0
-    return {"value": round(n_sample / dt, 4), "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"{n_sample} of the bench's 1080p frames through oracle/pipeline.extract_frame "
-                      f"(fp32 torch-CPU SCRFD-10G + ArcFace-R100 flip-TTA, numpy/C post), {faces} faces, "
-                      f"{dt:.1f} s"}
+    return out
+
+
+def load_traffic():
+    """HBM bytes per conv launch from the round's rocprofv3 FETCH_SIZE / WRITE_SIZE passes
+    (tools/pmc_traffic.py writes bench_traffic.json at the repo root, next to this file, so
+    it travels to the GPU box)."""
+    tpath = os.path.join(ROOT, "bench_traffic.json")
+    if not os.path.isfile(tpath):
+        return None, None
+    try:
+        t = json.load(open(tpath))
+    except Exception:
+        return None, None
+    return t.get("conv_hbm_bytes_per_launch"), t.get("dominant")
 
 
 def main():
@@ -114,6 +141,7 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--bank", type=int, default=32)
     ap.add_argument("--cpu-sample", type=int, default=48)
+    ap.add_argument("--cpu-sample-1t", type=int, default=4)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--precision", default="f16", choices=["f16", "f32"])
     ap.add_argument("--workload", default="c3", choices=["c3", "c4", "c5"],
@@ -156,10 +184,27 @@ def main():
         res = fe.extract_batch([None] * args.batch, dev_frames=devs, bank=bank)
         return res
 
+    res = step()
+    # plant a quarter of the bank with embeddings of faces the pipeline finds in these frames
+    # (a reference bank is built from the target's own faces, gui_app.py:922-986) so the
+    # accept path runs too; the rest stay random rows. The synthetic (untrained) embedder's
+    # outputs share a large common component, so the planted rows carry 0.3 of the mean
+    # removed plus noise of growing strength (as tests/test_gpu_bench_config.planted_bank):
+    # the distances then straddle the CLI's 0.32 threshold instead of accepting every face.
+    feats = [f["feat"] for r in res for f in r]
+    n_plant = min(len(feats), args.bank // 4)
+    if n_plant:
+        rng = np.random.default_rng(20260504)
+        mean = np.mean(feats, axis=0)
+        for k, i in enumerate(rng.choice(len(feats), n_plant, replace=False)):
+            v = feats[i] - 0.3 * mean + (0.1 + 0.1 * k) * rng.standard_normal(512).astype(np.float32) / np.sqrt(512.0)
+            bank_h[k] = v / np.linalg.norm(v)
+        bank = DeviceBank(ctx, bank_h)
     for _ in range(args.warmup):
         res = step()
     nfaces = sum(len(r) for r in res)
     accept = sum(1 for r in res for f in r if f["fd"] <= 0.45)
+    accept_cli = sum(1 for r in res for f in r if f["fd"] <= 0.32)
     nets = [fe._engine(640).net, fe._arc.net]
     if not os.getenv("PC_BENCH_NOPROF"):
         for n in nets:
@@ -188,13 +233,7 @@ def main():
     value = total_frames / elapsed
     achieved = conv_flops / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
     peak = PEAK_F16_TFLOPS if args.precision == "f16" else PEAK_F32_TFLOPS
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.isfile(tpath):
-        try:
-            traffic = json.load(open(tpath)).get("conv_hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    traffic, dominant = load_traffic()
     out = {
         "metric": "frames/sec detect+embed+match @1080p, 1/2/4/8 GPU; MFMA util %",
         "value": round(value, 3),
@@ -212,17 +251,20 @@ def main():
                                f"{args.bank}-embedding bank, 1080p, batch {args.batch} frames per GPU",
                    "frames_per_step_per_gpu": args.batch, "det_size": 640, "bank": args.bank,
                    "faces_per_frame": round(nfaces / args.batch, 3), "accepted_faces_per_step": accept,
+                   "accepted_faces_per_step_cli_0.32": accept_cli, "bank_planted_rows": n_plant,
                    "parallelism": f"frame-shard x{world} (no collective)"},
         "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": traffic,
                      "kernel": "implicit-GEMM MFMA convs (conv_fast / conv_igemm, SCRFD + ArcFace)",
                      "launches": conv_launches, "avg_launch_us": round(conv_ms * 1e3 / max(1, conv_launches), 2),
                      "flops_per_launch": round(conv_flops / max(1, conv_launches)),
-                     "conv_share_of_step": round(conv_ms * 1e-3 / (t1 - t0), 4)},
+                     "conv_share_of_step": round(conv_ms * 1e-3 / (t1 - t0), 4),
+                     "traffic_unit": "HBM bytes per conv launch (mean over the family, rocprofv3 PMC)",
+                     "dominant_kernel": dominant},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(frames, fe, bank_h, args.cpu_sample)
+        out["cpu_baseline"] = cpu_baseline(frames, fe, bank_h, args.cpu_sample, args.cpu_sample_1t)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

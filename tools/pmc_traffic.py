@@ -1,6 +1,10 @@
 """Reduce rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes to HBM bytes per conv launch.
 
-usage: python tools/pmc_traffic.py <pmc_dir> [<pmc_dir> ...] <out.json>
+usage: python tools/pmc_traffic.py <pmc_dir> [<pmc_dir> ...] <out.json> [--stats kernel_stats.csv]
+
+With --stats (the rocprofv3 --kernel-trace --stats summary of the same command) the
+dominant conv instantiation (largest total time) is reported on its own as well:
+its counter bytes per launch, average duration and the HBM rate they imply.
 
 Corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and WRITE_SIZE are in KiB;
 on gfx950 FETCH_SIZE reports half the bytes of a wide coalesced read (16 B/lane
@@ -32,8 +36,38 @@ def load(dirs):
     return vals
 
 
+def dominant_kernel(stats_csv, per_kernel):
+    best = None
+    with open(stats_csv) as fh:
+        for row in csv.DictReader(fh):
+            name = row.get("Name") or row.get("KernelName") or ""
+            if not any(t in name for t in ("conv_igemm", "conv_fast", "conv_halo")):
+                continue
+            tot = float(row.get("TotalDurationNs", 0) or 0)
+            if best is None or tot > best[1]:
+                best = (name, tot, float(row.get("AverageNs", 0) or 0), int(float(row.get("Calls", 0) or 0)))
+    if best is None:
+        return None
+    name, tot, avg_ns, calls = best
+    k = per_kernel.get(name, {})
+    f = k.get("FETCH_SIZE", (None, 0))[0]
+    w = k.get("WRITE_SIZE", (None, 0))[0]
+    res = {"kernel": name, "calls": calls, "avg_us": round(avg_ns / 1e3, 2), "total_ms": round(tot / 1e6, 3)}
+    if f is not None and w is not None:
+        hb = 2.0 * 1024.0 * f + 1024.0 * w
+        res.update(fetch_bytes_per_launch=2.0 * 1024.0 * f, write_bytes_per_launch=1024.0 * w,
+                   hbm_bytes_per_launch=hb, hbm_gbps=round(hb / avg_ns, 1) if avg_ns else None)
+    return res
+
+
 def main():
-    *dirs, out = sys.argv[1:]
+    args = sys.argv[1:]
+    stats = None
+    if "--stats" in args:
+        i = args.index("--stats")
+        stats = args[i + 1]
+        args = args[:i] + args[i + 2:]
+    *dirs, out = args
     vals = load(dirs)
     per_kernel = {}
     for ctr, kern in vals.items():
@@ -55,6 +89,8 @@ def main():
     }
     if nf and nw:
         res["conv_hbm_bytes_per_launch"] = res["conv_fetch_bytes_per_launch"] + res["conv_write_bytes_per_launch"]
+    if stats:
+        res["dominant"] = dominant_kernel(stats, per_kernel)
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps({k: v for k, v in res.items() if k != "per_kernel"}))
 
