@@ -20,9 +20,11 @@ adaptive rotation gating, cross-rotation NMS, landmark canonicalisation,
 sorting) stays on the host and follows _extract_with_scrfd_raw
 (face_embedder.py:2163-2482) step by step.
 
-Weights: the reference downloads scrfd_*_bnkps.onnx / glintr100.onnx; none exist
-offline, so this build synthesizes seeded weights of the same architectures
-(person_capture_amd/models.py). Backends that are not on this build's hot path
+Weights: scrfd_*_bnkps.onnx and arcface_r100.onnx (glintr100 / w600k_r50) are looked up
+where the reference's _ensure_file looks (plus PERSON_CAPTURE_AMD_MODELS) and mapped by
+onnx_models.py; when they are absent (the reference would download them; there is no
+network here) seeded synthetic weights of the same architectures stand in
+(person_capture_amd/models.py) and `weights_source` says so. Backends that are not on this build's hot path
 (YOLOv8-face detector, OpenCLIP embeddings) raise RuntimeError at construction,
 as the reference does for unavailable backends.
 """
@@ -36,7 +38,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
-from . import imageops, models
+from . import imageops, models, onnx_models
 from ._lib import PC_PREC_F16, PC_PREC_F32, ResizeDesc, WarpDesc, check
 from .engines import ArcFaceEngine, ScrfdEngine, opencv_vresize_simd_end
 from .runtime import GpuContext
@@ -138,11 +140,37 @@ class FaceEmbedder:
         self._scrfd_ctx_id = self._device_index
         seed = int(os.getenv("PERSON_CAPTURE_AMD_SEED", "0"))
         arc_kind = os.getenv("PERSON_CAPTURE_AMD_ARCFACE", "iresnet100")
+        # model files resolved as the reference does (face_embedder.py:598-606, 729-734): the SCRFD
+        # file named by yolo_model (+ ".onnx"), then arcface_r100.onnx (glintr100 / w600k_r50 as
+        # the zip fallback names them); weights mapped by onnx_models. Without the files (there is
+        # no download here) seeded synthetic weights of the same architectures stand in, unless
+        # PERSON_CAPTURE_AMD_REQUIRE_WEIGHTS=1.
+        self.weights_source: Dict[str, str] = {}
+        scrfd_file = model if model.lower().endswith(".onnx") else model + ".onnx"
+        scrfd_path = onnx_models.find_model_file(scrfd_file)
+        arc_path = next((p for p in map(onnx_models.find_model_file,
+                                        (onnx_models.ARCFACE_ONNX,) + onnx_models.ARCFACE_ALT) if p), None)
+        if os.getenv("PERSON_CAPTURE_AMD_REQUIRE_WEIGHTS", "0") == "1" and not (scrfd_path and arc_path):
+            raise RuntimeError(f"model files not found: {scrfd_file if not scrfd_path else ''} "
+                               f"{onnx_models.ARCFACE_ONNX if not arc_path else ''}".strip())
+        try:
+            if scrfd_path:
+                self._scrfd_params, self.scrfd_variant = onnx_models.load_scrfd(scrfd_path)
+                self.weights_source["scrfd"] = scrfd_path
+            else:
+                self._scrfd_params = synthetic_weights(f"scrfd_{self.scrfd_variant}", seed)
+                self.weights_source["scrfd"] = f"synthetic:scrfd_{self.scrfd_variant}:seed{seed}"
+            if arc_path:
+                self._arc_params, self._arc_depth, _ = onnx_models.load_arcface(arc_path)
+                self.weights_source["arcface"] = arc_path
+            else:
+                self._arc_params = synthetic_weights(arc_kind, seed)
+                self._arc_depth = int(arc_kind[len("iresnet"):])
+                self.weights_source["arcface"] = f"synthetic:{arc_kind}:seed{seed}"
+        except (ValueError, KeyError, OSError) as e:
+            raise RuntimeError(f"failed to load face models: {e}") from e
         if callable(progress):
-            progress(f"pcgpu: synthetic weights for scrfd_{self.scrfd_variant} + {arc_kind} (no ONNX files offline)")
-        self._scrfd_params = synthetic_weights(f"scrfd_{self.scrfd_variant}", seed)
-        self._arc_params = synthetic_weights(arc_kind, seed)
-        self._arc_depth = int(arc_kind[len("iresnet"):])
+            progress(f"pcgpu: weights scrfd={self.weights_source['scrfd']} arcface={self.weights_source['arcface']}")
         self._det_batch = int(os.getenv("PERSON_CAPTURE_AMD_DET_BATCH", "8"))
         self._arc_batch = int(os.getenv("PERSON_CAPTURE_AMD_ARC_BATCH", "256"))
         # frames per detection chunk of extract_batch: the host policy of chunk c runs
