@@ -34,6 +34,9 @@
  *   pc_resize_area_fast                cv2.resize(..., INTER_AREA) at integer ratios (face_embedder.py:2460)
  *   pc_yolo_detect                     PersonDetector.detect -> [ext] ultralytics YOLO.predict(conf, iou=0.45,
  *                                      classes=[0], max_det=40, imgsz=640) (detectors.py:271-296)
+ *   pc_yolo_pose_detect                FaceEmbedder YOLOv8-face backend (Y8F_DEFAULT, face_embedder.py:33) ->
+ *                                      [ext] ultralytics YOLO(pose).predict(conf, iou, max_det, imgsz) with
+ *                                      res.boxes + res.keypoints.xy (face_embedder.py:1680-1703, 1391-1429)
  *   pc_clip_prep / pc_clip_embed       ReIDEmbedder.extract: BGR2RGB + open_clip preprocess + encode_image +
  *                                      F.normalize (reid_embedder.py:38-57)
  *   pc_l2_normalize                    torch.nn.functional.normalize(feats, dim=1) (reid_embedder.py:55)
@@ -88,7 +91,7 @@ typedef struct pc_warp_desc {
   double M[6];
   uint8_t* d_dst;
   int32_t out_w, out_h;
-  int32_t border; /* 2 = BORDER_REFLECT, 4 = BORDER_REFLECT_101 */
+  int32_t border; /* 2 = BORDER_REFLECT, 4 = BORDER_REFLECT_101, 0 | (value << 8) = BORDER_CONSTANT */
   int32_t pad1_;
 } pc_warp_desc;
 
@@ -227,6 +230,13 @@ int pc_yolo_letterbox(pc_ctx* ctx, int precision, const pc_yolo_letterbox_desc* 
                       void* d_out);
 int pc_yolo_detect(pc_net* net, const pc_yolo_letterbox_desc* h_descs, int n, int Hp, int Wp, float conf, float iou,
                    const pc_yolo_scale* h_scale, int max_det, float* d_dets, int32_t* d_count, int32_t* d_ncand);
+/* Pose-head variant (YOLOv8-face, nkpt keypoints x (x, y, visibility)): as pc_yolo_detect (all
+ * classes kept, the head's nc = channels - 64 - 3 nkpt), plus d_kpts [n][max_det][nkpt][3] in frame
+ * pixels: Pose.kpts_decode, ops.scale_coords with h_kpt_pad [n][2] = the unrounded letterbox pad
+ * ((Wp - W gain) / 2, (Hp - H gain) / 2), clip, and x = y = 0 where visibility < 0.5. */
+int pc_yolo_pose_detect(pc_net* net, const pc_yolo_letterbox_desc* h_descs, int n, int Hp, int Wp, float conf,
+                        float iou, const pc_yolo_scale* h_scale, const float* h_kpt_pad, int max_det, int nkpt,
+                        float* d_dets, float* d_kpts, int32_t* d_count, int32_t* d_ncand);
 
 /* ---- ReID body embedding (OpenCLIP ViT-L/14 image tower) ---- */
 /* preprocess n crops -> ViT-L/14 patch matrix [n][257][608] (token 0 and K padding zero) */

@@ -187,11 +187,25 @@ void cv_warp_affine_u8(const uint8_t* src, int row_stride, int w, int h, const d
       const int sy = clampi(Y >> INTER_BITS, -32768, 32767);
       int wt[4];
       bilinear_tab(X & 31, Y & 31, wt);
+      uint8_t* o = dst + ((size_t)y * out_w + x) * 3;
+      if ((border & 0xFF) == 0) {   /* BORDER_CONSTANT, value border >> 8: outside taps read the value */
+        const int cv = border >> 8;
+        for (int c = 0; c < 3; ++c) {
+          int t[4];
+          for (int k = 0; k < 4; ++k) {
+            const int xx = sx + (k & 1), yy = sy + (k >> 1);
+            t[k] = ((unsigned)xx < (unsigned)w && (unsigned)yy < (unsigned)h) ? src[(size_t)yy * row_stride + xx * 3 + c]
+                                                                               : cv;
+          }
+          const int v = (t[0] * wt[0] + t[1] * wt[1] + t[2] * wt[2] + t[3] * wt[3] + (1 << 14)) >> 15;
+          o[c] = (uint8_t)clampi(v, 0, 255);
+        }
+        continue;
+      }
       const int x0 = border_interp(sx, w, border), x1 = border_interp(sx + 1, w, border);
       const int y0 = border_interp(sy, h, border), y1 = border_interp(sy + 1, h, border);
       const uint8_t* r0 = src + (size_t)y0 * row_stride;
       const uint8_t* r1 = src + (size_t)y1 * row_stride;
-      uint8_t* o = dst + ((size_t)y * out_w + x) * 3;
       for (int c = 0; c < 3; ++c) {
         int v = r0[x0 * 3 + c] * wt[0] + r0[x1 * 3 + c] * wt[1] + r1[x0 * 3 + c] * wt[2] + r1[x1 * 3 + c] * wt[3];
         v = (v + (1 << 14)) >> 15;

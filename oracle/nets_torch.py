@@ -105,11 +105,13 @@ def scrfd_forward(p, variant, x_nchw: torch.Tensor):
     return res
 
 
-def yolov8_forward(p, scale, x_nchw: torch.Tensor):
+def yolov8_forward(p, scale, x_nchw: torch.Tensor, nc: int = 80, kpt=None):
     """YOLOv8 DetectionModel forward, unfused (Conv2d -> BatchNorm2d(eps 1e-3) -> SiLU), the
     module semantics of [ext] ultralytics 8.3.205 nn/modules (Conv, C2f, Bottleneck, SPPF,
     Concat, nn.Upsample, Detect) that detectors.py:271-296 runs. x: [N,3,H,W] RGB/255.
-    Returns per stride (8,16,32) the raw Detect tensors [N,H,W,64+nc] = cat(cv2, cv3)."""
+    Returns per stride (8,16,32) the raw Detect tensors [N,H,W,64+nc] = cat(cv2, cv3); with
+    kpt = (nkpt, ndim) the Pose head's [N,H,W,64+nc+nkpt*ndim] = cat(cv2, cv3, cv4) (raw
+    keypoints, decoded by ref_algos.yolo_postprocess)."""
     from person_capture_amd.models_yolo import YOLO_BN_EPS, yolo_layers  # layer table only
     T = lambda k: torch.from_numpy(p[k])
 
@@ -122,7 +124,7 @@ def yolov8_forward(p, scale, x_nchw: torch.Tensor):
     with torch.no_grad():
         ys = []
         res = None
-        for L in yolo_layers(scale):
+        for L in yolo_layers(scale, nc, kpt):
             t, nm = L["type"], L["name"]
             xi = ys[L["from"][0]] if L["i"] > 0 else x_nchw
             if t == "Conv":
@@ -149,7 +151,11 @@ def yolov8_forward(p, scale, x_nchw: torch.Tensor):
                     b = F.conv2d(b, T(f"{nm}.cv2.{lvl}.2.weight"), T(f"{nm}.cv2.{lvl}.2.bias"))
                     c = conv(conv(ys[j], f"{nm}.cv3.{lvl}.0", 3), f"{nm}.cv3.{lvl}.1", 3)
                     c = F.conv2d(c, T(f"{nm}.cv3.{lvl}.2.weight"), T(f"{nm}.cv3.{lvl}.2.bias"))
-                    res.append(torch.cat([b, c], 1).permute(0, 2, 3, 1).contiguous())
+                    parts = [b, c]
+                    if L.get("nk"):
+                        k = conv(conv(ys[j], f"{nm}.cv4.{lvl}.0", 3), f"{nm}.cv4.{lvl}.1", 3)
+                        parts.append(F.conv2d(k, T(f"{nm}.cv4.{lvl}.2.weight"), T(f"{nm}.cv4.{lvl}.2.bias")))
+                    res.append(torch.cat(parts, 1).permute(0, 2, 3, 1).contiguous())
                 y = None
             ys.append(y)
     return res

@@ -237,7 +237,7 @@ def align_by_5pts(bgr: np.ndarray, canon5: np.ndarray) -> np.ndarray:
 def rotation_matrix_2d(cx: float, cy: float, angle_deg: float, scale: float) -> np.ndarray:
     """cv2.getRotationMatrix2D(center, angle, scale), double math (center as float32 Point2f)."""
     cx, cy = float(np.float32(cx)), float(np.float32(cy))
-    a = angle_deg * math.pi / 180.0
+    a = angle_deg * (math.pi / 180.0)   # OpenCV: angle *= CV_PI/180
     alpha, beta = math.cos(a) * scale, math.sin(a) * scale
     return np.array([[alpha, beta, (1 - alpha) * cx - beta * cy],
                      [-beta, alpha, beta * cx + (1 - alpha) * cy]], dtype=np.float64)

@@ -318,16 +318,21 @@ def yolo_letterbox(frame: np.ndarray, imgsz: int = 640, stride: int = 32) -> Tup
 
 
 def yolo_postprocess(heads: Sequence[np.ndarray], conf: float, iou: float, max_det: int, Hp: int, Wp: int,
-                     H0: int, W0: int) -> np.ndarray:
+                     H0: int, W0: int, nk: int = 0):
     """Detect inference decode + ops.non_max_suppression(classes=[0]) + ops.scale_boxes for one
-    image. heads: per stride [H][W][64+nc] f32. Returns [k][5] (x1, y1, x2, y2, conf)."""
+    image. heads: per stride [H][W][64+nc(+nk)] f32. Returns [k][5] (x1, y1, x2, y2, conf); with
+    nk > 0 (Pose head, kpt ndim 3) also the keypoints [k][nk/3][3] of the kept boxes:
+    Pose.kpts_decode (x = (raw * 2 + anchor - 0.5) * stride, sigmoid visibility), carried
+    through the NMS, ops.scale_coords (unrounded pad, then /gain, clip) and Results'
+    Keypoints masking (x, y = 0 where visibility < 0.5; [ext] ultralytics 8.3.205
+    engine/results.py)."""
     f32 = np.float32
     cand = []
     aoff = 0
     for hd, s in zip(heads, (8, 16, 32)):
         h, w, _ = hd.shape
         flat = hd.reshape(h * w, -1).astype(f32)
-        cls = flat[:, 64:]
+        cls = flat[:, 64:flat.shape[1] - nk]
         j = np.argmax(cls, axis=1)
         best = cls[np.arange(h * w), j]
         score = (1.0 / (1.0 + np.exp(-best.astype(np.float64)))).astype(f32)   # f64, rounded (as the device)
@@ -350,7 +355,15 @@ def yolo_postprocess(heads: Sequence[np.ndarray], conf: float, iou: float, max_d
             cx, cy = f32(f32(f32(x1 + x2) / f32(2)) * sf), f32(f32(f32(y1 + y2) / f32(2)) * sf)
             bw, bh = f32(f32(x2 - x1) * sf), f32(f32(y2 - y1) * sf)
             hw_, hh_ = f32(bw / f32(2)), f32(bh / f32(2))
-            cand.append((f32(cx - hw_), f32(cy - hh_), f32(cx + hw_), f32(cy + hh_), score[a], aoff + int(a)))
+            kp = None
+            if nk:
+                raw = flat[a, flat.shape[1] - nk:]
+                kp = np.zeros((nk // 3, 3), f32)
+                for q in range(nk // 3):
+                    kp[q, 0] = f32(f32(f32(raw[3 * q] * f32(2.0)) + f32(x)) * sf)
+                    kp[q, 1] = f32(f32(f32(raw[3 * q + 1] * f32(2.0)) + f32(y)) * sf)
+                    kp[q, 2] = f32(1.0 / (1.0 + np.exp(-float(raw[3 * q + 2]))))
+            cand.append((f32(cx - hw_), f32(cy - hh_), f32(cx + hw_), f32(cy + hh_), score[a], aoff + int(a), kp))
         aoff += h * w
     cand.sort(key=lambda c: (-float(c[4]), c[5]))
     kept = []
@@ -382,4 +395,16 @@ def yolo_postprocess(heads: Sequence[np.ndarray], conf: float, iou: float, max_d
         out[r, 2] = min(max(f32(f32(c[2] - f32(px)) / g), f32(0)), f32(W0))
         out[r, 3] = min(max(f32(f32(c[3] - f32(py)) / g), f32(0)), f32(H0))
         out[r, 4] = c[4]
-    return out
+    if not nk:
+        return out
+    kx, ky = f32((Wp - W0 * gain) / 2), f32((Hp - H0 * gain) / 2)   # scale_coords: pad not rounded
+    kpts = np.zeros((len(kept), nk // 3, 3), f32)
+    for r, c in enumerate(kept):
+        for q in range(nk // 3):
+            x = min(max(f32(f32(c[6][q, 0] - kx) / g), f32(0)), f32(W0))
+            y = min(max(f32(f32(c[6][q, 1] - ky) / g), f32(0)), f32(H0))
+            v = c[6][q, 2]
+            if v < f32(0.5):
+                x = y = f32(0)
+            kpts[r, q] = (x, y, v)
+    return out, kpts

@@ -117,6 +117,8 @@ SIGNATURES = {
     "pc_yolo_letterbox": ([_P, _I, C.POINTER(YoloLetterboxDesc), _I, _I, _I, _P], _I),
     "pc_yolo_detect": ([_P, C.POINTER(YoloLetterboxDesc), _I, _I, _I, _F, _F, C.POINTER(YoloScale), _I, _P, _P,
                         _P], _I),
+    "pc_yolo_pose_detect": ([_P, C.POINTER(YoloLetterboxDesc), _I, _I, _I, _F, _F, C.POINTER(YoloScale), _P, _I,
+                             _I, _P, _P, _P, _P], _I),
     "pc_clip_prep": ([_P, _I, C.POINTER(CropDesc), _I, _P], _I),
     "pc_clip_embed": ([_P, C.POINTER(CropDesc), _I, _P], _I),
     "pc_l2_normalize": ([_P, _P, _I, _I, _I, _F, _P], _I),

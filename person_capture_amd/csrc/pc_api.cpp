@@ -91,8 +91,12 @@ struct YoloLevel { const float* out; int H, W, cs, stride; int loc_offset; };
 struct YoloDecodeParams { YoloLevel lv[3]; int nlv, total, nc; float conf; float* cand; int* count; int cap; };
 struct YoloScale;
 hipError_t yolo_decode_launch(const YoloDecodeParams& p, int N, hipStream_t s);
+struct YoloKptScale;
+hipError_t yolo_kpts_launch(const YoloDecodeParams& p, int nk, int koff, int max_det, const int* nkeep,
+                            const int* keep_anchor, const YoloScale* sc, const YoloKptScale* ksc, float* kpts, int N,
+                            hipStream_t s);
 hipError_t yolo_nms_launch(const float* cand, const int* count, int cap, float iou, int max_det, const YoloScale* sc,
-                           float* dets, int* nkeep, int N, hipStream_t s);
+                           float* dets, int* nkeep, int N, hipStream_t s, int* keep_anchor = nullptr);
 // pc_clip.hip
 struct ClipPrepDesc {
   const uint8_t* src; int H, W, row_stride; int kh, kv;
@@ -132,6 +136,8 @@ struct pc_ctx {
   float* ycand = nullptr;
   int* ycount = nullptr;
   size_t ycand_images = 0;
+  int* ykeep = nullptr;        // pose: anchor index of every kept box
+  size_t ykeep_bytes = 0;
   // CLIP preprocessing tables + horizontal-pass scratch
   void* clip_tmp = nullptr;
   size_t clip_tmp_bytes = 0;
@@ -213,6 +219,7 @@ extern "C" int pc_ctx_destroy(pc_ctx* c) {
   if (c->nms_big) hipFree(c->nms_big);
   if (c->det_scale) hipFree(c->det_scale);
   if (c->ycand) hipFree(c->ycand);
+  if (c->ykeep) hipFree(c->ykeep);
   if (c->ycount) hipFree(c->ycount);
   if (c->clip_tmp) hipFree(c->clip_tmp);
   if (c->own_stream) hipStreamDestroy(c->own_stream);
@@ -1226,10 +1233,12 @@ extern "C" int pc_yolo_letterbox(pc_ctx* c, int prec, const pc_yolo_letterbox_de
   return PC_OK;
 }
 
-extern "C" int pc_yolo_detect(pc_net* net, const pc_yolo_letterbox_desc* h, int n, int Hp, int Wp, float conf,
-                              float iou, const pc_yolo_scale* h_scale, int max_det, float* dets, int32_t* count,
-                              int32_t* ncand) {
+static int yolo_detect_impl(pc_net* net, const pc_yolo_letterbox_desc* h, int n, int Hp, int Wp, float conf, float iou,
+                            const pc_yolo_scale* h_scale, int max_det, float* dets, int32_t* count, int32_t* ncand,
+                            int nkpt, const float* h_kpt_pad, float* kpts) {
   if (!net || !h || n <= 0 || !h_scale || max_det <= 0 || !dets || !count) return PC_ERR_ARG;
+  if (nkpt < 0 || (nkpt > 0 && (!h_kpt_pad || !kpts || max_det > 1024))) return PC_ERR_ARG;
+  const int nk = nkpt * 3;
   pc_ctx* c = net->ctx;
   if (n > net->max_batch) return fail(c, PC_ERR_ARG, "pc_yolo_detect: batch exceeds max batch");
   if ((int)net->outs.size() != 3) return fail(c, PC_ERR_FORMAT, "YOLO net must have 3 head outputs");
@@ -1261,7 +1270,7 @@ extern "C" int pc_yolo_detect(pc_net* net, const pc_yolo_letterbox_desc* h, int 
   for (int l = 0; l < 3; ++l) {
     const NetTensor& O = net->tens[net->outs[l]];
     if (!(O.is_f32 || net->f32)) return fail(c, PC_ERR_FORMAT, "YOLO head outputs must be f32");
-    const int ncl = O.C - 64;
+    const int ncl = O.C - 64 - nk;
     if (ncl <= 0 || (nc >= 0 && ncl != nc)) return fail(c, PC_ERR_FORMAT, "YOLO head channel layout");
     nc = ncl;
     p.lv[l].out = (const float*)tensor_ptr(net, net->outs[l]);
@@ -1281,9 +1290,38 @@ extern "C" int pc_yolo_detect(pc_net* net, const pc_yolo_letterbox_desc* h, int 
   if ((rc = stage_copy(c, h_scale, sizeof(pc_yolo_scale) * n, &dsc))) return rc;
   HIPCHK(c, hipMemsetAsync(c->ycount, 0, n * 4, c->stream));
   HIPCHK(c, yolo_decode_launch(p, n, c->stream));
-  HIPCHK(c, yolo_nms_launch(c->ycand, c->ycount, cap, iou, max_det, (const YoloScale*)dsc, dets, count, n, c->stream));
+  int* keep_anchor = nullptr;
+  if (nk) {
+    if (c->ykeep_bytes < (size_t)n * max_det * 4) {
+      if (c->ykeep) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->ykeep)); }
+      HIPCHK(c, hipMalloc((void**)&c->ykeep, (size_t)n * max_det * 4));
+      c->ykeep_bytes = (size_t)n * max_det * 4;
+    }
+    keep_anchor = c->ykeep;
+  }
+  HIPCHK(c, yolo_nms_launch(c->ycand, c->ycount, cap, iou, max_det, (const YoloScale*)dsc, dets, count, n, c->stream,
+                            keep_anchor));
+  if (nk) {
+    void* dks;
+    if ((rc = stage_copy(c, h_kpt_pad, sizeof(float) * 2 * n, &dks))) return rc;
+    HIPCHK(c, yolo_kpts_launch(p, nk, 64 + nc, max_det, count, keep_anchor, (const YoloScale*)dsc,
+                               (const YoloKptScale*)dks, kpts, n, c->stream));
+  }
   if (ncand) HIPCHK(c, hipMemcpyAsync(ncand, c->ycount, n * 4, hipMemcpyDeviceToDevice, c->stream));
   return PC_OK;
+}
+
+extern "C" int pc_yolo_detect(pc_net* net, const pc_yolo_letterbox_desc* h, int n, int Hp, int Wp, float conf,
+                              float iou, const pc_yolo_scale* h_scale, int max_det, float* dets, int32_t* count,
+                              int32_t* ncand) {
+  return yolo_detect_impl(net, h, n, Hp, Wp, conf, iou, h_scale, max_det, dets, count, ncand, 0, nullptr, nullptr);
+}
+
+extern "C" int pc_yolo_pose_detect(pc_net* net, const pc_yolo_letterbox_desc* h, int n, int Hp, int Wp, float conf,
+                                   float iou, const pc_yolo_scale* h_scale, const float* h_kpt_pad, int max_det,
+                                   int nkpt, float* dets, float* kpts, int32_t* count, int32_t* ncand) {
+  if (nkpt <= 0) return fail(net ? net->ctx : nullptr, PC_ERR_ARG, "pc_yolo_pose_detect: nkpt must be positive");
+  return yolo_detect_impl(net, h, n, Hp, Wp, conf, iou, h_scale, max_det, dets, count, ncand, nkpt, h_kpt_pad, kpts);
 }
 
 // ===========================================================================

@@ -164,7 +164,7 @@ struct WarpDesc {
   double M[6];          // dst -> src
   uint8_t* dst;         // out_h x out_w x 3, contiguous
   int out_w, out_h;
-  int border;           // 2 = BORDER_REFLECT, 4 = BORDER_REFLECT_101
+  int border;           // 2 = BORDER_REFLECT, 4 = BORDER_REFLECT_101, 0 | value << 8 = BORDER_CONSTANT
   int pad_;
 };
 
@@ -228,11 +228,27 @@ __global__ void warp_affine_u8(const WarpDesc* __restrict__ descs) {
   sy = sy < -32768 ? -32768 : (sy > 32767 ? 32767 : sy);
   int wt[4];
   bilinear_wtab(X & 31, Y & 31, wt);
+  uint8_t* o = d.dst + (long long)pix * 3;
+  if ((d.border & 0xFF) == 0) {   // BORDER_CONSTANT (value d.border >> 8): taps outside the crop read it
+    const int cv = d.border >> 8;
+    const bool in00 = (unsigned)sx < (unsigned)d.w && (unsigned)sy < (unsigned)d.h;
+    const bool in01 = (unsigned)(sx + 1) < (unsigned)d.w && (unsigned)sy < (unsigned)d.h;
+    const bool in10 = (unsigned)sx < (unsigned)d.w && (unsigned)(sy + 1) < (unsigned)d.h;
+    const bool in11 = (unsigned)(sx + 1) < (unsigned)d.w && (unsigned)(sy + 1) < (unsigned)d.h;
+    const uint8_t* p00 = d.src + (long long)sy * d.row_stride + sx * 3;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const int t0 = in00 ? p00[c] : cv, t1 = in01 ? p00[3 + c] : cv;
+      const int t2 = in10 ? p00[d.row_stride + c] : cv, t3 = in11 ? p00[d.row_stride + 3 + c] : cv;
+      const int v = (t0 * wt[0] + t1 * wt[1] + t2 * wt[2] + t3 * wt[3] + (1 << 14)) >> 15;
+      o[c] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+    }
+    return;
+  }
   const int x0 = border_interp(sx, d.w, d.border), x1 = border_interp(sx + 1, d.w, d.border);
   const int y0 = border_interp(sy, d.h, d.border), y1 = border_interp(sy + 1, d.h, d.border);
   const uint8_t* r0 = d.src + (long long)y0 * d.row_stride;
   const uint8_t* r1 = d.src + (long long)y1 * d.row_stride;
-  uint8_t* o = d.dst + (long long)pix * 3;
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
     int v = r0[x0 * 3 + c] * wt[0] + r0[x1 * 3 + c] * wt[1] + r1[x0 * 3 + c] * wt[2] + r1[x1 * 3 + c] * wt[3];

@@ -155,7 +155,8 @@ struct YoloScale { float gain; float padx, pady; float W0, H0; };
 
 __global__ __launch_bounds__(1024) void yolo_nms(const float* __restrict__ cand, const int* __restrict__ count, int cap,
                                                  float iou, int max_det, const YoloScale* __restrict__ sc,
-                                                 float* __restrict__ dets, int* __restrict__ nkeep) {
+                                                 float* __restrict__ dets, int* __restrict__ nkeep,
+                                                 int* __restrict__ keep_anchor) {
   __shared__ unsigned long long keys[YNMS_CAP];
   __shared__ unsigned supp[YNMS_CAP / 32];
   __shared__ int s_next;
@@ -204,6 +205,7 @@ __global__ __launch_bounds__(1024) void yolo_nms(const float* __restrict__ cand,
       d[2] = fminf(fmaxf((x2 - S.padx) / S.gain, 0.f), S.W0);
       d[3] = fminf(fmaxf((y2 - S.pady) / S.gain, 0.f), S.H0);
       d[4] = bi[4];
+      if (keep_anchor) keep_anchor[(long long)n * max_det + kept] = __float_as_int(bi[5]);
     }
     ++kept;
     for (int j = cur + 1 + tid; j < K; j += blockDim.x) {
@@ -230,6 +232,51 @@ __global__ __launch_bounds__(1024) void yolo_nms(const float* __restrict__ cand,
   if (tid == 0) nkeep[n] = kept;
 }
 
+// Pose head keypoints of the kept boxes (ultralytics Pose.kpts_decode, ndim 3): x = (raw * 2 +
+// anchor_x - 0.5) * stride with anchor_x - 0.5 = grid x exactly, visibility = sigmoid (f64,
+// rounded, as the scores), then ops.scale_coords (the unrounded letterbox pad, / gain, clip to
+// the frame) and Results' Keypoints masking (x = y = 0 where visibility < 0.5).
+struct YoloKptScale { float kpadx, kpady; };
+
+__global__ void yolo_kpts(YoloDecodeParams p, int nk, int koff, int max_det, const int* __restrict__ nkeep,
+                          const int* __restrict__ keep_anchor, const YoloScale* __restrict__ sc,
+                          const YoloKptScale* __restrict__ ksc, float* __restrict__ kpts) {
+  const int n = blockIdx.x;
+  const int k = threadIdx.x;
+  if (k >= nkeep[n]) return;
+  const int a = keep_anchor[(long long)n * max_det + k];
+  int l = 0;
+  while (l + 1 < p.nlv && a >= p.lv[l + 1].loc_offset) ++l;
+  const YoloLevel L = p.lv[l];
+  const int r = a - L.loc_offset;
+  const int y = r / L.W, x = r - (r / L.W) * L.W;
+  const float* raw = L.out + ((long long)n * L.H * L.W + r) * L.cs + koff;
+  const YoloScale S = sc[n];
+  const YoloKptScale K = ksc[n];
+  const float sf = (float)L.stride;
+  float* o = kpts + ((long long)n * max_det + k) * nk;
+  for (int q = 0; q < nk / 3; ++q) {
+    const float px = (raw[3 * q] * 2.0f + (float)x) * sf;
+    const float py = (raw[3 * q + 1] * 2.0f + (float)y) * sf;
+    const float v = (float)(1.0 / (1.0 + exp(-(double)raw[3 * q + 2])));
+    float ox = fminf(fmaxf((px - K.kpadx) / S.gain, 0.f), S.W0);
+    float oy = fminf(fmaxf((py - K.kpady) / S.gain, 0.f), S.H0);
+    if (v < 0.5f) { ox = 0.f; oy = 0.f; }
+    o[3 * q] = ox;
+    o[3 * q + 1] = oy;
+    o[3 * q + 2] = v;
+  }
+}
+
+hipError_t yolo_kpts_launch(const YoloDecodeParams& p, int nk, int koff, int max_det, const int* nkeep,
+                            const int* keep_anchor, const YoloScale* sc, const YoloKptScale* ksc, float* kpts, int N,
+                            hipStream_t s) {
+  if (max_det > 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(yolo_kpts, dim3(N), dim3((max_det + 63) / 64 * 64), 0, s, p, nk, koff, max_det, nkeep,
+                     keep_anchor, sc, ksc, kpts);
+  return hipGetLastError();
+}
+
 hipError_t yolo_letterbox_launch(int f32, const YoloLetterboxDesc* d_descs, int N, int Hp, int Wp, void* out,
                                  hipStream_t s) {
   dim3 grid((Hp * Wp + 255) / 256, N);
@@ -245,9 +292,10 @@ hipError_t yolo_decode_launch(const YoloDecodeParams& p, int N, hipStream_t s) {
 }
 
 hipError_t yolo_nms_launch(const float* cand, const int* count, int cap, float iou, int max_det, const YoloScale* sc,
-                           float* dets, int* nkeep, int N, hipStream_t s) {
+                           float* dets, int* nkeep, int N, hipStream_t s, int* keep_anchor) {
   if (cap > YNMS_CAP) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(yolo_nms, dim3(N), dim3(1024), 0, s, cand, count, cap, iou, max_det, sc, dets, nkeep);
+  hipLaunchKernelGGL(yolo_nms, dim3(N), dim3(1024), 0, s, cand, count, cap, iou, max_det, sc, dets, nkeep,
+                     keep_anchor);
   return hipGetLastError();
 }
 

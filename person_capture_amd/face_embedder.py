@@ -41,6 +41,7 @@ import numpy as np
 from . import imageops, models, onnx_models
 from ._lib import PC_PREC_F16, PC_PREC_F32, ResizeDesc, WarpDesc, check
 from .engines import ArcFaceEngine, ScrfdEngine, opencv_vresize_simd_end
+from .face_yolo import YoloFaceBranch
 from .runtime import GpuContext
 
 Y8F_DEFAULT = "yolov8l-face.pt"   # reference default (face_embedder.py:33)
@@ -103,8 +104,8 @@ class _DevImage:
         self.ptr, self.H, self.W, self.stride, self._buf = int(ptr), int(H), int(W), int(stride), buf
 
 
-class FaceEmbedder:
-    """Face detection (SCRFD) + ArcFace identity embedding on the MI355X.
+class FaceEmbedder(YoloFaceBranch):
+    """Face detection (SCRFD, or the YOLOv8-face default) + ArcFace identity embedding on the MI355X.
     Returns list of dicts: {'bbox': np.int32[x1,y1,x2,y2], 'feat': np.float32[D], 'quality': float}."""
 
     def __init__(self, ctx: str = 'cuda', yolo_model: str = Y8F_DEFAULT, conf: float = 0.30,
@@ -119,13 +120,11 @@ class FaceEmbedder:
         override = os.getenv("PERSON_CAPTURE_AMD_FACE_MODEL", "").strip()
         if not model.lower().startswith("scrfd") and override:
             model = override
-        if not os.path.basename(model).lower().startswith("scrfd"):
-            raise RuntimeError(
-                f"Face detector backend '{yolo_model}' (YOLOv8-face) is not part of this MI355X build; pass "
-                f"yolo_model='scrfd_10g_bnkps' (or set PERSON_CAPTURE_AMD_FACE_MODEL=scrfd_10g_bnkps).")
         if not use_arcface:
             raise RuntimeError("OpenCLIP face embeddings are not part of this MI355X build; use_arcface=True.")
-        self.detector_backend = "scrfd"
+        # backend choice as the reference (face_embedder.py:383-420, 500-520): names starting with
+        # "scrfd" select SCRFD, anything else is a YOLOv8-face checkpoint name
+        self.detector_backend = "scrfd" if os.path.basename(model).lower().startswith("scrfd") else "yolo"
         base = os.path.basename(model).lower().replace(".onnx", "").replace("_trt", "")
         self.scrfd_variant = "2.5g" if "2.5g" in base else "10g"
         self._scrfd_model_path = model
@@ -147,14 +146,18 @@ class FaceEmbedder:
         # PERSON_CAPTURE_AMD_REQUIRE_WEIGHTS=1.
         self.weights_source: Dict[str, str] = {}
         scrfd_file = model if model.lower().endswith(".onnx") else model + ".onnx"
-        scrfd_path = onnx_models.find_model_file(scrfd_file)
+        scrfd_path = onnx_models.find_model_file(scrfd_file) if self.detector_backend == "scrfd" else None
         arc_path = next((p for p in map(onnx_models.find_model_file,
                                         (onnx_models.ARCFACE_ONNX,) + onnx_models.ARCFACE_ALT) if p), None)
-        if os.getenv("PERSON_CAPTURE_AMD_REQUIRE_WEIGHTS", "0") == "1" and not (scrfd_path and arc_path):
+        if os.getenv("PERSON_CAPTURE_AMD_REQUIRE_WEIGHTS", "0") == "1" and not (
+                (scrfd_path or self.detector_backend != "scrfd") and arc_path):
             raise RuntimeError(f"model files not found: {scrfd_file if not scrfd_path else ''} "
                                f"{onnx_models.ARCFACE_ONNX if not arc_path else ''}".strip())
         try:
-            if scrfd_path:
+            if self.detector_backend == "yolo":
+                self._init_yolo_face(model or Y8F_DEFAULT, seed)
+                self._scrfd_params = None
+            elif scrfd_path:
                 self._scrfd_params, self.scrfd_variant = onnx_models.load_scrfd(scrfd_path)
                 self.weights_source["scrfd"] = scrfd_path
             else:
@@ -170,7 +173,7 @@ class FaceEmbedder:
         except (ValueError, KeyError, OSError) as e:
             raise RuntimeError(f"failed to load face models: {e}") from e
         if callable(progress):
-            progress(f"pcgpu: weights scrfd={self.weights_source['scrfd']} arcface={self.weights_source['arcface']}")
+            progress("pcgpu: weights " + " ".join(f"{k}={v}" for k, v in self.weights_source.items()))
         self._det_batch = int(os.getenv("PERSON_CAPTURE_AMD_DET_BATCH", "8"))
         self._arc_batch = int(os.getenv("PERSON_CAPTURE_AMD_ARC_BATCH", "256"))
         # frames per detection chunk of extract_batch: the host policy of chunk c runs
@@ -211,9 +214,16 @@ class FaceEmbedder:
         self.rot_after_hit_frames = 8
         self.fast_no_face_imgsz = 512
         self._scrfd_fixed_shape = (640, 640)
-        self.scrfd = self._engine(640)
-        if callable(progress):
-            progress(f"SCRFD(pcgpu) ready on cuda:{self._device_index} det=(640, 640)")
+        if self.detector_backend == "scrfd":
+            self.scrfd = self._engine(640)
+            if callable(progress):
+                progress(f"SCRFD(pcgpu) ready on cuda:{self._device_index} det=(640, 640)")
+        else:
+            self.scrfd = None
+            self.det = f"pcgpu-yolov8{self.yolo_scale}-face"
+            self.backend = "arcface"
+            if callable(progress):
+                progress(f"YOLOv8-face(pcgpu) ready on cuda:{self._device_index}")
 
     # ------------------------------------------------------------------ knobs
     def set_prescan_fast(self, enable: bool, *, mode: str = "rr") -> None:
@@ -365,6 +375,13 @@ class FaceEmbedder:
         'fd' = Processor._fd_min(feat, bank), computed on the device."""
         self._bank = bank
         n = len(frames) if dev_frames is None else len(dev_frames)
+        if self.detector_backend == "yolo":   # face_embedder.py:1671-2093, frame by frame
+            out_y: List[list] = []
+            for i in range(n):
+                im = dev_frames[i] if dev_frames is not None else (
+                    None if frames[i] is None or frames[i].size == 0 else self._upload(frames[i], key="yf_frame"))
+                out_y.append([] if im is None else self._extract_with_yolo(im, imgsz))
+            return out_y
         imgs: List[Optional[_DevImage]] = []
         for i in range(n):
             if dev_frames is not None:

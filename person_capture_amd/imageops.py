@@ -18,6 +18,13 @@ ARC_DST = np.array([[38.2946, 51.6963], [73.5318, 51.5014], [56.0252, 71.7366], 
                     [70.7299, 92.2041]], dtype=np.float32)
 BORDER_REFLECT = 2
 BORDER_REFLECT_101 = 4
+
+
+def border_constant(value: int) -> int:
+    """cv2.BORDER_CONSTANT with a gray borderValue (value, value, value) in the warp descriptor."""
+    return (int(value) & 0xFF) << 8
+
+
 _DBL_EPSILON = 2.220446049250313e-16
 
 

@@ -66,8 +66,10 @@ def yolo_scale_of(model_name: str) -> str:
     return "n"
 
 
-def yolo_layers(scale: str = "n", nc: int = YOLO_NC) -> List[dict]:
-    """Resolved layer table: type, inputs (absolute indices), channels, repeats."""
+def yolo_layers(scale: str = "n", nc: int = YOLO_NC, kpt: Optional[Tuple[int, int]] = None) -> List[dict]:
+    """Resolved layer table: type, inputs (absolute indices), channels, repeats. kpt = (nkpt, ndim)
+    turns the Detect head into ultralytics' Pose head (yolov8-pose.yaml, the YOLOv8-face models:
+    kpt_shape [5, 3]) with its cv4 keypoint branch of width c4 = max(ch[0] // 4, nkpt * ndim)."""
     depth, width, maxc = YOLO_SCALES[scale]
     div8 = lambda x: int(math.ceil(x / 8) * 8)
     out: List[dict] = []
@@ -95,7 +97,10 @@ def yolo_layers(scale: str = "n", nc: int = YOLO_NC) -> List[dict]:
             chs = [ch[j] for j in frm]
             c2b = max(16, chs[0] // 4, REG_MAX * 4)
             c3 = max(chs[0], min(nc, 100))
-            L.update(ch=chs, c2b=c2b, c3=c3, nc=nc)
+            L.update(ch=chs, c2b=c2b, c3=c3, nc=nc, nk=0)
+            if kpt is not None:
+                nk = kpt[0] * kpt[1]
+                L.update(type="Pose", nk=nk, kpt=tuple(kpt), c4=max(chs[0] // 4, nk))
             c2 = 0
         L["cout"] = c2
         out.append(L)
@@ -119,11 +124,20 @@ def _conv_init(rng, p: Params, name: str, c1: int, c2: int, k: int) -> None:
     p[name + ".bn.running_var"] = np.ones(c2, np.float32)
 
 
-def synth_yolov8(scale: str = "n", seed: int = 0, calibrate: bool = True, target_per_image=(1.5, 0.8, 0.4)) -> Params:
-    """Seeded YOLOv8 weights (state-dict names of ultralytics' DetectionModel)."""
-    rng = np.random.default_rng(np.random.SeedSequence([20260503, ord(scale), seed]))
+# YOLOv8-face synthetic priors: a box ~2 strides wide and ~2.5 tall around the anchor and the
+# 5 landmarks (eyes, nose, mouth corners) in strides from the anchor centre; the Pose head
+# decodes x = (raw * 2 + anchor_x - 0.5) * stride, so raw = (offset + 0.5) / 2
+FACE_BOX_PRIOR = (2.0, 2.5, 2.0, 2.5)
+FACE_KPT_PRIOR = ((-0.7, -0.5), (0.7, -0.5), (0.0, 0.2), (-0.5, 0.9), (0.5, 0.9))
+
+
+def synth_yolov8(scale: str = "n", seed: int = 0, calibrate: bool = True, target_per_image=(1.5, 0.8, 0.4),
+                 nc: int = YOLO_NC, kpt: Optional[Tuple[int, int]] = None,
+                 box_prior=(2.5, 4.5, 2.5, 4.5)) -> Params:
+    """Seeded YOLOv8 weights (state-dict names of ultralytics' DetectionModel / PoseModel)."""
+    rng = np.random.default_rng(np.random.SeedSequence([20260503, ord(scale), seed] + ([nc, 7] if kpt else [])))
     p: Params = {}
-    for L in yolo_layers(scale):
+    for L in yolo_layers(scale, nc, kpt):
         nm, t = L["name"], L["type"]
         if t == "Conv":
             _conv_init(rng, p, nm, L["c1"], L["c2"], L["k"])
@@ -138,7 +152,7 @@ def synth_yolov8(scale: str = "n", seed: int = 0, calibrate: bool = True, target
             c_ = L["c1"] // 2
             _conv_init(rng, p, nm + ".cv1", L["c1"], c_, 1)
             _conv_init(rng, p, nm + ".cv2", 4 * c_, L["c2"], 1)
-        elif t == "Detect":
+        elif t in ("Detect", "Pose"):
             for lvl, x in enumerate(L["ch"]):
                 _conv_init(rng, p, f"{nm}.cv2.{lvl}.0", x, L["c2b"], 3)
                 _conv_init(rng, p, f"{nm}.cv2.{lvl}.1", L["c2b"], L["c2b"], 3)
@@ -146,7 +160,7 @@ def synth_yolov8(scale: str = "n", seed: int = 0, calibrate: bool = True, target
                 # DFL prior: bins peaked near 2-3 strides sideways, 4-6 strides up/down (upright people)
                 bins = np.arange(REG_MAX, dtype=np.float64)
                 prior = []
-                for mu in (2.5, 4.5, 2.5, 4.5):
+                for mu in box_prior:
                     prior.append(-0.5 * ((bins - mu) / 1.2) ** 2)
                 p[f"{nm}.cv2.{lvl}.2.bias"] = np.concatenate(prior).astype(np.float32)
                 _conv_init(rng, p, f"{nm}.cv3.{lvl}.0", x, L["c3"], 3)
@@ -155,11 +169,30 @@ def synth_yolov8(scale: str = "n", seed: int = 0, calibrate: bool = True, target
                 b = np.full(L["nc"], -12.0, np.float32)
                 b[0] = -4.0
                 p[f"{nm}.cv3.{lvl}.2.bias"] = b
+                if t == "Pose":
+                    _conv_init(rng, p, f"{nm}.cv4.{lvl}.0", x, L["c4"], 3)
+                    _conv_init(rng, p, f"{nm}.cv4.{lvl}.1", L["c4"], L["c4"], 3)
+                    p[f"{nm}.cv4.{lvl}.2.weight"] = _he(rng, (L["nk"], L["c4"], 1, 1), 0.05)
+                    nkp, nd = L["kpt"]
+                    kb = np.zeros((nkp, nd), np.float32)
+                    for k in range(nkp):
+                        dx, dy = FACE_KPT_PRIOR[k % len(FACE_KPT_PRIOR)]
+                        kb[k, 0], kb[k, 1] = (dx + 0.5) / 2.0, (dy + 0.5) / 2.0
+                        if nd == 3:
+                            kb[k, 2] = 3.0   # visible (sigmoid 0.95)
+                    p[f"{nm}.cv4.{lvl}.2.bias"] = kb.reshape(-1)
             p[nm + ".dfl.conv.weight"] = np.arange(REG_MAX, dtype=np.float32).reshape(1, REG_MAX, 1, 1)
     if calibrate:
         from .synth_calib import calibrate_yolo
-        calibrate_yolo(p, scale, rng, target_per_image)
+        calibrate_yolo(p, scale, rng, target_per_image, nc=nc, kpt=kpt)
     return p
+
+
+def synth_yolov8_face(scale: str = "l", seed: int = 0, calibrate: bool = True) -> Params:
+    """Seeded YOLOv8-face weights (the reference default Y8F_DEFAULT = yolov8l-face.pt,
+    face_embedder.py:33: a PoseModel, one class, kpt_shape [5, 3])."""
+    return synth_yolov8(scale, seed, calibrate, target_per_image=(2.0, 1.0, 0.5), nc=1, kpt=(5, 3),
+                        box_prior=FACE_BOX_PRIOR)
 
 
 # ---------------------------------------------------------------------------
@@ -226,11 +259,13 @@ def _conv(P: Program, p: Params, x: _T, name: str, c2: int, k: int, s: int, out:
            res_mode=RES_SAME, act_after_res=0, flops_cout=c2)
 
 
-def compile_yolov8(p: Params, scale: str = "n", Hp: int = 384, Wp: int = 640) -> Program:
+def compile_yolov8(p: Params, scale: str = "n", Hp: int = 384, Wp: int = 640, nc: int = YOLO_NC,
+                   kpt: Optional[Tuple[int, int]] = None) -> Program:
     """YOLOv8 -> program for an Hp x Wp letterboxed canvas (NHWC4: RGB/255, channel 3 = 0).
-    Outputs per stride 8/16/32: f32 [H][W][64 + nc] (DFL logits | class logits)."""
+    Outputs per stride 8/16/32: f32 [H][W][64 + nc (+ nk)] (DFL logits | class logits | raw
+    keypoints of the Pose head)."""
     assert Hp % 32 == 0 and Wp % 32 == 0
-    layers = yolo_layers(scale)
+    layers = yolo_layers(scale, nc, kpt)
     P = Program()
     xin = P.input_tensor(Hp, Wp, 4)
     # spatial size of every layer output
@@ -310,37 +345,42 @@ def compile_yolov8(p: Params, scale: str = "n", Hp: int = 384, Wp: int = 640) ->
         elif t == "Upsample":
             y = out_tensor(i)
             P.upsample2(y.t, x.t)
-        elif t == "Detect":
+        elif t in ("Detect", "Pose"):
             c2b, c3, nc = L["c2b"], L["c3"], L["nc"]
-            bp, cp3 = cpad(c2b), cpad(c3)
+            nk, c4 = L["nk"], L.get("c4", 0)
+            bp, cp3, cp4 = cpad(c2b), cpad(c3), (cpad(c4) if nk else 0)
             for lvl, j in enumerate(L["from"]):
                 xi = outs[j]
                 Hl, Wl = hw[j]
-                # cv2[l][0] and cv3[l][0] read the same input: one launch, rows [box | cls]
-                h1 = P.act(Hl, Wl, bp + cp3)
-                sb, bb = bn_fold_eps(p, f"{nm}.cv2.{lvl}.0.bn")
-                sc_, bc = bn_fold_eps(p, f"{nm}.cv3.{lvl}.0.bn")
-                wb = p[f"{nm}.cv2.{lvl}.0.conv.weight"].astype(np.float64) * sb[:, None, None, None]
-                wc = p[f"{nm}.cv3.{lvl}.0.conv.weight"].astype(np.float64) * sc_[:, None, None, None]
-                rows = np.concatenate([np.arange(c2b), bp + np.arange(c3)])
+                # cv2[l][0], cv3[l][0] (and cv4[l][0]) read the same input: one launch, rows [box | cls | kpt]
+                branches = [("cv2", c2b, 0), ("cv3", c3, bp)] + ([("cv4", c4, bp + cp3)] if nk else [])
+                h1 = P.act(Hl, Wl, bp + cp3 + cp4)
+                ws, bs, rows = [], [], []
+                for br, cw, off in branches:
+                    sb, bb = bn_fold_eps(p, f"{nm}.{br}.{lvl}.0.bn")
+                    ws.append(p[f"{nm}.{br}.{lvl}.0.conv.weight"].astype(np.float64) * sb[:, None, None, None])
+                    bs.append(bb)
+                    rows.append(off + np.arange(cw))
+                rows = np.concatenate(rows)
                 _, _, cin_pad = P.dims(xi.t)
-                wp = pack_mapped(np.concatenate([wb, wc], axis=0), xi.cmap, cin_pad, bp + cp3, rows)
-                bias = np.zeros(bp + cp3)
-                bias[rows] = np.concatenate([bb, bc])
-                P.conv(h1, [(xi.t, 3, 3, 1, 1, xi.ctrue)], wp, bp + cp3, bias=bias, act=ACT_SILU,
-                       flops_cout=c2b + c3)
-                hb = _T(P.view(h1, 0, bp), [(0, c2b)])
-                hc = _T(P.view(h1, bp, cp3), [(0, c3)])
-                b2 = _T(P.act(Hl, Wl, bp), [(0, c2b)])
-                _conv(P, p, hb, f"{nm}.cv2.{lvl}.1", c2b, 3, 1, b2.t)
-                c2t = _T(P.act(Hl, Wl, cp3), [(0, c3)])
-                _conv(P, p, hc, f"{nm}.cv3.{lvl}.1", c3, 3, 1, c2t.t)
-                o = P.act(Hl, Wl, cpad(4 * REG_MAX + nc), is_f32=1)
-                _conv(P, p, b2, f"{nm}.cv2.{lvl}.2", 4 * REG_MAX, 1, 1, P.view(o, 0, 4 * REG_MAX), act=ACT_NONE,
-                      plain=True)
-                _conv(P, p, c2t, f"{nm}.cv3.{lvl}.2", nc, 1, 1, P.view(o, 4 * REG_MAX, cpad(4 * REG_MAX + nc) - 64),
-                      act=ACT_NONE, plain=True)
-                heads.append(P.view(o, 0, 4 * REG_MAX + nc))
+                wp = pack_mapped(np.concatenate(ws, axis=0), xi.cmap, cin_pad, bp + cp3 + cp4, rows)
+                bias = np.zeros(bp + cp3 + cp4)
+                bias[rows] = np.concatenate(bs)
+                P.conv(h1, [(xi.t, 3, 3, 1, 1, xi.ctrue)], wp, bp + cp3 + cp4, bias=bias, act=ACT_SILU,
+                       flops_cout=c2b + c3 + (c4 if nk else 0))
+                ctot = 4 * REG_MAX + nc + nk
+                o = P.act(Hl, Wl, cpad(ctot), is_f32=1)
+                # second conv of each branch, then its plain 1x1 into the output slice
+                offs = [0, 4 * REG_MAX, 4 * REG_MAX + nc]
+                outs_c = [4 * REG_MAX, nc, nk]
+                for (br, cw, off), oo, oc in zip(branches, offs, outs_c):
+                    cwp = cpad(cw)
+                    hin = _T(P.view(h1, off, cwp), [(0, cw)])
+                    h2 = _T(P.act(Hl, Wl, cwp), [(0, cw)])
+                    _conv(P, p, hin, f"{nm}.{br}.{lvl}.1", cw, 3, 1, h2.t)
+                    width = cpad(ctot) - oo if br != "cv2" else 4 * REG_MAX
+                    _conv(P, p, h2, f"{nm}.{br}.{lvl}.2", oc, 1, 1, P.view(o, oo, width), act=ACT_NONE, plain=True)
+                heads.append(P.view(o, 0, ctot))
             continue
         outs[i] = y
     P.outputs = heads

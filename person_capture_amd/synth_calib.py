@@ -112,7 +112,7 @@ def calibrate_scrfd(p, variant, rng, target_per_image, D=640, n=2):
             p[f"bbox_head.{s}.cls.bias"] = np.full(logits.shape[1], -thr, np.float32)
 
 
-def calibrate_yolo(p, scale, rng, target_per_image, Hp=384, Wp=640, n=2):
+def calibrate_yolo(p, scale, rng, target_per_image, Hp=384, Wp=640, n=2, nc=80, kpt=None):
     """YOLOv8: BN statistics from synthetic letterboxed 1080p-like canvases (noise in the
     middle rows, 114 padding top/bottom, as LetterBox leaves it), then the class-0 logit
     bias per level so ~target_per_image anchors per canvas pass score 0.5."""
@@ -141,7 +141,7 @@ def calibrate_yolo(p, scale, rng, target_per_image, Hp=384, Wp=640, n=2):
     with torch.no_grad():
         x = torch.from_numpy(img[..., ::-1].astype(np.float32) / 255.0).permute(0, 3, 1, 2).contiguous()
         ys = []
-        for L in yolo_layers(scale):
+        for L in yolo_layers(scale, nc, kpt):
             t, nm = L["type"], L["name"]
             xi = ys[L["from"][0]] if L["i"] > 0 else x
             if t == "Conv":
@@ -175,5 +175,7 @@ def calibrate_yolo(p, scale, rng, target_per_image, Hp=384, Wp=640, n=2):
                     # persons per frame after NMS, not the 40-box cap
                     p[f"{nm}.cv3.{lvl}.2.bias"][0] = np.float32(-thr - 0.6190392 - 2.0)
                     conv(conv(ys[j], f"{nm}.cv2.{lvl}.0", 3), f"{nm}.cv2.{lvl}.1", 3)
+                    if L.get("nk"):
+                        conv(conv(ys[j], f"{nm}.cv4.{lvl}.0", 3), f"{nm}.cv4.{lvl}.1", 3)
                 y = None
             ys.append(y)

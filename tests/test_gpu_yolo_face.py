@@ -1,0 +1,124 @@
+"""YOLOv8-face backend (the reference default Y8F_DEFAULT = 'yolov8l-face.pt',
+face_embedder.py:33) against the CPU oracle oracle/yolo_face.py, f32 parity mode.
+
+The synthetic (untrained) Pose model scores every anchor within a narrow logit band, so the
+sequences lower the class bias by DELTA and run at conf 0.05 (the TTA / rotation passes use
+min(conf, 0.10)): at -1.5 some frames hit at 0 degrees with landmarks (aligned chips) and
+others only through the 1.25x TTA pass, whose faces carry no landmarks of the original
+predict and go through _redetect_align_on_rotations (crop rotations 90/270/180, centre- and
+confidence-weighted pick) or the resize fallback; at -2.1 the 1.5x TTA pass, the
+full-frame rotations with probe + heavy 1280/1536 passes and the +-45 / +-135 affine
+rotations (114 border) are reached. Branches reached are read from the oracle's trace and
+asserted. Per frame: identical int boxes; chips byte-identical, or (landmarks a few f32 bits
+apart) the oracle embedding of the device chip within 1e-4 of the device feature; quality
+of the device chip within 1e-9 rel.
+"""
+import numpy as np
+import pytest
+
+from oracle import cv_ops
+from oracle import nets_torch as nt
+from oracle import ref_algos as ra
+from oracle import yolo_face as oy
+from person_capture_amd import face_embedder as fe_mod
+from person_capture_amd import models_yolo as my
+
+pytestmark = pytest.mark.gpu
+H, W = 240, 320
+
+
+def _frames(seeds):
+    return [np.random.default_rng(s).integers(0, 256, (H, W, 3), dtype=np.uint8) for s in seeds]
+
+
+def _shift(p, delta):
+    p = dict(p)
+    for lvl in range(3):
+        k = f"model.22.cv3.{lvl}.2.bias"
+        p[k] = p[k] + np.float32(delta)
+    return p
+
+
+def _device(monkeypatch, delta, conf=0.05):
+    monkeypatch.setenv("PERSON_CAPTURE_AMD_PRECISION", "f32")
+    monkeypatch.setenv("PERSON_CAPTURE_AMD_ARCFACE", "iresnet50")
+    fe = fe_mod.FaceEmbedder(ctx="cuda:0", yolo_model="yolov8n-face.pt", conf=conf)
+    assert fe.detector_backend == "yolo" and fe.yolo_scale == "n"
+    fe._yf_params = _shift(fe._yf_params, delta)
+    fe._yf_engines.clear()
+    fe.debug_chips = True
+    o = oy.OracleYoloFaceEmbedder(fe._yf_params, "n", fe._arc_params, 50, conf=conf)
+    return fe, o
+
+
+def _embed(o, chip, flip=True):
+    e = nt.iresnet_forward(o.p_a, o.depth, nt.arcface_input_from_chips(chip[None])).numpy()
+    ef = nt.iresnet_forward(o.p_a, o.depth, nt.arcface_input_from_chips(chip[None, :, ::-1])).numpy() if flip else None
+    return ra.arcface_postprocess(e, ef)[0]
+
+
+def _run_compare(fe, o, frames, flip=True):
+    got = fe.extract_batch(frames)
+    traces, n_exact, n_chained = set(), 0, 0
+    for fi, (f, g) in enumerate(zip(frames, got)):
+        r = o.extract(f)
+        traces.update(t for t in o.trace if not t.startswith("predict"))
+        assert len(g) == len(r), (fi, len(g), len(r), o.trace)
+        for a, b in zip(sorted(g, key=lambda x: tuple(x["bbox"])), sorted(r, key=lambda x: tuple(x["bbox"]))):
+            assert np.array_equal(a["bbox"], b["bbox"]), (fi, a["bbox"], b["bbox"])
+            assert abs(cv_ops.face_quality(a["chip"]) - a["quality"]) <= 1e-9 * max(1.0, a["quality"])
+            if np.array_equal(a["chip"], b["chip"]):
+                assert np.abs(a["feat"] - b["feat"]).max() < 1e-4
+                n_exact += 1
+            else:
+                assert np.abs(_embed(o, a["chip"], flip) - a["feat"]).max() < 1e-4
+                n_chained += 1
+    return traces, n_exact, n_chained
+
+
+def test_yolo_face_zero_degree_tta_redetect(gpu_ctx, monkeypatch):
+    fe, o = _device(monkeypatch, -1.5)
+    traces, ne, nc = _run_compare(fe, o, _frames(range(4)))
+    print("branches:", sorted(traces), "exact", ne, "chained", nc)
+    for b in ("tta1.25", "nolandmarks", "redetect"):
+        assert b in traces, b
+    assert ne >= nc and ne + nc >= 6
+
+
+def test_yolo_face_rotation_and_affine_fallbacks(gpu_ctx, monkeypatch):
+    fe, o = _device(monkeypatch, -2.1)
+    traces, ne, nc = _run_compare(fe, o, _frames(range(3)))
+    print("branches:", sorted(traces), "exact", ne, "chained", nc)
+    for b in ("tta1.5", "rot90", "rot270", "rot180", "affine45", "affine-135"):
+        assert b in traces, b
+    assert ne + nc >= 2
+
+
+def test_yolo_face_prescan_rotation_round_robin(gpu_ctx, monkeypatch):
+    """set_prescan_fast(True): no TTA, one rotation per empty frame alternating 90 / 270, no affine
+    pass, one ArcFace forward per face."""
+    fe, o = _device(monkeypatch, -2.1)
+    fe.set_prescan_fast(True)
+    o._fast_prescan = True
+    traces, ne, nc = _run_compare(fe, o, _frames([2, 2, 0]), flip=False)
+    print("branches:", sorted(traces))
+    assert "rot90" in traces and "rot270" in traces
+    assert not any(t.startswith(("tta", "affine")) for t in traces)
+    assert fe._prescan_rr == o._prescan_rr
+
+
+def test_default_face_embedder_is_yolov8l_face(gpu_ctx, monkeypatch):
+    """An unchanged caller's FaceEmbedder() (main.py:172: Y8F_DEFAULT) constructs and returns faces
+    in the reference's dict format."""
+    monkeypatch.delenv("PERSON_CAPTURE_AMD_FACE_MODEL", raising=False)
+    fe = fe_mod.FaceEmbedder()
+    assert fe.detector_backend == "yolo" and fe.yolo_scale == "l" and fe.backend == "arcface"
+    frame = np.full((360, 640, 3), 60, np.uint8)
+    frame[100:260, 200:440] = np.random.default_rng(3).integers(0, 256, (160, 240, 3), dtype=np.uint8)
+    faces = fe.extract(frame)
+    assert isinstance(faces, list)
+    for f in faces:
+        assert f["bbox"].dtype == np.int32 and f["bbox"].shape == (4,)
+        assert f["feat"].shape == (512,) and abs(float(np.linalg.norm(f["feat"])) - 1.0) < 1e-3
+        assert isinstance(f["quality"], float)
+    assert fe.extract(None) == [] and fe.extract(np.zeros((0, 0, 3), np.uint8)) == []

@@ -93,3 +93,55 @@ def test_yolo_postprocess_contract():
     np.testing.assert_allclose(d[0, :4], [(cx - 24) * 3, (cy - 40 - 12) * 3, (cx + 24) * 3, (cy + 40 - 12) * 3],
                                atol=0.05)
     assert len(ra.yolo_postprocess(heads, 0.99, 0.45, 40, 384, 640, 1080, 1920)) == 0
+
+
+@pytest.fixture(scope="module")
+def y8face():
+    return my.synth_yolov8_face("n", seed=4)
+
+
+def test_face_pose_layer_table():
+    """yolov8-pose head (the YOLOv8-face models, kpt_shape [5, 3]): cv4 width max(ch0 // 4, 15)."""
+    L = my.yolo_layers("l", 1, (5, 3))[22]
+    assert L["type"] == "Pose" and L["nk"] == 15 and L["c4"] == max(L["ch"][0] // 4, 15) and L["nc"] == 1
+
+
+@pytest.mark.parametrize("Hp,Wp", [(128, 192)])
+def test_yolo_face_program_matches_oracle(y8face, Hp, Wp):
+    """The Pose program's [DFL | cls | kpt] head maps against the literal oracle forward."""
+    rng = np.random.default_rng(6)
+    x = np.zeros((2, Hp, Wp, 4), np.float32)
+    x[..., :3] = rng.integers(0, 256, (2, Hp, Wp, 3)).astype(np.float32) / 255.0
+    ref = nt.yolov8_forward(y8face, "n", torch.from_numpy(np.ascontiguousarray(x[..., :3].transpose(0, 3, 1, 2))),
+                            nc=1, kpt=(5, 3))
+    outs = run_program(my.compile_yolov8(y8face, "n", Hp, Wp, nc=1, kpt=(5, 3)), x)
+    for o, r in zip(outs, ref):
+        got = o.permute(0, 2, 3, 1).numpy()
+        r = r.numpy()
+        assert got.shape == r.shape and r.shape[-1] == 64 + 1 + 15
+        assert np.abs(got - r).max() / max(1.0, np.abs(r).max()) < 1e-4
+
+
+def test_yolo_pose_postprocess_contract():
+    """A planted face anchor: keypoints decode as (raw * 2 + anchor - 0.5) * stride, scale_coords
+    with the unrounded pad, invisible points (sigmoid < 0.5) zeroed as Results.keypoints does."""
+    heads = [np.full((h, w, 80), -20.0, np.float32) for h, w in ((48, 80), (24, 40), (12, 20))]
+    hd = heads[0]
+    hd[..., :64] = 0.0
+    hd[20, 30, :64] = -8.0
+    for k, b in enumerate((3, 5, 3, 5)):
+        hd[20, 30, 16 * k + b] = 8.0
+    hd[20, 30, 64] = 3.0
+    raw = np.array([[0.1, 0.2, 4.0], [0.9, 0.2, 4.0], [0.5, 0.6, 4.0], [0.2, 0.9, -4.0], [0.8, 0.9, 4.0]],
+                   np.float32)
+    hd[20, 30, 65:] = raw.reshape(-1)
+    d, k = ra.yolo_postprocess(heads, 0.3, 0.3, 60, 384, 640, 1080, 1920, nk=15)
+    assert d.shape == (1, 5) and k.shape == (1, 5, 3)
+    gain = 1 / 3
+    for q in range(5):
+        if raw[q, 2] < 0:
+            assert k[0, q, 0] == 0 and k[0, q, 1] == 0
+            continue
+        x = (raw[q, 0] * 2 + 30) * 8
+        y = (raw[q, 1] * 2 + 20) * 8
+        assert abs(k[0, q, 0] - x / gain) < 1e-2 and abs(k[0, q, 1] - (y - 12) / gain) < 1e-2
