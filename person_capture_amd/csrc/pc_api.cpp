@@ -92,6 +92,9 @@ struct YoloDecodeParams { YoloLevel lv[3]; int nlv, total, nc; float conf; float
 struct YoloScale;
 hipError_t yolo_decode_launch(const YoloDecodeParams& p, int N, hipStream_t s);
 struct YoloKptScale;
+hipError_t yolo_nms_big_launch(const float* cand, const int* count, int cap, int pcap, unsigned long long* keys,
+                               int* slot_of, float* kept, float iou, int max_det, const YoloScale* sc, float* dets,
+                               int* nkeep, int* keep_anchor, int N, hipStream_t s);
 hipError_t yolo_kpts_launch(const YoloDecodeParams& p, int nk, int koff, int max_det, const int* nkeep,
                             const int* keep_anchor, const YoloScale* sc, const YoloKptScale* ksc, float* kpts, int N,
                             hipStream_t s);
@@ -136,6 +139,9 @@ struct pc_ctx {
   float* ycand = nullptr;
   int* ycount = nullptr;
   size_t ycand_images = 0;
+  int ycand_cap = 0;
+  void* ybig = nullptr;        // global-memory NMS: keys, slot map, kept boxes
+  size_t ybig_bytes = 0;
   int* ykeep = nullptr;        // pose: anchor index of every kept box
   size_t ykeep_bytes = 0;
   // CLIP preprocessing tables + horizontal-pass scratch
@@ -220,6 +226,7 @@ extern "C" int pc_ctx_destroy(pc_ctx* c) {
   if (c->det_scale) hipFree(c->det_scale);
   if (c->ycand) hipFree(c->ycand);
   if (c->ykeep) hipFree(c->ykeep);
+  if (c->ybig) hipFree(c->ybig);
   if (c->ycount) hipFree(c->ycount);
   if (c->clip_tmp) hipFree(c->clip_tmp);
   if (c->own_stream) hipStreamDestroy(c->own_stream);
@@ -1245,14 +1252,6 @@ static int yolo_detect_impl(pc_net* net, const pc_yolo_letterbox_desc* h, int n,
   const NetTensor& I = net->tens[net->in_tensor];
   if (I.H != Hp || I.W != Wp || I.C != 4) return fail(c, PC_ERR_ARG, "pc_yolo_detect: canvas does not match the net input");
   if (int e = check_yolo_descs(c, h, n, Hp, Wp)) return e;
-  const int cap = 16384;
-  if (c->ycand_images < (size_t)n) {
-    if (c->ycand) hipFree(c->ycand);
-    if (c->ycount) hipFree(c->ycount);
-    HIPCHK(c, hipMalloc((void**)&c->ycand, (size_t)n * cap * 8 * 4));
-    HIPCHK(c, hipMalloc((void**)&c->ycount, (size_t)n * 4));
-    c->ycand_images = n;
-  }
   const size_t need = (size_t)net->max_batch * Hp * Wp * 4 * (net->f32 ? 4 : 2);
   if (net->prep_bytes < need) {
     if (net->prep) HIPCHK(c, hipFree(net->prep));
@@ -1279,7 +1278,17 @@ static int yolo_detect_impl(pc_net* net, const pc_yolo_letterbox_desc* h, int n,
     p.lv[l].loc_offset = loc;
     loc += O.H * O.W;
   }
-  if (loc > cap) return fail(c, PC_ERR_CAPACITY, "pc_yolo_detect: more anchors than the NMS capacity");
+  // candidate slots for every anchor: a low threshold on a big canvas may pass most of them
+  // (above 16384 candidates the global-memory NMS runs)
+  const int cap = std::max(16384, loc);
+  if (c->ycand_images < (size_t)n || c->ycand_cap < cap) {
+    if (c->ycand) { HIPCHK(c, hipStreamSynchronize(c->stream)); hipFree(c->ycand); }
+    if (c->ycount) hipFree(c->ycount);
+    HIPCHK(c, hipMalloc((void**)&c->ycand, (size_t)n * cap * 8 * 4));
+    HIPCHK(c, hipMalloc((void**)&c->ycount, (size_t)n * 4));
+    c->ycand_images = n;
+    c->ycand_cap = cap;
+  }
   p.total = loc;
   p.nc = nc;
   p.conf = conf;
@@ -1301,6 +1310,20 @@ static int yolo_detect_impl(pc_net* net, const pc_yolo_letterbox_desc* h, int n,
   }
   HIPCHK(c, yolo_nms_launch(c->ycand, c->ycount, cap, iou, max_det, (const YoloScale*)dsc, dets, count, n, c->stream,
                             keep_anchor));
+  if (loc > 16384) {
+    int pcap = 8192;
+    while (pcap < cap) pcap <<= 1;
+    const size_t kb = (size_t)n * pcap * 8 + (size_t)n * cap * 4 + (size_t)n * max_det * 16;
+    if (c->ybig_bytes < kb) {
+      if (c->ybig) { HIPCHK(c, hipStreamSynchronize(c->stream)); hipFree(c->ybig); }
+      HIPCHK(c, hipMalloc(&c->ybig, kb));
+      c->ybig_bytes = kb;
+    }
+    char* b = (char*)c->ybig;
+    HIPCHK(c, yolo_nms_big_launch(c->ycand, c->ycount, cap, pcap, (unsigned long long*)b,
+                                  (int*)(b + (size_t)n * pcap * 8), (float*)(b + (size_t)n * pcap * 8 + (size_t)n * cap * 4),
+                                  iou, max_det, (const YoloScale*)dsc, dets, count, keep_anchor, n, c->stream));
+  }
   if (nk) {
     void* dks;
     if ((rc = stage_copy(c, h_kpt_pad, sizeof(float) * 2 * n, &dks))) return rc;

@@ -163,6 +163,7 @@ __global__ __launch_bounds__(1024) void yolo_nms(const float* __restrict__ cand,
   const int n = blockIdx.x;
   const int tid = threadIdx.x;
   const int K = min(count[n], cap);
+  if (K > YNMS_CAP) return;   // yolo_nms_big handles this image
   const float* cb = cand + (long long)n * cap * 8;
   int P = 1;
   while (P < K) P <<= 1;
@@ -277,6 +278,163 @@ hipError_t yolo_kpts_launch(const YoloDecodeParams& p, int nk, int koff, int max
   return hipGetLastError();
 }
 
+// The same NMS for an image with more than YNMS_CAP candidates (low thresholds at the heavy
+// sizes up to 2048: 86016 anchors): keys in global memory, sorted by one workgroup (bitonic
+// network, strides below YBIG_TILE in LDS), the first max_nms (30000, ultralytics'
+// non_max_suppression cap) walked in blocks of 1024 — each candidate first tested against
+// every box kept so far, then the block resolved in order. Keys (score desc, anchor asc),
+// IoU arithmetic and the suppression test are scrfd-style ports of yolo_nms's.
+constexpr int YBIG_TILE = 8192;
+constexpr int YMAX_NMS = 30000;
+
+__device__ inline void ycmpswap(unsigned long long& a, unsigned long long& b, bool up) {
+  if ((a > b) == up) { const unsigned long long t = a; a = b; b = t; }
+}
+
+__global__ __launch_bounds__(1024) void yolo_nms_big(const float* __restrict__ cand, const int* __restrict__ count,
+                                                     int cap, int pcap, unsigned long long* __restrict__ keys_g,
+                                                     int* __restrict__ slot_of, float* __restrict__ kept_g, float iou,
+                                                     int max_det, const YoloScale* __restrict__ sc,
+                                                     float* __restrict__ dets, int* __restrict__ nkeep,
+                                                     int* __restrict__ keep_anchor) {
+  __shared__ unsigned long long tile[YBIG_TILE];
+  __shared__ float sbox[1024][4];
+  __shared__ unsigned char ssup[1024];
+  __shared__ int s_next;
+  const int n = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int K = min(count[n], cap);
+  if (K <= YNMS_CAP) return;   // yolo_nms handled this image
+  const float* cb = cand + (long long)n * cap * 8;
+  unsigned long long* keys = keys_g + (long long)n * pcap;
+  int* smap = slot_of + (long long)n * cap;
+  float* kept_box = kept_g + (long long)n * max_det * 4;
+  int P = YBIG_TILE;
+  while (P < K) P <<= 1;
+  for (int i = tid; i < P; i += 1024) {
+    unsigned long long key = ~0ull;
+    if (i < K) {
+      const unsigned u = __float_as_uint(cb[i * 8 + 4]);   // score > 0
+      const unsigned aidx = __float_as_uint(cb[i * 8 + 5]);
+      key = ((unsigned long long)(~u) << 32) | aidx;
+      smap[aidx] = i;
+    }
+    keys[i] = key;
+  }
+  __syncthreads();
+  for (int t0 = 0; t0 < P; t0 += YBIG_TILE) {
+    for (int i = tid; i < YBIG_TILE; i += 1024) tile[i] = keys[t0 + i];
+    __syncthreads();
+    for (int k = 2; k <= YBIG_TILE; k <<= 1)
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int li = tid; li < YBIG_TILE; li += 1024) {
+          const int lx = li ^ j;
+          if (lx > li) ycmpswap(tile[li], tile[lx], ((t0 + li) & k) == 0);
+        }
+        __syncthreads();
+      }
+    for (int i = tid; i < YBIG_TILE; i += 1024) keys[t0 + i] = tile[i];
+    __syncthreads();
+  }
+  for (int k = 2 * YBIG_TILE; k <= P; k <<= 1) {
+    int j = k >> 1;
+    for (; j >= YBIG_TILE; j >>= 1) {
+      for (int i = tid; i < P; i += 1024) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          unsigned long long a = keys[i], b = keys[ixj];
+          ycmpswap(a, b, (i & k) == 0);
+          keys[i] = a; keys[ixj] = b;
+        }
+      }
+      __syncthreads();
+    }
+    for (int t0 = 0; t0 < P; t0 += YBIG_TILE) {
+      for (int i = tid; i < YBIG_TILE; i += 1024) tile[i] = keys[t0 + i];
+      __syncthreads();
+      for (int jj = j; jj > 0; jj >>= 1) {
+        for (int li = tid; li < YBIG_TILE; li += 1024) {
+          const int lx = li ^ jj;
+          if (lx > li) ycmpswap(tile[li], tile[lx], ((t0 + li) & k) == 0);
+        }
+        __syncthreads();
+      }
+      for (int i = tid; i < YBIG_TILE; i += 1024) keys[t0 + i] = tile[i];
+      __syncthreads();
+    }
+  }
+  const YoloScale S = sc[n];
+  const int KN = min(K, YMAX_NMS);
+  int nk = 0;
+  for (int b0 = 0; b0 < KN && nk < max_det; b0 += 1024) {
+    const int i = b0 + tid;
+    bool sup = i >= KN;
+    float x1 = 0.f, y1 = 0.f, x2 = 0.f, y2 = 0.f, area = 0.f;
+    int si = 0;
+    if (!sup) {
+      si = smap[(unsigned)(keys[i] & 0xFFFFFFFFull)];
+      const float* bj = cb + si * 8;
+      x1 = bj[0]; y1 = bj[1]; x2 = bj[2]; y2 = bj[3];
+      area = (x2 - x1) * (y2 - y1);
+      for (int q = 0; q < nk; ++q) {
+        const float* kb = kept_box + q * 4;
+        const float xx1 = fmaxf(kb[0], x1), yy1 = fmaxf(kb[1], y1);
+        const float xx2 = fminf(kb[2], x2), yy2 = fminf(kb[3], y2);
+        const float w = fmaxf(xx2 - xx1, 0.0f), h = fmaxf(yy2 - yy1, 0.0f);
+        const float inter = w * h;
+        const float area_k = (kb[2] - kb[0]) * (kb[3] - kb[1]);
+        if (inter / (area_k + area - inter) > iou) { sup = true; break; }
+      }
+    }
+    sbox[tid][0] = x1; sbox[tid][1] = y1; sbox[tid][2] = x2; sbox[tid][3] = y2;
+    ssup[tid] = sup ? 1 : 0;
+    __syncthreads();
+    int cur = 0;
+    while (nk < max_det) {
+      if (tid == 0) s_next = 1024;
+      __syncthreads();
+      if (tid >= cur && !ssup[tid]) atomicMin(&s_next, tid);
+      __syncthreads();
+      const int c = s_next;
+      if (c >= 1024) break;
+      if (tid == c) {
+        float* kb = kept_box + nk * 4;
+        kb[0] = x1; kb[1] = y1; kb[2] = x2; kb[3] = y2;
+        float* d = dets + ((long long)n * max_det + nk) * 5;
+        d[0] = fminf(fmaxf((x1 - S.padx) / S.gain, 0.f), S.W0);
+        d[1] = fminf(fmaxf((y1 - S.pady) / S.gain, 0.f), S.H0);
+        d[2] = fminf(fmaxf((x2 - S.padx) / S.gain, 0.f), S.W0);
+        d[3] = fminf(fmaxf((y2 - S.pady) / S.gain, 0.f), S.H0);
+        d[4] = cb[si * 8 + 4];
+        if (keep_anchor) keep_anchor[(long long)n * max_det + nk] = __float_as_int(cb[si * 8 + 5]);
+      }
+      if (tid > c && !ssup[tid]) {
+        const float cx1 = sbox[c][0], cy1 = sbox[c][1], cx2 = sbox[c][2], cy2 = sbox[c][3];
+        const float xx1 = fmaxf(cx1, x1), yy1 = fmaxf(cy1, y1);
+        const float xx2 = fminf(cx2, x2), yy2 = fminf(cy2, y2);
+        const float w = fmaxf(xx2 - xx1, 0.0f), h = fmaxf(yy2 - yy1, 0.0f);
+        const float inter = w * h;
+        const float area_c = (cx2 - cx1) * (cy2 - cy1);
+        if (inter / (area_c + area - inter) > iou) ssup[tid] = 1;
+      }
+      ++nk;
+      cur = c + 1;
+      __syncthreads();
+    }
+    __syncthreads();
+  }
+  if (tid == 0) nkeep[n] = nk;
+}
+
+hipError_t yolo_nms_big_launch(const float* cand, const int* count, int cap, int pcap, unsigned long long* keys,
+                               int* slot_of, float* kept, float iou, int max_det, const YoloScale* sc, float* dets,
+                               int* nkeep, int* keep_anchor, int N, hipStream_t s) {
+  if (max_det > 1024 * 64) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(yolo_nms_big, dim3(N), dim3(1024), 0, s, cand, count, cap, pcap, keys, slot_of, kept, iou, max_det,
+                     sc, dets, nkeep, keep_anchor);
+  return hipGetLastError();
+}
+
 hipError_t yolo_letterbox_launch(int f32, const YoloLetterboxDesc* d_descs, int N, int Hp, int Wp, void* out,
                                  hipStream_t s) {
   dim3 grid((Hp * Wp + 255) / 256, N);
@@ -293,7 +451,6 @@ hipError_t yolo_decode_launch(const YoloDecodeParams& p, int N, hipStream_t s) {
 
 hipError_t yolo_nms_launch(const float* cand, const int* count, int cap, float iou, int max_det, const YoloScale* sc,
                            float* dets, int* nkeep, int N, hipStream_t s, int* keep_anchor) {
-  if (cap > YNMS_CAP) return hipErrorInvalidValue;
   hipLaunchKernelGGL(yolo_nms, dim3(N), dim3(1024), 0, s, cand, count, cap, iou, max_det, sc, dets, nkeep,
                      keep_anchor);
   return hipGetLastError();

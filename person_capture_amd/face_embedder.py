@@ -214,6 +214,9 @@ class FaceEmbedder(YoloFaceBranch):
         self.rot_after_hit_frames = 8
         self.fast_no_face_imgsz = 512
         self._scrfd_fixed_shape = (640, 640)
+        # when a list, extract_batch appends (frame index, policy_state()) after each frame's
+        # detector policy (the speculative pre-scan driver rolls back with it)
+        self.state_trace: Optional[list] = None
         if self.detector_backend == "scrfd":
             self.scrfd = self._engine(640)
             if callable(progress):
@@ -452,6 +455,8 @@ class FaceEmbedder(YoloFaceBranch):
                 first = spec[i] if dyn == spec_dyn[i] else self._detect_once(im, dyn, float(self.conf))
                 kept = self._scrfd_policy(im, dyn, first)
                 faces_per_frame[i] = kept
+                if self.state_trace is not None:
+                    self.state_trace.append((i, self.policy_state()))
                 jobs.extend(self._face_jobs(im, i, kept))
             lap("policy")
             per = self._embed_per()
@@ -473,6 +478,15 @@ class FaceEmbedder(YoloFaceBranch):
         return out
 
     # ------------------------------------------------------------------ detector policy
+    def policy_state(self) -> tuple:
+        """The per-instance state the SCRFD policy carries from frame to frame
+        (face_embedder.py:489-497): frame index, no-face streak, last face index, rotation
+        cycle, pre-scan round-robin counter."""
+        return (self._frame_idx, self._no_face_streak, self._last_face_idx, self._rot_cycle, self._prescan_rr)
+
+    def set_policy_state(self, st: tuple) -> None:
+        self._frame_idx, self._no_face_streak, self._last_face_idx, self._rot_cycle, self._prescan_rr = st
+
     def _dyn_for(self, im: _DevImage, imgsz: Optional[int]) -> int:
         """face_embedder.py:2190-2204."""
         H0, W0 = im.H, im.W

@@ -1,0 +1,290 @@
+"""Pre-scan driver: the sampling loop of Processor._prescan (gui_app.py:1101-1668) over
+device-resident frames, batched speculatively on the MI355X.
+
+Per sample (gui_app.py:1468-1622): the escalation hint follows the `active` span state
+(`_prescan_rr_mode = "full" if active else "rr"`, set_prescan_hint(escalate=active)); the
+fd9 skip gate (after `prescan_fd9_grace` samples with no match, only every
+`prescan_fd9_probe_period`-th sample is extracted while idle); an extracted sample is
+downscaled to `prescan_max_width` with INTER_AREA (:1505-1507, on the device), run through
+FaceEmbedder.extract, each face matched against the live bank (_fd_min), confident
+good-quality faces grow the bank (_stream_ref_bank_update with the add cooldown), and the
+best distance drives the enter/exit hysteresis that builds the keep-spans (pad, min length,
+merge), closed at the end and bridged over short gaps (:1648-1668).
+
+The loop is sequential: sample k+1's detector settings, skip decision and bank depend on
+sample k. It runs in chunks: the driver predicts the gate decisions and hints of the next
+`batch` samples assuming the current regime holds (idle without a match stays idle; a
+match keeps the span open), runs all predicted extractions in ONE FaceEmbedder.extract_batch
+(downscale, SCRFD, align, ArcFace batched on the device), then replays the host logic
+sample by sample. At the first sample whose real state differs from the prediction, the
+chunk is cut there: the FaceEmbedder's per-frame policy state is restored from its state
+trace and the next chunk starts at that sample. Results are therefore identical to the
+sequential loop; a regime change only costs the tail of one chunk.
+
+Not here (GUI/IO plumbing outside the per-frame hot path): the command queue (pause, seek,
+step, live cfg edits), decoder seeking, previews and progress signals, and the edge
+refinement re-scan (:1670-) which reuses this same per-sample step at a finer stride.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from .match import fd_min, stream_ref_bank_update
+
+
+@dataclass
+class PrescanConfig:
+    """The SessionConfig fields the loop reads (gui_app.py:554-590 defaults)."""
+    prescan_stride: int = 24
+    prescan_max_width: int = 416
+    prescan_face_conf: float = 0.5
+    prescan_fd_enter: float = 0.45
+    prescan_fd_add: float = 0.22
+    prescan_fd_exit: float = 0.52
+    prescan_add_cooldown_samples: int = 5
+    prescan_rot_probe_period: int = 3
+    prescan_probe_imgsz: int = 512
+    prescan_no_upscale_det: bool = True
+    prescan_probe_conf: float = 0.03
+    prescan_heavy_90: int = 1536
+    prescan_heavy_180: int = 1280
+    prescan_min_segment_sec: float = 1.0
+    prescan_pad_sec: float = 1.5
+    prescan_bridge_gap_sec: float = 1.0
+    prescan_exit_cooldown_sec: float = 0.50
+    prescan_bank_max: int = 64
+    prescan_diversity_dedup_cos: float = 0.968
+    prescan_replace_margin: float = 0.010
+    prescan_fd9_skip: bool = True
+    prescan_fd9_grace: int = 1
+    prescan_fd9_probe_period: int = 2
+    prescan_weights: Tuple[float, float, float] = (0.70, 0.25, 0.05)
+    face_quality_min: float = 70.0
+
+
+@dataclass
+class SampleRecord:
+    idx: int            # frame index
+    extracted: bool
+    best: float         # best fd of the sample (9.0 when skipped or no face)
+    n_faces: int
+    bank_action: str    # last bank action of the sample ("" when none)
+    active: bool        # span state after the sample
+
+
+class _LoopState:
+    __slots__ = ("active", "start", "neg_run", "fd9_streak", "last_add_sample", "spans", "bank_list", "bank",
+                 "processed", "added")
+
+    def __init__(self, ref_feat):
+        if ref_feat is None:
+            self.bank_list: List[np.ndarray] = []
+        else:
+            arr = np.asarray(ref_feat, dtype=np.float32)
+            if arr.ndim == 1:
+                arr = arr.reshape(1, -1)
+            arr = arr / np.maximum(np.linalg.norm(arr, axis=1, keepdims=True), 1e-6)
+            self.bank_list = [row.copy() for row in arr]
+        self.bank = np.vstack(self.bank_list).astype(np.float32) if self.bank_list else None
+        self.active = False
+        self.start = 0
+        self.neg_run = 0
+        self.fd9_streak = 0
+        self.last_add_sample = -10 ** 9
+        self.spans: List[Tuple[int, int]] = []
+        self.processed = 0
+        self.added = 0
+
+    def copy(self) -> "_LoopState":
+        c = _LoopState.__new__(_LoopState)
+        for k in self.__slots__:
+            v = getattr(self, k)
+            setattr(c, k, list(v) if isinstance(v, list) else v)
+        return c
+
+
+class PrescanRunner:
+    """Processor._prescan's sampling loop for one FaceEmbedder (SCRFD backend)."""
+
+    def __init__(self, face, cfg: PrescanConfig, fps: float, total_frames: int, ref_feat=None, batch: int = 32):
+        self.face, self.cfg, self.fps, self.total = face, cfg, float(fps), int(total_frames)
+        self.ref_feat = ref_feat
+        self.batch = max(1, int(batch))
+        self.records: List[SampleRecord] = []
+        self.chunks = 0
+        self.cuts = 0
+
+    # ---- FaceEmbedder runtime configuration (gui_app.py:1162-1196) ----
+    def _apply_face_cfg(self) -> None:
+        f, c = self.face, self.cfg
+        f.conf = min(0.95, max(0.01, float(c.prescan_face_conf)))
+        f._probe_conf = float(c.prescan_probe_conf)
+        f._prescan_period = int(c.prescan_rot_probe_period)
+        f._prescan_probe_imgsz = int(c.prescan_probe_imgsz)
+        f._prescan_no_upscale_det = bool(c.prescan_no_upscale_det)
+        f._high_90 = int(c.prescan_heavy_90)
+        f._high_180 = int(c.prescan_heavy_180)
+
+    def _gate(self, st: _LoopState) -> Tuple[bool, bool]:
+        """(skip_extract, gate_active) of the fd9 skip gate (gui_app.py:1479-1492)."""
+        c = self.cfg
+        if (not st.active) and c.prescan_fd9_skip:
+            grace = max(0, int(c.prescan_fd9_grace))
+            period = max(1, int(c.prescan_fd9_probe_period))
+            if st.fd9_streak >= grace:
+                return (st.fd9_streak % period) != 0, True
+        return False, False
+
+    def _downscale(self, im, k: int):
+        """gui_app.py:1505-1507: INTER_AREA to prescan_max_width when wider."""
+        Wmax = int(self.cfg.prescan_max_width)
+        if im.W > Wmax:
+            nh = int(round(im.H * (Wmax / float(im.W))))
+            return self.face._dev_resize(im, f"prescan{k}", dsize=(Wmax, nh), area=True)
+        return im
+
+    def _finish_sample(self, st: _LoopState, idx: int, sample_idx: int, faces, extracted: bool) -> SampleRecord:
+        """Bank growth, fd9 streak and span hysteresis of one sample (gui_app.py:1512-1622)."""
+        c = self.cfg
+        best = 9.0
+        action = ""
+        if extracted:
+            for f in faces:
+                feat = f.get("feat")
+                if feat is None:
+                    continue
+                fd = fd_min(feat, st.bank)
+                best = min(best, fd)
+                if fd <= float(c.prescan_fd_add) and (sample_idx - st.last_add_sample) >= int(
+                        c.prescan_add_cooldown_samples) and f.get("quality", 1e9) >= c.face_quality_min:
+                    st.bank, action, _ = stream_ref_bank_update(
+                        st.bank_list, st.bank, feat, float(f.get("quality", 0.0)), cap=int(c.prescan_bank_max),
+                        dedup_cos=float(c.prescan_diversity_dedup_cos), rep_margin=float(c.prescan_replace_margin),
+                        weights=tuple(c.prescan_weights))
+                    if action in ("added", "replaced"):
+                        st.last_add_sample = sample_idx
+                        st.added += action == "added"
+        st.fd9_streak = st.fd9_streak + 1 if best >= 8.99 else 0
+        stride = max(1, int(c.prescan_stride))
+        pad = int(round(c.prescan_pad_sec * self.fps))
+        min_len = int(round(c.prescan_min_segment_sec * self.fps))
+        if best <= float(c.prescan_fd_enter):
+            if not st.active:
+                st.active = True
+                st.fd9_streak = 0
+                st.start = idx
+            st.neg_run = 0
+        elif st.active:
+            st.neg_run += 1
+            exit_cool = int(round(max(0.0, float(c.prescan_exit_cooldown_sec)) * self.fps))
+            if st.neg_run * stride >= exit_cool or best >= float(c.prescan_fd_exit):
+                s = max(0, st.start - pad)
+                e = min(self.total - 1, idx + pad)
+                if e - s + 1 >= min_len:
+                    if st.spans and s <= st.spans[-1][1] + 1:
+                        st.spans[-1] = (st.spans[-1][0], max(st.spans[-1][1], e))
+                    else:
+                        st.spans.append((s, e))
+                st.active = False
+                st.neg_run = 0
+                st.fd9_streak = 0
+        n = len(faces) if extracted else 0
+        return SampleRecord(idx, extracted, float(best), n, action, st.active)
+
+    def run(self, frame_at: Callable[[int], object]) -> Tuple[List[Tuple[int, int]], Optional[np.ndarray]]:
+        """frame_at(frame_index) -> the frame as a device image (face_embedder._DevImage) or a host
+        BGR array. Returns (spans, updated bank) like Processor._prescan."""
+        f, c = self.face, self.cfg
+        self._apply_face_cfg()
+        f.configure_rotation_strategy(adaptive=False)
+        f.set_prescan_fast(True, mode="rr")
+        f.set_prescan_hint(escalate=False)
+        self._apply_face_cfg()
+        stride = max(1, int(c.prescan_stride))
+        samples = list(range(0, self.total, stride))
+        st = _LoopState(self.ref_feat)
+        k = 0
+        while k < len(samples):
+            # ---- predict the next chunk under the current regime ----
+            sim = st.copy()
+            plan = []   # (sample position, skip)
+            for j in range(k, min(len(samples), k + self.batch)):
+                skip, _ = self._gate(sim)
+                plan.append((j, skip))
+                # regime assumption: idle stays without a match, a span stays open with one
+                sim.fd9_streak = sim.fd9_streak + 1 if not sim.active else 0
+            active0 = st.active
+            f._prescan_rr_mode = "full" if active0 else "rr"
+            f.set_prescan_hint(escalate=active0)
+            todo = [j for j, skip in plan if not skip]
+            ims = []
+            for j in todo:
+                im = frame_at(samples[j])
+                if not hasattr(im, "ptr"):
+                    im = f._upload(np.ascontiguousarray(im), key=f"prescan_src{j % self.batch}")
+                ims.append(self._downscale(im, j - k))
+            state0 = f.policy_state()
+            f.state_trace = []
+            try:
+                res = f.extract_batch([None] * len(ims), dev_frames=ims) if ims else []
+            finally:
+                trace = f.state_trace
+                f.state_trace = None
+            by_pos = {j: r for j, r in zip(todo, res)}
+            state_after = {todo[t]: s for t, (_, s) in enumerate(trace)}
+            self.chunks += 1
+            # ---- replay; cut at the first divergence ----
+            last_state = state0
+            cut = None
+            for j, skip_pred in plan:
+                skip, _ = self._gate(st)
+                if skip != skip_pred or st.active != active0:
+                    cut = j
+                    break
+                rec = self._finish_sample(st, samples[j], st.processed, by_pos.get(j, []), not skip)
+                st.processed += 1
+                self.records.append(rec)
+                if not skip:
+                    last_state = state_after[j]
+            if cut is not None:
+                self.cuts += 1
+                k = cut
+            else:
+                k = plan[-1][0] + 1
+            f.set_policy_state(last_state)
+        if st.active:
+            pad = int(round(c.prescan_pad_sec * self.fps))
+            min_len = int(round(c.prescan_min_segment_sec * self.fps))
+            s, e = max(0, st.start - pad), self.total - 1
+            if e - s + 1 >= min_len:
+                if st.spans and s <= st.spans[-1][1] + 1:
+                    st.spans[-1] = (st.spans[-1][0], max(st.spans[-1][1], e))
+                else:
+                    st.spans.append((s, e))
+        spans = st.spans
+        if spans and c.prescan_bridge_gap_sec > 0:
+            gap = int(round(c.prescan_bridge_gap_sec * self.fps))
+            bridged = []
+            cs, ce = spans[0]
+            for s, e in spans[1:]:
+                if s - ce <= gap:
+                    ce = max(ce, e)
+                else:
+                    bridged.append((cs, ce))
+                    cs, ce = s, e
+            bridged.append((cs, ce))
+            spans = bridged
+        f.set_prescan_fast(False)
+        f.set_prescan_hint(escalate=False)
+        self.final_state = st
+        return spans, st.bank
+
+
+def prescan_sequential(face, cfg: PrescanConfig, fps: float, total_frames: int, frame_at, ref_feat=None):
+    """The same loop one sample per extract (batch 1): the reference's own order, for tests."""
+    r = PrescanRunner(face, cfg, fps, total_frames, ref_feat=ref_feat, batch=1)
+    out = r.run(frame_at)
+    return out, r
