@@ -361,19 +361,25 @@ def main_other(args):
         wl = (f"C4: YOLOv8n persons + SCRFD-10G@640 per person crop + ArcFace-R100 flip-TTA + CLIP ViT-L/14 ReID "
               f"per crop + match vs {bank_n}-embedding bank, 1080p, batch {args.batch} frames per GPU")
     else:
-        fe.set_prescan_fast(True)
-        small = [None] * args.batch
-        Wmax = 416
+        # the pre-scan driver (Processor._prescan's sampling loop, person_capture_amd/prescan.py):
+        # the resident 4K frames are the sampled frames of a clip at stride 24 (gui_app.py:555),
+        # downscaled to 416 wide on the device, fast pre-scan SCRFD + ArcFace, fd against the
+        # 1024-row bank, bank growth and span hysteresis replayed in sample order
+        from person_capture_amd.prescan import PrescanConfig, PrescanRunner
+        pcfg = PrescanConfig()
+        stride = pcfg.prescan_stride
+        bank_h = synth_bank(bank_n)
 
         def step():
-            for i, d in enumerate(devs):   # gui_app.py:1505-1507
-                nh = int(round(H * (Wmax / float(W))))
-                small[i] = fe._dev_resize(d, f"prescan{i}", dsize=(Wmax, nh), area=True)
-            faces = fe.extract_batch([None] * len(small), dev_frames=small, bank=bank)
-            stats["faces"] = sum(len(f) for f in faces)
-            return faces
-        wl = (f"C5: pre-scan 4K frames -> INTER_AREA 416 wide, SCRFD-10G@384, ArcFace-R100 (1 forward), match vs "
-              f"{bank_n}-embedding bank, batch {args.batch} frames per GPU")
+            r = PrescanRunner(fe, pcfg, 30.0, args.batch * stride, ref_feat=bank_h, batch=args.batch)
+            spans, _ = r.run(lambda idx: devs[idx // stride])
+            stats["faces"] = sum(x.n_faces for x in r.records)
+            stats["extracted_samples"] = sum(1 for x in r.records if x.extracted)
+            stats["driver_chunks"], stats["driver_cuts"], stats["spans"] = r.chunks, r.cuts, len(spans)
+            return spans
+        wl = (f"C5: pre-scan driver over 4K frames sampled at stride {stride} -> INTER_AREA 416 wide, fast pre-scan "
+              f"SCRFD-10G, ArcFace-R100 (1 forward, 2 while a span is active), fd vs {bank_n}-embedding bank, "
+              f"batch {args.batch} samples per GPU")
     for k in range(args.warmup):
         t = time.perf_counter()
         step()
@@ -381,7 +387,7 @@ def main_other(args):
         print(f"[bench {args.workload}] warmup {k}: {time.perf_counter() - t:.3f} s {stats}", file=sys.stderr,
               flush=True)
     if args.workload == "c5":
-        nets.append(fe._engine(fe._dyn_for(small[0], None)).net)
+        nets += [e.net for e in fe._scrfd_engines.values()]
     for n in nets:
         n.profile(True)
     elapsed, local_dt = _timed(world, ctx, args.steps, step)

@@ -180,6 +180,8 @@ class FaceEmbedder(YoloFaceBranch):
         # while the device works on chunk c+1 (0 = one chunk, no overlap)
         self._pipe_chunk = int(os.getenv("PERSON_CAPTURE_AMD_PIPE_CHUNK", "32"))
         self._pipe_ahead = int(os.getenv("PERSON_CAPTURE_AMD_PIPE_AHEAD", "2"))
+        # batched speculative fallback passes (TTA / edge pad / pre-scan rotations) per chunk
+        self._fb_prefetch = os.getenv("PERSON_CAPTURE_AMD_FALLBACK_PREFETCH", "1") != "0"
         # host phase timers of extract_batch (diagnostics; bench.py prints them)
         self.host_times: Optional[Dict[str, float]] = {} if os.getenv("PERSON_CAPTURE_AMD_HOST_TIMING") else None
         self._scrfd_engines: Dict[int, ScrfdEngine] = {}
@@ -217,6 +219,8 @@ class FaceEmbedder(YoloFaceBranch):
         # when a list, extract_batch appends (frame index, policy_state()) after each frame's
         # detector policy (the speculative pre-scan driver rolls back with it)
         self.state_trace: Optional[list] = None
+        self._fb_cache: Dict[tuple, tuple] = {}
+        self.fb_stats = [0, 0]   # fallback detections served by the batched prefetch / run one by one
         if self.detector_backend == "scrfd":
             self.scrfd = self._engine(640)
             if callable(progress):
@@ -286,6 +290,129 @@ class FaceEmbedder(YoloFaceBranch):
     def _detect_batch(self, imgs: Sequence[_DevImage], dyn: int, conf: float):
         eng = self._engine(int(dyn))
         return eng.detect_frames([(im.ptr, im.H, im.W, im.stride) for im in imgs], thresh=float(conf))
+
+    # ------------------------------------------------------------------ batched fallback passes
+    def _fb_detect(self, im: _DevImage, view: tuple, dyn: int, conf: float, make):
+        """One fallback detection of `view` of frame `im` (("tta", s), ("pad", p), ("rot", deg, pad))
+        at det size dyn and threshold conf: from the speculative batch prefetch when it ran with
+        exactly these parameters, else now (make() builds the view image on the device)."""
+        key = (im.ptr, im.H, im.W, im.stride) + tuple(view) + (int(dyn), float(conf))
+        hit = self._fb_cache.pop(key, None)
+        if hit is not None:
+            self.fb_stats[0] += 1
+            return hit
+        self.fb_stats[1] += 1
+        return self._detect_once(make(), dyn, conf)
+
+    def _fb_run(self, jobs: list) -> None:
+        """jobs: (key, view image, det size, conf): batched per (size, conf), results into the cache."""
+        groups: Dict[Tuple[int, float], list] = {}
+        for key, img, D, cf in jobs:
+            groups.setdefault((D, cf), []).append((key, img))
+        for (D, cf), lst in groups.items():
+            res = self._engine(D).detect_frames([(g.ptr, g.H, g.W, g.stride) for _, g in lst], thresh=cf)
+            for (key, _), r in zip(lst, res):
+                self._fb_cache[key] = r
+
+    def _empty_at_0(self, im: _DevImage, first) -> bool:
+        bb, kp = first
+        min_px = int(getattr(self, "scrfd_min_box_px", 8))
+        d = self._accumulate0(np.asarray(bb), np.asarray(kp, np.float32), im.W, im.H) if len(bb) else []
+        return not any(x[0][2] - x[0][0] >= min_px and x[0][3] - x[0][1] >= min_px for x in d)
+
+    def _prefetch_fallbacks(self, idx: List[int], imgs: Sequence[Optional[_DevImage]], spec: list,
+                            spec_dyn: list) -> None:
+        """Speculative batched fallback passes for the frames of a chunk whose 0-degree pass (at the
+        predicted det size) found nothing, in the order _scrfd_policy would run them: TTA scales then
+        the edge pad (stage by stage over the frames still empty), or in fast pre-scan with fixed
+        rotation gating the round-robin rotation probe and, where it hits, the heavy pass. Results
+        are cached under their exact parameters; the sequential policy walk consumes them (a frame
+        whose state-dependent parameters came out differently simply misses and detects then)."""
+        empty = [i for i in idx if imgs[i] is not None and spec[i] is not None and spec_dyn[i] is not None
+                 and self._empty_at_0(imgs[i], spec[i])]
+        if not empty:
+            return
+        ks = 0
+
+        def scratch_img(kind, i, build):
+            nonlocal ks
+            ks += 1
+            return build(f"fb_{kind}{ks}")
+
+        if not self._fast_prescan:
+            probe_conf = min(float(self.conf), float(self.scrfd_probe_conf_cap))
+            pending = list(empty)
+            for s in tuple(self.scrfd_tta_scales) + (1.25,):
+                jobs = []
+                for i in pending:
+                    im = imgs[i]
+                    if s == 1.25 and max(im.W, im.H) > 1920:
+                        continue
+                    dyn_s = _round32(min(self._heavy_cap, max(320, int(spec_dyn[i] * s))))
+                    img_s = scratch_img("tta", i, lambda k: self._dev_resize(im, k, fx=s, fy=s, area=s < 1.0))
+                    key = (im.ptr, im.H, im.W, im.stride, "tta", s, dyn_s, float(probe_conf))
+                    jobs.append((key, img_s, dyn_s, probe_conf))
+                self._fb_run(jobs)
+                pending = [i for i in pending if not any(len(self._fb_cache.get(j[0], ((),))[0]) for j in jobs
+                                                         if j[0][:4] == (imgs[i].ptr, imgs[i].H, imgs[i].W,
+                                                                         imgs[i].stride))]
+            jobs = []
+            for i in pending:
+                im = imgs[i]
+                pad = int(round(min(64, float(self.scrfd_edge_pad_frac) * max(im.W, im.H))))
+                if pad > 0:
+                    img_p = scratch_img("pad", i, lambda k: self._dev_rotate_pad(im, 0, pad, key=k))
+                    jobs.append(((im.ptr, im.H, im.W, im.stride, "pad", pad, spec_dyn[i], float(probe_conf)), img_p,
+                                 spec_dyn[i], probe_conf))
+            self._fb_run(jobs)
+            return
+        if self.rot_adaptive:
+            return   # rotation gating depends on the sequential hit history
+        rr = self._prescan_rr
+        probe_conf = max(0.02, float(getattr(self, "_probe_conf", 0.02)))
+        plan = []
+        for i in empty:
+            if self._prescan_rr_mode == "rr":
+                degs = ((90, 270)[rr % 2],)
+                rr += 1
+            else:
+                degs = (90, 270)
+            plan.append((i, degs))
+        jobs = []
+        for i, degs in plan:
+            im = imgs[i]
+            probe_dyn = _round32(max(320, min(spec_dyn[i], int(getattr(self, "_prescan_probe_imgsz", 384)))))
+            for deg in degs:
+                img_r = scratch_img("rot", i, lambda k: self._dev_rotate_pad(im, deg, 0, key=k))
+                jobs.append(((im.ptr, im.H, im.W, im.stride, "rot", deg, 0, probe_dyn, float(probe_conf)), img_r,
+                             probe_dyn, probe_conf))
+        self._fb_run(jobs)
+        jobs = []
+        for i, degs in plan:
+            im = imgs[i]
+            probe_dyn = _round32(max(320, min(spec_dyn[i], int(getattr(self, "_prescan_probe_imgsz", 384)))))
+            dyn = spec_dyn[i]
+            L = max(im.H, im.W)
+            heavy_cap = max(int(getattr(self, "_heavy_cap", 2048)), dyn)
+            for deg in degs:
+                pk = (im.ptr, im.H, im.W, im.stride, "rot", deg, 0, probe_dyn, float(probe_conf))
+                hits = len(self._fb_cache.get(pk, ((),))[0])
+                do_heavy = hits > 0 or self._prescan_escalate
+                if hits == 0:
+                    continue
+                if deg == 180:
+                    heavy = min(_round32(max(dyn, int(0.67 * L))), heavy_cap)
+                else:
+                    heavy = min(_round32(max(dyn, int(0.75 * L))), heavy_cap)
+                override = getattr(self, "_high_180" if deg == 180 else "_high_90", None)
+                if override and override > 0:
+                    heavy = max(heavy, _round32(int(override)))
+                heavy = min(heavy, int(getattr(self, "_heavy_cap", 2048)))
+                D = heavy if do_heavy else dyn
+                conf_deg = max(0.10, float(self.conf) * (0.8 if deg in (90, 270) else 0.6))
+                img_h = scratch_img("rot", i, lambda k: self._dev_rotate_pad(im, deg, 24, key=k))
+                jobs.append(((im.ptr, im.H, im.W, im.stride, "rot", deg, 24, D, float(conf_deg)), img_h, D, conf_deg))
+        self._fb_run(jobs)
 
     def _detect_once(self, img: _DevImage, dyn: int, conf: float):
         return self._detect_batch([img], dyn, conf)[0]
@@ -377,6 +504,7 @@ class FaceEmbedder(YoloFaceBranch):
         bank: optional match.DeviceBank; each face dict then also carries
         'fd' = Processor._fd_min(feat, bank), computed on the device."""
         self._bank = bank
+        self._fb_cache = {}
         n = len(frames) if dev_frames is None else len(dev_frames)
         if self.detector_backend == "yolo":   # face_embedder.py:1671-2093, frame by frame
             out_y: List[list] = []
@@ -444,6 +572,9 @@ class FaceEmbedder(YoloFaceBranch):
                 for i, r in zip(sub, eng.collect(pend)):
                     spec[i] = r
             lap("det_wait")
+            if self._fb_prefetch:
+                self._prefetch_fallbacks(frames_c, imgs, spec, spec_dyn)
+                lap("fallback_prefetch")
             launch_det(ci + ahead)
             lap("det_launch")
             for i in frames_c:
@@ -467,6 +598,7 @@ class FaceEmbedder(YoloFaceBranch):
         if jobs:
             emb_pending.append(self._embed_launch(imgs, jobs, len(emb_pending)))
         lap("embed_launch")
+        self._fb_cache = {}
         out: List[list] = [[] for _ in range(n)]
         for pend in emb_pending:
             self._embed_collect(pend, out)
@@ -578,9 +710,9 @@ class FaceEmbedder(YoloFaceBranch):
                 if s == 1.0:
                     continue
                 try:
-                    img_s = self._dev_resize(im, "tta", fx=s, fy=s, area=s < 1.0)
                     dyn_s = _round32(min(self._heavy_cap, max(320, int(dyn * s))))
-                    bb_s, kp_s = self._detect_once(img_s, dyn_s, probe_conf)
+                    bb_s, kp_s = self._fb_detect(im, ("tta", s), dyn_s, probe_conf,
+                                                 lambda: self._dev_resize(im, "tta", fx=s, fy=s, area=s < 1.0))
                 except Exception:
                     bb_s, kp_s = None, None
                 if bb_s is None or len(bb_s) == 0:
@@ -599,8 +731,8 @@ class FaceEmbedder(YoloFaceBranch):
                 pad = int(round(min(64, float(self.scrfd_edge_pad_frac) * max(W0, H0))))
                 if pad > 0:
                     try:
-                        img_p = self._dev_rotate_pad(im, 0, pad, key="edgepad")
-                        bb_p, kp_p = self._detect_once(img_p, dyn, probe_conf)
+                        bb_p, kp_p = self._fb_detect(im, ("pad", pad), dyn, probe_conf,
+                                                     lambda: self._dev_rotate_pad(im, 0, pad, key="edgepad"))
                     except Exception:
                         bb_p, kp_p = None, None
                     if bb_p is not None and len(bb_p) > 0:
@@ -655,17 +787,17 @@ class FaceEmbedder(YoloFaceBranch):
             else:
                 rot_seq = (90, 270, 180)
             for deg in rot_seq:
-                rimg_probe = self._dev_rotate_pad(im, deg, 0, key="rot_probe")
                 probe_conf = max(0.02, float(getattr(self, "_probe_conf", 0.02)))
                 probe_dyn = _round32(max(320, min(dyn, int(getattr(self, "_prescan_probe_imgsz", 384)))))
-                probe_boxes, _ = self._detect_once(rimg_probe, probe_dyn, probe_conf)
+                probe_boxes, _ = self._fb_detect(im, ("rot", deg, 0), probe_dyn, probe_conf,
+                                                 lambda: self._dev_rotate_pad(im, deg, 0, key="rot_probe"))
                 probe_hits = len(probe_boxes) if probe_boxes is not None else 0
                 do_heavy = (probe_hits > 0) or (self._fast_prescan and self._prescan_escalate) or \
                     (not self._fast_prescan)
                 if self._fast_prescan and probe_hits == 0:
                     continue
                 pad = 24
-                rimg = self._dev_rotate_pad(im, deg, pad, key="rot_heavy")
+                rimg_make = lambda: self._dev_rotate_pad(im, deg, pad, key="rot_heavy")
                 if self._fast_prescan:
                     heavy = heavy180 if deg == 180 else heavy90
                     override = getattr(self, "_high_180" if deg == 180 else "_high_90", None)
@@ -683,7 +815,7 @@ class FaceEmbedder(YoloFaceBranch):
                 conf_deg = max(0.10, float(self.conf) * (0.8 if deg in (90, 270) else 0.6))
                 rb = rk = None
                 for det_size in det_sizes:
-                    rb, rk = self._detect_once(rimg, det_size, conf_deg)
+                    rb, rk = self._fb_detect(im, ("rot", deg, pad), det_size, conf_deg, rimg_make)
                     if rb is not None and len(rb) > 0:
                         break
                     rb = rk = None

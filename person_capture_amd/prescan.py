@@ -77,7 +77,7 @@ class SampleRecord:
 
 class _LoopState:
     __slots__ = ("active", "start", "neg_run", "fd9_streak", "last_add_sample", "spans", "bank_list", "bank",
-                 "processed", "added")
+                 "processed", "added", "last_found")
 
     def __init__(self, ref_feat):
         if ref_feat is None:
@@ -97,6 +97,7 @@ class _LoopState:
         self.spans: List[Tuple[int, int]] = []
         self.processed = 0
         self.added = 0
+        self.last_found = False   # did the last extracted sample have a face with a finite fd
 
     def copy(self) -> "_LoopState":
         c = _LoopState.__new__(_LoopState)
@@ -168,6 +169,8 @@ class PrescanRunner:
                         st.last_add_sample = sample_idx
                         st.added += action == "added"
         st.fd9_streak = st.fd9_streak + 1 if best >= 8.99 else 0
+        if extracted:
+            st.last_found = best < 8.99
         stride = max(1, int(c.prescan_stride))
         pad = int(round(c.prescan_pad_sec * self.fps))
         min_len = int(round(c.prescan_min_segment_sec * self.fps))
@@ -214,8 +217,9 @@ class PrescanRunner:
             for j in range(k, min(len(samples), k + self.batch)):
                 skip, _ = self._gate(sim)
                 plan.append((j, skip))
-                # regime assumption: idle stays without a match, a span stays open with one
-                sim.fd9_streak = sim.fd9_streak + 1 if not sim.active else 0
+                # regime assumption: the last extracted sample's outcome repeats (faces with a finite
+                # distance keep the fd9 streak at 0, an empty sample grows it; skipped samples grow it)
+                sim.fd9_streak = 0 if (not skip and sim.last_found) else sim.fd9_streak + 1
             active0 = st.active
             f._prescan_rr_mode = "full" if active0 else "rr"
             f.set_prescan_hint(escalate=active0)

@@ -187,7 +187,8 @@ def test_scrfd_fallback_branches(gpu_ctx, monkeypatch):
     o.rot_every_n, o.rot_after_hit_frames = 3, 6
     frames = fallback_sequence()
     got, ref, traces = _run(fe, o, frames)
-    print("branches:", sorted(traces))
+    print("branches:", sorted(traces), "fallback detections prefetched/inline:", fe.fb_stats)
+    assert fe.fb_stats[0] > 0   # the batched speculative prefetch served some of them
     for b in ("tta0.75", "tta0.6", "tta1.25", "edgepad", "rot90", "rot270", "rot180", "eyeroll",
               "size512", "size1280", "size1536"):
         assert b in traces, b
@@ -205,8 +206,11 @@ def test_prescan_fast_branches(gpu_ctx, monkeypatch):
     o = op.OracleFaceEmbedder(fe._scrfd_params, "2.5g", fe._arc_params, 50, conf=0.5, rot_phase=id(fe) & 7)
     o._fast_prescan = True
     frames = prescan_sequence()
+    fe.configure_rotation_strategy(adaptive=False)   # as Processor._prescan does (gui_app.py:1188)
+    o.rot_adaptive = False
     got, ref, traces = _run(fe, o, frames)
-    print("branches:", sorted(traces))
+    print("branches:", sorted(traces), "fallback detections prefetched/inline:", fe.fb_stats)
+    assert fe.fb_stats[0] > 0
     for b in ("rot90", "rot270", "size384", "size1536"):
         assert b in traces, b
     assert "tta0.75" not in traces and "edgepad" not in traces

@@ -18,6 +18,7 @@ SHAPES = [
     ("gemm_1x1_2304", 256, 14, 2304, 256, 1, 1),
     ("s2_3x3_128", 256, 28, 128, 128, 3, 1),
     ("s1_3x3_64", 256, 56, 64, 64, 3, 1),
+    ("s0_3x3_64_112", 256, 112, 64, 64, 3, 1),
     ("s4_3x3_512", 256, 7, 512, 512, 3, 1),
     ("sc_160_64", 64, 160, 64, 64, 3, 1),
     ("sc_80_96", 64, 80, 96, 96, 3, 1),
