@@ -104,6 +104,40 @@ class _DevImage:
         self.ptr, self.H, self.W, self.stride, self._buf = int(ptr), int(H), int(W), int(stride), buf
 
 
+def cv_resize_into(ctx: GpuContext, img: _DevImage, p: dict, d_dst: int) -> None:
+    """Run the cv2.resize kernel imageops.resize_plan chose, writing new_h x new_w x 3 contiguous at d_dst."""
+    lib, h = ctx.lib, ctx.handle
+    nw, nh = p["new_w"], p["new_h"]
+    kind = p["kind"]
+    if kind == "copy":
+        check(lib.pc_copy_2d(h, C.c_void_p(d_dst), nw * 3, C.c_void_p(img.ptr), img.stride, nw * 3, nh), h, "copy_2d")
+    elif kind == "area_fast":
+        check(lib.pc_resize_area_fast(h, img.ptr, img.stride, p["isx"], p["isy"], d_dst, nh, nw), h,
+              "resize_area_fast")
+    elif kind == "area":
+        (xt, xs), (yt, ys) = imageops.area_tables(img.W, nw, p["scale_x"]), imageops.area_tables(img.H, nh, p["scale_y"])
+        check(lib.pc_resize_area(h, img.ptr, img.stride, xt, xs, len(xt), yt, ys, len(yt), d_dst, nh, nw), h,
+              "resize_area")
+    else:
+        d = ResizeDesc()
+        d.d_src, d.H, d.W, d.row_stride = img.ptr, img.H, img.W, img.stride
+        d.new_w, d.new_h, d.scale_x, d.scale_y = nw, nh, p["scale_x"], p["scale_y"]
+        d.inv_x, d.inv_y, d.area_mode = p["inv_x"], p["inv_y"], p["area_mode"]
+        d.simd_end = opencv_vresize_simd_end(nw * 3)
+        d.d_dst = d_dst
+        check(lib.pc_resize_linear(h, (ResizeDesc * 1)(d), 1), h, "resize_linear")
+
+
+def dev_resize(ctx: GpuContext, img: _DevImage, key: str, dsize: Optional[Tuple[int, int]] = None, fx: float = 0.0,
+               fy: float = 0.0, area: bool = False) -> _DevImage:
+    """cv2.resize(img, dsize or None, fx, fy, INTER_AREA if area else INTER_LINEAR) on the device, into
+    the context's scratch buffer `key`."""
+    p = imageops.resize_plan(img.H, img.W, dsize, fx, fy, area)
+    buf = ctx.scratch(key, p["new_w"] * p["new_h"] * 3)
+    cv_resize_into(ctx, img, p, buf.ptr)
+    return _DevImage(buf.ptr, p["new_h"], p["new_w"], p["new_w"] * 3, buf)
+
+
 class FaceEmbedder(YoloFaceBranch):
     """Face detection (SCRFD, or the YOLOv8-face default) + ArcFace identity embedding on the MI355X.
     Returns list of dicts: {'bbox': np.int32[x1,y1,x2,y2], 'feat': np.float32[D], 'quality': float}."""
@@ -428,34 +462,10 @@ class FaceEmbedder(YoloFaceBranch):
     def _dev_resize(self, img: _DevImage, key: str, dsize: Optional[Tuple[int, int]] = None, fx: float = 0.0,
                     fy: float = 0.0, area: bool = False) -> _DevImage:
         """cv2.resize(img, dsize or None, fx, fy, INTER_AREA if area else INTER_LINEAR) on the device."""
-        p = imageops.resize_plan(img.H, img.W, dsize, fx, fy, area)
-        buf = self._ctx.scratch(key, p["new_w"] * p["new_h"] * 3)
-        self._cv_resize(img, p, buf.ptr)
-        return _DevImage(buf.ptr, p["new_h"], p["new_w"], p["new_w"] * 3, buf)
+        return dev_resize(self._ctx, img, key, dsize, fx, fy, area)
 
     def _cv_resize(self, img: _DevImage, p: dict, d_dst: int) -> None:
-        """Run the kernel imageops.resize_plan chose, writing new_h x new_w x 3 contiguous at d_dst."""
-        lib, h = self._ctx.lib, self._ctx.handle
-        nw, nh = p["new_w"], p["new_h"]
-        kind = p["kind"]
-        if kind == "copy":
-            check(lib.pc_copy_2d(h, C.c_void_p(d_dst), nw * 3, C.c_void_p(img.ptr), img.stride, nw * 3, nh), h,
-                  "copy_2d")
-        elif kind == "area_fast":
-            check(lib.pc_resize_area_fast(h, img.ptr, img.stride, p["isx"], p["isy"], d_dst, nh, nw), h,
-                  "resize_area_fast")
-        elif kind == "area":
-            (xt, xs), (yt, ys) = imageops.area_tables(img.W, nw, p["scale_x"]), imageops.area_tables(img.H, nh, p["scale_y"])
-            check(lib.pc_resize_area(h, img.ptr, img.stride, xt, xs, len(xt), yt, ys, len(yt), d_dst, nh, nw), h,
-                  "resize_area")
-        else:
-            d = ResizeDesc()
-            d.d_src, d.H, d.W, d.row_stride = img.ptr, img.H, img.W, img.stride
-            d.new_w, d.new_h, d.scale_x, d.scale_y = nw, nh, p["scale_x"], p["scale_y"]
-            d.inv_x, d.inv_y, d.area_mode = p["inv_x"], p["inv_y"], p["area_mode"]
-            d.simd_end = opencv_vresize_simd_end(nw * 3)
-            d.d_dst = d_dst
-            check(lib.pc_resize_linear(h, (ResizeDesc * 1)(d), 1), h, "resize_linear")
+        cv_resize_into(self._ctx, img, p, d_dst)
 
     # ------------------------------------------------------------------ static helpers (reference API)
     _ARC_DST = imageops.ARC_DST

@@ -34,6 +34,9 @@ def _stub_cv2():
     def cvt(img, code):
         if code == 4:
             return np.ascontiguousarray(img[..., ::-1])
+        if code == 6:   # BGR2GRAY: only called on B == G == R frames below, where it is exactly channel 0
+            assert np.array_equal(img[..., 0], img[..., 1]) and np.array_equal(img[..., 0], img[..., 2])
+            return np.ascontiguousarray(img[..., 0])
         raise NotImplementedError(code)
     cv2.cvtColor = cvt
     cv2.flip = lambda img, f: np.ascontiguousarray(img[:, ::-1])
@@ -202,6 +205,43 @@ def main():
             comb.append(np.nan if v is None else v)
     np.savez_compressed(os.path.join(OUT, "utils_main.npz"), a=a, b=b, cosdist=cd, l2=l2,
                         ebr_in=np.array(ebr_in), ebr_out=np.array(ebr_out), combine=np.array(comb, np.float64))
+    # ---- post-match geometry (main.py:17-83, utils.py:152-197) ----
+    rng2 = np.random.default_rng(20260516)
+    esm_in, esm_out = [], []
+    for t in range(400):
+        W, H = int(rng2.integers(200, 3000)), int(rng2.integers(200, 2000))
+        x1, y1 = int(rng2.integers(0, W - 20)), int(rng2.integers(0, H - 20))
+        x2, y2 = int(rng2.integers(x1 + 10, W + 1)), int(rng2.integers(y1 + 10, H + 1))
+        ratio = ["2:3", "16:9", "1:1", "4:5"][t % 4]
+        fb = None
+        if t % 3:
+            fx1, fy1 = float(rng2.uniform(x1, x2)), float(rng2.uniform(y1, y2))
+            fb = (fx1, fy1, fx1 + float(rng2.uniform(4, 400)), fy1 + float(rng2.uniform(4, 400)))
+        r = M._enforce_scale_and_margins((x1, y1, x2, y2), ratio, W, H, fb)
+        esm_in.append([x1, y1, x2, y2, t % 4, W, H] + (list(fb) if fb else [-1, -1, -1, -1]))
+        esm_out.append(r)
+    clip_in, clip_out = [], []
+    for t in range(200):
+        W, H = int(rng2.integers(50, 2000)), int(rng2.integers(50, 2000))
+        b = [float(rng2.uniform(-300, W + 300)), float(rng2.uniform(-300, H + 300))]
+        b += [b[0] + float(rng2.uniform(1, W)), b[1] + float(rng2.uniform(1, H))]
+        clip_in.append(b + [W, H])
+        clip_out.append(M._clip_to_frame(*b, W, H))
+    borders, bb_out = [], []
+    for t in range(24):
+        H, W = int(rng2.integers(60, 400)), int(rng2.integers(60, 400))
+        g = rng2.integers(30, 256, (H, W), dtype=np.uint8)
+        top, bot, left, right = (int(rng2.integers(0, 40)) for _ in range(4))
+        dark = int(rng2.integers(0, 12))
+        g[:top] = dark; g[H - bot:] = dark; g[:, :left] = dark; g[:, W - right:] = dark
+        img = np.repeat(g[..., None], 3, axis=2)
+        thr = [10, 5, 20][t % 3]
+        borders.append(img)
+        bb_out.append(list(U.detect_black_borders(img, thr=thr)) + [thr])
+    np.savez_compressed(os.path.join(OUT, "postmatch.npz"), esm_in=np.array(esm_in, np.float64),
+                        esm_out=np.array(esm_out, np.int64), clip_in=np.array(clip_in, np.float64),
+                        clip_out=np.array(clip_out, np.int64), bb_out=np.array(bb_out, np.int64),
+                        **{f"border{i}": b for i, b in enumerate(borders)})
     print("golden vectors written to", OUT)
 
 
