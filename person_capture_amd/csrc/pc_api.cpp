@@ -27,6 +27,10 @@ int conv_fast_valid(int cfg, int rowb);
 int conv_halo_num_cfgs();
 int conv_halo_tile(int cfg, int* bc, int* bp);
 int conv_halo_fits(int cfg, int KH, int KW, int W);
+hipError_t conv_t2d_launch(const ConvParams& p, hipStream_t s);
+int conv_t2d_supported(int cin, int npad, int KH, int KW, int stride, int pad, int act, int out_f32, int ycs,
+                       int ycoff);
+int conv_t2d_rows(int npad);
 hipError_t splitk_reduce_launch(int f32, const float* part, int splitk, int M, int npad, int cout, const float* bias,
                                 const float* slope, int act, void* y, int ycs, int out_f32, hipStream_t s);
 hipError_t stem_launch(int f32, const StemParams& p, hipStream_t s);
@@ -331,7 +335,7 @@ enum { OP_CONV = 1, OP_STEM = 2, OP_MAXPOOL = 3, OP_UPSAMPLE = 4, OP_LAYERNORM =
 struct NetBuf { long long elems; int is_f32; void* d = nullptr; };
 struct NetTensor { int buf, H, W, C, cs, coff, is_f32; };
 struct NetOp { int w[32]; };
-struct ConvPlan { int rowb, cfg, splitk, halo = -1, fast = -1; long long M_per_image; double flops_per_image; };
+struct ConvPlan { int rowb, cfg, splitk, halo = -1, fast = -1, t2d = -1; long long M_per_image; double flops_per_image; };
 // A stem (tiny Cin) runs as im2col + a 1x1 MFMA conv over 32-element K rows.
 struct StemPlan {
   int use_mfma = 0, npad = 0, cfg = 0, rowb = 0, cin_true = 0;
@@ -518,6 +522,27 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl) {
       }
       pl.fast = best;
       if (best >= 0) { pl.halo = -1; pl.rowb = best_rowb; }
+    }
+  }
+  // 3x3 stride-1 convs over 32/64 channels run on the 2-D block kernel with register-
+  // resident weights (pc_conv_t2d.hip, f16) when its 16-pixel-wide blocks cover the
+  // image with little waste. PC_CONV_T2D=0 disables, =2 forces wherever it can run.
+  pl.t2d = -1;
+  {
+    const char* e = getenv("PC_CONV_T2D");
+    const int mode = e ? atoi(e) : ((getenv("PC_CONV_CFG") || getenv("PC_CONV_HALO") || getenv("PC_CONV_FAST")) ? 0 : 1);
+    const NetTensor& X = n->tens[w[3]];
+    if (mode > 0 && !n->f32 && nseg == 1 && pl.splitk == 1 && X.H == Y.H && X.W == Y.W &&
+        conv_t2d_supported(X.C, npad, w[4], w[5], w[6], w[7], w[20], Y.is_f32, Y.cs, Y.coff) && w[15] >= 9LL * X.C &&
+        (double)X.H * X.W * n->max_batch * X.cs * esz + kZeroTail < 4294967296.0 &&
+        (double)M < 2147483647.0) {
+      const int th = conv_t2d_rows(npad);
+      const double cover = (double)Y.H * Y.W / ((double)((Y.H + th - 1) / th * th) * ((Y.W + 15) / 16 * 16));
+      if (mode == 2 || cover >= 0.75) {
+        pl.t2d = 0;
+        pl.fast = -1;
+        pl.halo = -1;
+      }
     }
   }
   if (Y.C > npad) return fail(n->ctx, PC_ERR_FORMAT, "conv output tensor wider than npad");
@@ -813,7 +838,9 @@ static int run_ops(pc_net* n, int N) {
       p.partial = n->partial;
       p.zero = c->zero;
       if (const char* e = getenv("PC_CONV_DBG")) p.dbg = atoi(e);
-      if (pl.fast >= 0) {
+      if (pl.t2d >= 0) {
+        HIPCHK(c, conv_t2d_launch(p, s));
+      } else if (pl.fast >= 0) {
         HIPCHK(c, conv_fast_launch(n->f32, pl.rowb, pl.fast, p, s));
       } else if (pl.halo >= 0) {
         HIPCHK(c, conv_halo_launch(n->f32, pl.halo, p, s));
@@ -959,7 +986,8 @@ extern "C" int pc_net_profile_ops(pc_net* n, double* out, int max_recs) {
     double* o = out + 6 * k++;
     const bool conv = r.op >= 0 && n->ops[r.op].w[0] == OP_CONV;
     o[0] = r.op; o[1] = r.kind; o[2] = ms; o[3] = r.flops;
-    o[4] = conv ? (n->plans[r.op].fast >= 0 ? 100 + n->plans[r.op].fast : n->plans[r.op].halo) : -1;
+    o[4] = conv ? (n->plans[r.op].t2d >= 0 ? 200 + n->plans[r.op].t2d
+                  : n->plans[r.op].fast >= 0 ? 100 + n->plans[r.op].fast : n->plans[r.op].halo) : -1;
     o[5] = conv ? n->plans[r.op].cfg : -1;
   }
   return k;

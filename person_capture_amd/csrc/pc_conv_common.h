@@ -104,19 +104,25 @@ __device__ __forceinline__ void vmcnt_wait(int n) {
 
 // Fused epilogue shared by the conv kernels: acc[a][b] is the 16x16 fragment of
 // channels c0 + wr*WTC + a*16 + (lane>>4)*4 + j, pixels p0 + wc*WTP + b*16 + (lane&15).
-template <typename T, int TC, int TP, int WTC, int WTP>
-__device__ __forceinline__ void conv_epilogue(const ConvParams& p, f32x4 (&acc)[TC][TP], int c0, int p0, int wr,
-                                              int wc, int lane, int z) {
+// conv_epilogue_map: the same with the pixel of fragment column b given by pixf(b)
+// (-1: not an output pixel) and the wave's first channel cw = c0 + wr*WTC - for
+// kernels whose pixel tiles are not linear runs (pc_conv_t2d.hip: 2-D blocks).
+// PIN: one fragment column at a time (no loads hoisted across columns) - for kernels
+// that hold many registers live through the epilogue.
+template <typename T, int TC, int TP, bool PIN = false, typename PixF>
+__device__ __forceinline__ void conv_epilogue_map(const ConvParams& p, f32x4 (&acc)[TC][TP], int cw, int lane, int z,
+                                                  PixF&& pixf) {
   const int chq = (lane >> 4) * 4;
   // compile-time (a, b) everywhere: a runtime fragment index would demote acc to scratch
   static_for<TP>([&](auto bc) __attribute__((always_inline)) {
     constexpr int b = decltype(bc)::value;
-    const int pix = p0 + wc * WTP + b * 16 + (lane & 15);
-    if (pix >= p.M) return;
+    if constexpr (PIN) __builtin_amdgcn_sched_barrier(0);
+    const int pix = pixf(b);
+    if (pix < 0) return;
     if (p.splitk > 1) {
       static_for<TC>([&](auto ac) __attribute__((always_inline)) {
         constexpr int a = decltype(ac)::value;
-        const int ch = c0 + wr * WTC + a * 16 + chq;
+        const int ch = cw + a * 16 + chq;
         float* dst = p.partial + ((long long)z * p.M + pix) * p.npad + ch;
         *reinterpret_cast<f32x4*>(dst) = acc[a][b];
       });
@@ -144,7 +150,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, f32x4 (&acc)[
     if (p.res_mode == RES_UP2) rpix = ((long long)n * p.rH + (oh >> 1)) * p.rW + (ow >> 1);
     static_for<TC>([&](auto ac) __attribute__((always_inline)) {
       constexpr int a = decltype(ac)::value;
-      const int ch = c0 + wr * WTC + a * 16 + chq;
+      const int ch = cw + a * 16 + chq;
       if (ch >= p.cwrite) return;
       const int nv = min(4, p.cwrite - ch);
       float v[4] = {acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]};
@@ -179,6 +185,15 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, f32x4 (&acc)[
       else
         store4<T>(reinterpret_cast<T*>(p.y) + (long long)pix * p.ycs + ch, v, nv);
     });
+  });
+}
+
+template <typename T, int TC, int TP, int WTC, int WTP>
+__device__ __forceinline__ void conv_epilogue(const ConvParams& p, f32x4 (&acc)[TC][TP], int c0, int p0, int wr,
+                                              int wc, int lane, int z) {
+  conv_epilogue_map<T, TC, TP>(p, acc, c0 + wr * WTC, lane, z, [&](int b) __attribute__((always_inline)) {
+    const int pix = p0 + wc * WTP + b * 16 + (lane & 15);
+    return pix < p.M ? pix : -1;
   });
 }
 

@@ -1,0 +1,373 @@
+// 3x3 stride-1 "same" convolution over 2-D pixel blocks with weights held in
+// registers (gfx950) - the small-channel trunk layers (Cin 32/64 -> 32/64 channels:
+// SCRFD's 320x320 / 160x160 / 80x80 stages, IResNet's 112x112 / 56x56 stage).
+//
+// Why a third conv kernel: at 32-64 channels the implicit-GEMM kernels (pc_conv_fast)
+// stage one im2col row per (pixel, tap), i.e. every input pixel moves L2 -> LDS nine
+// times, and their K loop is only 9-18 tiles long, so prologue, barriers and the
+// per-tile epilogue dominate (SCRFD 320x320x32: 157 TF/s; 160x160x64: 340 TF/s). The
+// linear-run halo kernel (pc_conv_halo) stages each pixel once but its halo is the
+// pixel run +- (W+1), 2-3x the tile on wide images. Here:
+//
+//  * a workgroup (8 waves) is persistent over output blocks of TH x 16 pixels of one
+//    image (TH = 32 / 16 for 32 / 64 output channels); the block's input halo
+//    (TH+2) x 18 pixels x Cin is staged into LDS once, by LDS-DMA, double-buffered:
+//    block i+1's halo is in flight while block i is multiplied;
+//  * the whole weight matrix of a wave's 32 output channels (9 x Cin of K) lives in
+//    VGPRs as MFMA A-fragments for the life of the workgroup, so the only LDS traffic
+//    is one ds_read_b128 B-fragment per 2 MFMAs;
+//  * halo rows are 64 B (one 32-channel chunk), row pitch 24 pixels; 16-byte chunk c of
+//    row r sits at c ^ ((r >> 1) & 3) (conflict-free ds_read_b128 for any 16 consecutive
+//    rows, pc_conv_halo.hip), and with the pitch a multiple of 8 a tap-row shift keeps
+//    the swizzle, so every tap's fragment address is one of 3 per-lane bases per
+//    fragment plus a compile-time immediate;
+//  * one barrier per block; the epilogue (bias / border-class bias, activation,
+//    residual, channel padding; conv_epilogue_map) stores straight from the
+//    accumulators after the barrier, while the next block's DMA is in flight.
+//
+// K order (tap-major, 32-channel chunks, lane group fq = 8-channel slice) is the
+// implicit-GEMM kernels' order, so results are bit-identical to conv_fast's.
+#include "pc_conv_common.h"
+
+namespace pc {
+
+// B-fragment reads of one K step: TP rows P pixels apart, compile-time offsets
+template <int STRIDE, int IMM, int... I>
+__device__ __forceinline__ void t2d_read_frags(const char* a0, f16x8* fb, std::integer_sequence<int, I...>) {
+  ((fb[I] = *reinterpret_cast<const f16x8*>(a0 + IMM + I * STRIDE)), ...);
+}
+// NCH: 32-channel input chunks (Cin = 32*NCH); G: 32-channel output groups (npad = 32*G);
+// NW waves, each owning TP output rows of 16 pixels x 32 output channels.
+template <int NCH, int G, int NW, int TP>
+__global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, int ntx, int ntiles) {
+  constexpr int TW = 16, P = 24, TC = 2;
+  constexpr int TH = TP * NW / G;             // output rows per block
+  constexpr int NRP = (TH + 2) * P;           // halo rows per channel chunk
+  constexpr int NINST = NRP / 16;             // DMA instructions per chunk
+  constexpr int BUFB = NCH * NRP * 64;        // one halo buffer
+  constexpr int NKS = 9 * NCH;                // 32-element K steps
+  constexpr int TB = 10 * 64;                 // bias classes [9][64] + slopes [64] (f32)
+  static_assert(NRP % 16 == 0 && P % 8 == 0 && P >= TW + 2 && (TP == 4 || TP == 8), "halo geometry");
+  static_assert(2 * BUFB + TB * 4 + TH * 16 * (64 * G + 16) <= 163840, "LDS");
+  static_assert(NW % G == 0, "wave roles");
+
+  // two halo buffers as two objects: the compiler then sees that a ds_read of one
+  // cannot alias the LDS-DMA into the other and does not drain vmcnt before it
+  __shared__ __attribute__((aligned(16))) char hbuf0[BUFB];
+  __shared__ __attribute__((aligned(16))) char hbuf1[BUFB];
+  __shared__ __attribute__((aligned(16))) float tab[TB];
+  // output staging: [pixel][npad] f16 rows, pitch padded by 16 B (conflict-free 8-byte
+  // fragment writes, 16-byte aligned row reads)
+  constexpr int NPAD = 32 * G, PITCH = NPAD * 2 + 16, BPIX = TH * TW, CH8 = NPAD / 8;
+  constexpr int SIT = BPIX * CH8 / (64 * NW);   // 16-byte chunks per thread per block
+  static_assert(SIT * 64 * NW == BPIX * CH8, "staging split");
+  __shared__ __attribute__((aligned(16))) char stg[BPIX * PITCH];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  __builtin_assume(wave >= 0 && wave < NW);
+  const int g = wave % G, pg = wave / G;      // output-channel group, pixel-row group
+  const int fr = lane & 15, fq = lane >> 4;
+  const ConvSeg& S = p.seg[0];
+  const char* xs = reinterpret_cast<const char*>(S.x);
+  const unsigned xrow = (unsigned)S.cs * 2u;
+  const int H = S.H, W = S.W;
+
+  // blocks of one XCD form a contiguous range (neighbouring halos share its L2)
+  int t_hi = ntiles, t_first = blockIdx.x, t_step = gridDim.x;
+  if ((gridDim.x & 7) == 0) {
+    const int xcd = blockIdx.x & 7;
+    const int t_lo = (int)((long long)xcd * ntiles / 8);
+    t_hi = (int)((long long)(xcd + 1) * ntiles / 8);
+    t_first = t_lo + (blockIdx.x >> 3);
+    t_step = gridDim.x >> 3;
+  }
+  if (t_first >= t_hi) return;   // whole workgroup: nothing issued, no barrier pending
+
+  auto decode = [&](int tile, int& n, int& ty, int& tx) __attribute__((always_inline)) {
+    const int per = nty * ntx;
+    n = tile / per;
+    const int r = tile - n * per;
+    ty = r / ntx;
+    tx = r - ty * ntx;
+  };
+
+  // halo of block `tile` -> buffer dst (rows past the image / pitch padding read zeros)
+  constexpr int NDMA = NCH * NINST, PERW = (NDMA + NW - 1) / NW;
+  auto dma = [&](int tile, char* dst) __attribute__((always_inline)) {
+    int n, ty, tx;
+    decode(tile, n, ty, tx);
+    const int oy0 = ty * TH - 1, ox0 = tx * TW - 1;
+    static_for<PERW>([&](auto kc) __attribute__((always_inline)) {
+      const int i = decltype(kc)::value * NW + wave;
+      if (NDMA % NW == 0 || i < NDMA) {
+        const int j = i / NINST, gi = i - j * NINST;
+        const int h = gi * 16 + (lane >> 2);
+        const int hy = h / P, hx = h - hy * P;
+        const int iy = oy0 + hy, ix = ox0 + hx;
+        const unsigned sc = (unsigned)(((lane & 3) ^ ((h >> 1) & 3)) << 4);
+        const bool ok = hx < TW + 2 && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+        const unsigned pix = (unsigned)((n * H + iy) * W + ix);
+        unsigned off = ok ? pix * xrow + sc : S.zero_off + sc;
+        asm volatile("" : "+v"(off));
+        __builtin_amdgcn_global_load_lds((gptr_t)(xs + j * 64 + off),
+                                         (lds_ptr_t)(dst + j * NRP * 64 + gi * 1024), 16, 0, 0);
+      }
+    });
+  };
+
+  int tile = t_first;
+  dma(tile, hbuf0);
+
+  // epilogue tables: bias of border class c (BIAS_BORDER9; BIAS_CHANNEL: every class the
+  // same row) at [c*64 + ch], negative-side slopes at [576 + ch] (PReLU a, ReLU 0, none 1)
+  for (int i = threadIdx.x; i < TB; i += 64 * NW) {
+    const int c = i & 63, cls = i >> 6;
+    float v = 0.f;
+    if (c < p.npad) {
+      if (cls < 9) {
+        if (p.bias_mode == BIAS_CHANNEL) v = p.bias[c];
+        else if (p.bias_mode == BIAS_BORDER9) v = p.bias[cls * p.npad + c];
+      } else {   // negative-side slope of the piecewise-linear activations
+        v = p.act == ACT_PRELU ? p.slope[c] : (p.act == ACT_RELU ? 0.f : 1.f);
+      }
+    }
+    tab[i] = v;
+  }
+
+  // weights -> registers: A fragment (ks, a) = rows g*32 + a*16 + fr, K ks*32 + fq*8 .. +7
+  f16x8 wa[NKS][TC];
+  {
+    const char* wb = reinterpret_cast<const char*>(p.w);
+#pragma unroll
+    for (int a = 0; a < TC; ++a) {
+      const char* row = wb + (long long)(g * 32 + a * 16 + fr) * p.ktot * 2 + fq * 16;
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) wa[ks][a] = *reinterpret_cast<const f16x8*>(row + ks * 64);
+    }
+    // retire the weight loads here, visibly to the compiler: otherwise its wait for them
+    // lands before the first MFMA inside the block loop as a vmcnt(0), which would also
+    // wait for the next block's halo DMA
+#pragma unroll
+    for (int a = 0; a < TC; ++a)
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) asm volatile("" : "+v"(wa[ks][a]));
+  }
+
+  auto bar = [&]() __attribute__((always_inline)) {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  bar();
+
+  const bool has_res = p.res_mode != RES_NONE;
+  const bool border = p.bias_mode == BIAS_BORDER9;
+  const int chq = fq * 4;
+
+  f32x4 acc[TC][TP];
+  // one block: multiply from `cur` while the next block's halo goes into `oth`
+  auto block = [&](const char* cur, char* oth) __attribute__((always_inline)) {
+    const int nxt = tile + t_step;
+    if (nxt < t_hi && !(p.dbg & 1)) dma(nxt, oth);   // dbg (tuning only): 1 no halo DMA
+
+    int n, ty, tx;
+    decode(tile, n, ty, tx);
+    const int oy0 = ty * TH + pg * TP, ox = tx * TW + fr;
+    const bool colok = ox < W;
+
+    // residual of this block's pixels, requested now so it arrives during the MFMAs
+    // (not zero-filled when unused: writing registers that a load of the previous block
+    // targeted would make the compiler drain vmcnt - the next halo - right here)
+    f16x4 rv[TP][TC];
+    // (addresses of pixels outside the image are clamped, not branched around: a load
+    // under a divergent branch merges into a phi that waits for it right there)
+    if (has_res) {
+#pragma unroll
+      for (int t = 0; t < TP; ++t) {
+        const int oy = oy0 + t;
+        const bool ok = colok && oy < H;
+        const int qy = ok ? oy : 0, qx = ok ? ox : 0;
+        const long long rpix = p.res_mode == RES_UP2 ? ((long long)n * p.rH + (qy >> 1)) * p.rW + (qx >> 1)
+                                                     : ((long long)n * H + qy) * W + qx;
+        const f16* rp = reinterpret_cast<const f16*>(p.res) + rpix * p.rcs;
+#pragma unroll
+        for (int a = 0; a < TC; ++a) {
+          const int ch = g * 32 + a * 16 + chq;
+          if ((p.cwrite & 3) == 0) {   // uniform: whole 4-channel groups
+            rv[t][a] = *reinterpret_cast<const f16x4*>(rp + min(ch, p.cwrite - 4));
+          } else {
+            rv[t][a] = f16x4{};
+            for (int j = 0; j < 4; ++j)
+              if (ch + j < p.cwrite) rv[t][a][j] = rp[ch + j];
+          }
+        }
+      }
+    }
+
+#pragma unroll
+    for (int a = 0; a < TC; ++a)
+#pragma unroll
+      for (int t = 0; t < TP; ++t) acc[a][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // per-lane fragment bases for tap column tw; fragment t (output row pg*TP + t) is
+    // t*P rows further, and as P*t/2 is a multiple of 4 it keeps the swizzle: immediate
+    unsigned ad[3];
+#pragma unroll
+    for (int tw = 0; tw < 3; ++tw) {
+      const int h = pg * TP * P + tw + fr;
+      ad[tw] = (unsigned)(h * 64 + ((fq ^ ((h >> 1) & 3)) << 4));
+    }
+    // K step ks = (th*3 + tw)*NCH + j; its B fragments are read one step ahead of its
+    // MFMAs (two fragment sets live; the schedule is pinned so the compiler does not
+    // hoist every read of the block and spill the weight registers).
+    f16x8 fb0[TP], fb1[TP];
+    if (!(p.dbg & 2)) static_for<NKS + 1>([&](auto ksc) __attribute__((always_inline)) {
+      constexpr int ks = decltype(ksc)::value - 1;   // -1: prologue read of step 0
+      f16x8(&cur_f)[TP] = (ks & 1) ? fb1 : fb0;
+      f16x8(&nxt_f)[TP] = (ks & 1) ? fb0 : fb1;
+      constexpr int H1 = TP > 4 ? 4 : TP;   // reads issued before the wait
+      if constexpr (ks + 1 < NKS) {
+        constexpr int tap = (ks + 1) / NCH, j = (ks + 1) - tap * NCH;
+        constexpr int th = tap / 3, tw = tap - th * 3;
+        t2d_read_frags<P * 64, j * NRP * 64 + th * P * 64>(cur + ad[tw], nxt_f,
+                                                          std::make_integer_sequence<int, H1>{});
+      }
+      if constexpr (ks + 1 < NKS && TP > H1) {
+        constexpr int tap = (ks + 1) / NCH, j = (ks + 1) - tap * NCH;
+        constexpr int th = tap / 3, tw = tap - th * 3;
+        t2d_read_frags<P * 64, j * NRP * 64 + th * P * 64 + H1 * P * 64>(cur + ad[tw], nxt_f + H1,
+                                                                       std::make_integer_sequence<int, TP - H1>{});
+      }
+      if constexpr (ks >= 0) {
+#pragma unroll
+        for (int a = 0; a < TC; ++a)
+#pragma unroll
+          for (int t = 0; t < TP; ++t)
+            acc[a][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[ks][a], cur_f[t], acc[a][t], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+
+    // next halo landed (own DMAs; also the residual) and every wave is done with `cur`
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+
+    // ---- epilogue: bias (per channel / border class), activation, residual, padding ----
+    f32x4 sl[TC];
+    const int cc = !border ? 0 : (ox == 0 ? 0 : (ox >= W - 1 ? 2 : 1));
+#pragma unroll
+    for (int a = 0; a < TC; ++a) sl[a] = *reinterpret_cast<const f32x4*>(tab + 576 + g * 32 + a * 16 + chq);
+    // finishing: the planner sends only the piecewise-linear activations here (none /
+    // ReLU / PReLU: one select with the per-channel negative slope of the table, 1 / 0 /
+    // a), so the act-before / act-after-residual order is a select, not a branch
+    if (!has_res) {
+#pragma unroll
+      for (int t = 0; t < TP; ++t)
+#pragma unroll
+        for (int a = 0; a < TC; ++a) rv[t][a] = f16x4{};
+    }
+    const bool after = p.act_after_res != 0;
+    // f16 rows through LDS: each pixel's channels leave as whole 16-byte chunks of
+    // contiguous pixel rows (per-fragment 8-byte stores of 16 pixels ran the kernel at a
+    // third of its no-store speed)
+#pragma unroll
+    for (int t = 0; t < TP; ++t) {
+      const int oy = oy0 + t;
+      const int rc = !border ? 0 : (oy == 0 ? 0 : (oy >= H - 1 ? 2 : 1));
+#pragma unroll
+      for (int a = 0; a < TC; ++a) {
+        const int ch = g * 32 + a * 16 + chq;
+        const f32x4 bt = *reinterpret_cast<const f32x4*>(tab + (rc * 3 + cc) * 64 + ch);
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float x = acc[a][t][j] + bt[j];
+          const float r = (float)rv[t][a][j];
+          const float xr = x + r;                                    // act(acc + b + res)
+          const float y1 = xr > 0.f ? xr : xr * sl[a][j];
+          const float y0 = (x > 0.f ? x : x * sl[a][j]) + r;         // act(acc + b) + res
+          v[j] = ch + j < p.cout ? (after ? y1 : y0) : 0.f;          // channel padding stays 0
+        }
+        *reinterpret_cast<f16x4*>(stg + ((pg * TP + t) * TW + fr) * PITCH + ch * 2) =
+            f16x4{(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
+      }
+    }
+    __syncthreads();
+    if (!(p.dbg & 4)) {   // dbg 4 (tuning only): no stores
+      const int cw8 = (p.cwrite + 7) >> 3;
+#pragma unroll
+      for (int k = 0; k < SIT; ++k) {
+        const int idx = threadIdx.x + k * 64 * NW;
+        const int pl = idx / CH8, cq = idx - (idx / CH8) * CH8;
+        const int oy = ty * TH + pl / TW, oxx = tx * TW + (pl & (TW - 1));
+        if (oy >= H || oxx >= W || cq >= cw8) continue;
+        const f16x8 val = *reinterpret_cast<const f16x8*>(stg + pl * PITCH + cq * 16);
+        f16* yp = reinterpret_cast<f16*>(p.y) + (((long long)n * H + oy) * W + oxx) * p.ycs + cq * 8;
+        if (cq * 8 + 8 <= p.cwrite) {
+          *reinterpret_cast<f16x8*>(yp) = val;
+        } else {
+          for (int j = 0; j < 8; ++j)
+            if (cq * 8 + j < p.cwrite) yp[j] = val[j];
+        }
+      }
+    }
+    tile = nxt;
+  };
+  for (;;) {
+    block(hbuf0, hbuf1);
+    if (tile >= t_hi) break;
+    block(hbuf1, hbuf0);
+    if (tile >= t_hi) break;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+
+// (Cin, npad) pairs the kernel is instantiated for, piecewise-linear activations, f16
+// output in whole 16-byte pixel chunks; 0 if the conv cannot run on it
+int conv_t2d_supported(int cin, int npad, int KH, int KW, int stride, int pad, int act, int out_f32, int ycs,
+                       int ycoff) {
+  if (KH != 3 || KW != 3 || stride != 1 || pad != 1) return 0;
+  if (act != ACT_NONE && act != ACT_RELU && act != ACT_PRELU) return 0;
+  if (out_f32 || (ycs & 7) || (ycoff & 7)) return 0;
+  return (cin == 32 && (npad == 32 || npad == 64)) || (cin == 64 && npad == 64);
+}
+
+// output rows per block for npad (the block is TH x 16 pixels)
+int conv_t2d_rows(int npad) { return npad == 32 ? 32 : 16; }
+
+template <int NCH, int G, int NW, int TP>
+static hipError_t launch_t2d(const ConvParams& p, hipStream_t s) {
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+      ncu = 256;
+  }
+  constexpr int TH = TP * NW / G;
+  const int nty = (p.OH + TH - 1) / TH, ntx = (p.OW + 15) / 16;
+  const long long nt = (long long)p.N * nty * ntx;
+  if (nt <= 0 || nt >= (1LL << 31)) return hipErrorInvalidValue;
+  const int grid = (int)std::min<long long>(nt, ncu);
+  hipLaunchKernelGGL((conv_t2d<NCH, G, NW, TP>), dim3(grid), dim3(64 * NW), 0, s, p, nty, ntx, (int)nt);
+  return hipGetLastError();
+}
+
+hipError_t conv_t2d_launch(const ConvParams& p, hipStream_t s) {
+  const ConvSeg& S = p.seg[0];
+  if (p.nseg != 1 || p.splitk != 1 || S.H != p.OH || S.W != p.OW || p.cwrite > p.npad ||
+      !conv_t2d_supported(S.C, p.npad, S.KH, S.KW, S.stride, S.pad, p.act, p.out_f32, p.ycs, 0) ||
+      (reinterpret_cast<uintptr_t>(p.y) & 15) || p.ktot < 9LL * S.C)
+    return hipErrorInvalidValue;
+  // Cin 64: the 144 weight registers leave no room for a second wave per SIMD, so 4
+  // waves of 8 rows each (a block is 16 x 16 pixels either way)
+  if (S.C == 32) return p.npad == 32 ? launch_t2d<1, 1, 8, 4>(p, s) : launch_t2d<1, 2, 8, 4>(p, s);
+  return launch_t2d<2, 2, 4, 8>(p, s);
+}
+
+}  // namespace pc

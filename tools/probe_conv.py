@@ -21,6 +21,8 @@ SHAPES = [
     ("s0_3x3_64_112", 256, 112, 64, 64, 3, 1),
     ("s4_3x3_512", 256, 7, 512, 512, 3, 1),
     ("sc_160_64", 64, 160, 64, 64, 3, 1),
+    ("sc_320_32", 64, 320, 32, 32, 3, 1),
+    ("sc_320_32_64", 64, 320, 32, 64, 3, 1),
     ("sc_80_96", 64, 80, 96, 96, 3, 1),
     ("sc_40_96", 64, 40, 96, 96, 3, 1),
     ("sc_20_224", 64, 20, 224, 224, 3, 1),
@@ -58,11 +60,18 @@ def main():
                 os.environ.pop("PC_CONV_ROWB", None)
             os.environ.pop("PC_CONV_HALO", None)
             os.environ.pop("PC_CONV_FAST", None)
+            os.environ.pop("PC_CONV_T2D", None)
             if c.startswith("f"):
                 os.environ.pop("PC_CONV_CFG", None)
                 os.environ["PC_CONV_FAST"] = str(int(c[1:]) + 1)
             elif c == "auto":
                 os.environ.pop("PC_CONV_CFG", None)
+            elif c == "t2d":          # 2-D block kernel (pc_conv_t2d.hip) where it can run
+                os.environ.pop("PC_CONV_CFG", None)
+                os.environ["PC_CONV_T2D"] = "2"
+            elif c == "not2d":
+                os.environ.pop("PC_CONV_CFG", None)
+                os.environ["PC_CONV_T2D"] = "0"
             elif c.startswith("h"):
                 os.environ.pop("PC_CONV_CFG", None)
                 os.environ["PC_CONV_HALO"] = str(int(c[1:]) + 1)

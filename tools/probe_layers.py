@@ -52,7 +52,8 @@ def main():
         key = describe(P, P.ops[int(op)])
         a = agg[key]
         a[0] += 1; a[1] += ms; a[2] += fl
-        a[3] = (f"f{int(halo) - 100}" if halo >= 100 else f"h{int(halo)}") if halo >= 0 else \
+        a[3] = (f"t{int(halo) - 200}" if halo >= 200 else f"f{int(halo) - 100}" if halo >= 100 else f"h{int(halo)}") \
+            if halo >= 0 else \
             (f"g{int(cfg)}" if cfg >= 0 else "-")
         tot_ms += ms; tot_fl += fl
     print(f"{which} batch {B}: {tot_ms / reps:.3f} ms/run, {tot_fl / (tot_ms * 1e-3) / 1e12:.1f} TFLOP/s overall")
