@@ -31,6 +31,9 @@ hipError_t conv_t2d_launch(const ConvParams& p, hipStream_t s);
 int conv_t2d_supported(int cin, int npad, int KH, int KW, int stride, int pad, int act, int out_f32, int ycs,
                        int ycoff);
 int conv_t2d_rows(int npad);
+int stem_fused_ok(int f32, int cin, int cin_true, int KH, int KW, int npad, int cwrite, int ycs, int ycoff);
+hipError_t stem_fused_launch(const StemParams& p, const void* wpk, const float* bias, const float* slope, int npad,
+                             int cwrite, hipStream_t s);
 hipError_t splitk_reduce_launch(int f32, const float* part, int splitk, int M, int npad, int cout, const float* bias,
                                 const float* slope, int act, void* y, int ycs, int out_f32, hipStream_t s);
 hipError_t stem_launch(int f32, const StemParams& p, hipStream_t s);
@@ -868,7 +871,17 @@ static int run_ops(pc_net* n, int N) {
       p.cpad = w[12];
       p.y = tensor_ptr(n, w[1]);
       const StemPlan& st = n->stems[i];
-      if (!st.use_mfma) {
+      const int st_cwrite = std::min(Y.C, st.npad);
+      // fused gather + MFMA stem (pc_stem.hip) unless PC_STEM_UNFUSED is set
+      const bool fused = st.use_mfma && !getenv("PC_STEM_UNFUSED") &&
+                         stem_fused_ok(n->f32, X.C, st.cin_true, p.KH, p.KW, st.npad, st_cwrite, Y.cs, Y.coff) &&
+                         X.cs % 4 == 0 && (reinterpret_cast<uintptr_t>(p.x) & 7) == 0 &&
+                         (reinterpret_cast<uintptr_t>(p.y) & 15) == 0;
+      if (fused) {
+        rec.kind = OP_CONV;
+        rec.flops = n->plans[i].flops_per_image * N;
+        HIPCHK(c, stem_fused_launch(p, st.w, st.bias, st.slope, st.npad, st_cwrite, s));
+      } else if (!st.use_mfma) {
         HIPCHK(c, stem_launch(n->f32, p, s));
       } else {
         HIPCHK(c, stem_im2col_launch(n->f32, p, st.cin_true, n->stem_col, s));

@@ -1,0 +1,119 @@
+// Fused network stem (gfx950): 3x3 conv over a 3-channel NHWC4 input, one MFMA K step.
+//
+// The stem's window is 3 x 3 x 3 = 27 values, i.e. one 32-element K row of
+// v_mfma_f32_16x16x32_f16. The previous path materialised that row for every output
+// pixel in HBM (stem_im2col3: 64 B written + read back per pixel, 6x the algorithmic
+// bytes) and then ran a 1x1 conv over it. Here a wave takes 16 consecutive output
+// pixels: each lane gathers the nine 4-channel input pixels of its output pixel (8-byte
+// loads, L1/L2 resident neighbourhoods), keeps the 8 K values of its lane group
+// (fq = lane >> 4: k = 8*fq .. 8*fq+7, k = tap*3 + channel, zero past 27), multiplies
+// them against the register-resident [npad][32] weight fragments, and finishes bias +
+// activation in registers. The f16 results go through a small per-wave LDS image so that
+// every pixel leaves as whole 16-byte chunks of contiguous pixel rows.
+//
+// Same K positions and the same MFMA as the im2col + 1x1 path, so the results are equal
+// to it (the sign of an exact zero aside).
+#include "pc_conv_common.h"
+
+namespace pc {
+
+template <int NPAD>
+__global__ __launch_bounds__(256) void stem_fused(StemParams p, const f16* __restrict__ wpk,
+                                                   const float* __restrict__ bias, const float* __restrict__ slope,
+                                                   int cwrite) {
+  constexpr int TC = NPAD / 16;
+  constexpr int PITCH = NPAD * 2 + 16;        // padded f16 row of the staging image
+  constexpr int CH8 = NPAD / 8;               // 16-byte chunks per pixel
+  __shared__ __attribute__((aligned(16))) char stg[4][16 * PITCH];
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const long long M = (long long)p.N * p.OH * p.OW;
+  const long long q0 = ((long long)blockIdx.x * 4 + wave) * 16;
+  if (q0 >= M) return;   // whole wave (the image is per wave; no workgroup barrier below)
+
+  // weights: A fragment a = rows a*16 + fr, K fq*8 .. fq*8+7
+  f16x8 wa[TC];
+#pragma unroll
+  for (int a = 0; a < TC; ++a) wa[a] = *reinterpret_cast<const f16x8*>(wpk + (a * 16 + fr) * 32 + fq * 8);
+
+  // the window of this lane's pixel (rows past M gather zeros and are not stored)
+  const long long q = q0 + fr;
+  const int hw = p.OH * p.OW;
+  const int n = (int)(q / hw);
+  const int rem = (int)(q - (long long)n * hw);
+  const int oh = rem / p.OW, ow = rem - (rem / p.OW) * p.OW;
+  const f16* xb = reinterpret_cast<const f16*>(p.x) + (long long)n * p.H * p.W * p.xcs;
+  f16 v[27];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int ih = oh * p.stride - p.pad + t / 3, iw = ow * p.stride - p.pad + t % 3;
+    f16x4 e = {};
+    if (q < M && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W)
+      e = *reinterpret_cast<const f16x4*>(xb + ((long long)ih * p.W + iw) * p.xcs);
+    v[3 * t] = e[0];
+    v[3 * t + 1] = e[1];
+    v[3 * t + 2] = e[2];
+  }
+  f16x8 b;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const f16 z = (f16)0.f;
+    const f16 g3 = 24 + e < 27 ? v[24 + e] : z;
+    b[e] = fq == 0 ? v[e] : (fq == 1 ? v[8 + e] : (fq == 2 ? v[16 + e] : g3));
+  }
+
+  char* my = stg[wave];
+#pragma unroll
+  for (int a = 0; a < TC; ++a) {
+    f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[a], b, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    const int ch = a * 16 + fq * 4;   // output rows of this lane: pixel fr, channels ch .. ch+3
+    float o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float x = acc[j] + bias[ch + j];
+      x = act_apply(x, p.act, slope ? slope[ch + j] : 0.f);
+      o[j] = ch + j < p.cout ? x : 0.f;   // channel padding stays exactly zero
+    }
+    *reinterpret_cast<f16x4*>(my + fr * PITCH + ch * 2) = f16x4{(f16)o[0], (f16)o[1], (f16)o[2], (f16)o[3]};
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int cw8 = cwrite >> 3;   // host guarantees cwrite % 8 == 0
+#pragma unroll
+  for (int k = 0; k < (16 * CH8 + 63) / 64; ++k) {
+    const int idx = lane + k * 64;
+    const int pl = idx / CH8, cq = idx - (idx / CH8) * CH8;
+    if (pl >= 16 || cq >= cw8 || q0 + pl >= M) continue;
+    const f16x8 val = *reinterpret_cast<const f16x8*>(my + pl * PITCH + cq * 16);
+    *reinterpret_cast<f16x8*>(reinterpret_cast<f16*>(p.y) + (q0 + pl) * p.ycs + cq * 8) = val;
+  }
+}
+
+// can the fused stem run this op? (f16, NHWC4 input with 3 true channels, 3x3 window,
+// npad 32 / 64 / 128, whole 16-byte output chunks)
+int stem_fused_ok(int f32, int cin, int cin_true, int KH, int KW, int npad, int cwrite, int ycs, int ycoff) {
+  return !f32 && cin == 4 && cin_true == 3 && KH == 3 && KW == 3 && (npad == 32 || npad == 64 || npad == 128) &&
+         cwrite % 8 == 0 && cwrite <= npad && ycs % 8 == 0 && ycoff % 8 == 0;
+}
+
+hipError_t stem_fused_launch(const StemParams& p, const void* wpk, const float* bias, const float* slope, int npad,
+                             int cwrite, hipStream_t s) {
+  const long long M = (long long)p.N * p.OH * p.OW;
+  const long long groups = (M + 15) / 16;
+  const long long nwg = (groups + 3) / 4;
+  if (nwg <= 0 || nwg >= (1LL << 31) || p.xcs % 4 || (reinterpret_cast<uintptr_t>(p.y) & 15) ||
+      (reinterpret_cast<uintptr_t>(p.x) & 7))
+    return hipErrorInvalidValue;
+  const f16* w = reinterpret_cast<const f16*>(wpk);
+  switch (npad) {
+    case 32: hipLaunchKernelGGL(stem_fused<32>, dim3((unsigned)nwg), dim3(256), 0, s, p, w, bias, slope, cwrite); break;
+    case 64: hipLaunchKernelGGL(stem_fused<64>, dim3((unsigned)nwg), dim3(256), 0, s, p, w, bias, slope, cwrite); break;
+    case 128: hipLaunchKernelGGL(stem_fused<128>, dim3((unsigned)nwg), dim3(256), 0, s, p, w, bias, slope, cwrite); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace pc
