@@ -214,10 +214,13 @@ class FaceEmbedder(YoloFaceBranch):
         # while the device works on chunk c+1 (0 = one chunk, no overlap)
         self._pipe_chunk = int(os.getenv("PERSON_CAPTURE_AMD_PIPE_CHUNK", "32"))
         self._pipe_ahead = int(os.getenv("PERSON_CAPTURE_AMD_PIPE_AHEAD", "2"))
-        # at the end of every detection chunk's policy, launch the faces collected so far as
-        # one ArcFace batch when there are at least this many (fraction of a full batch): the
-        # device then never waits for the host to fill a full batch (0 = full batches only)
-        self._embed_flush = float(os.getenv("PERSON_CAPTURE_AMD_EMBED_FLUSH", "0.25"))
+        # at the end of every detection chunk's policy (but the last), launch the faces
+        # collected so far as ArcFace batches of whole quanta: the device then never waits
+        # for the host to fill a full batch. The quantum is the face count whose flip-TTA
+        # images fill one round of the dominant 14x14x256 conv's 256x224 tiles over the CUs
+        # (256 CUs x 224 px / 196 px per image / 2 images per face = 146); partial rounds
+        # cost a whole round of that layer. 0 = full batches only.
+        self._embed_quantum = int(os.getenv("PERSON_CAPTURE_AMD_EMBED_QUANTUM", "146"))
         # batched speculative fallback passes (TTA / edge pad / pre-scan rotations) per chunk
         self._fb_prefetch = os.getenv("PERSON_CAPTURE_AMD_FALLBACK_PREFETCH", "1") != "0"
         # host phase timers of extract_batch (diagnostics; bench.py prints them)
@@ -608,13 +611,15 @@ class FaceEmbedder(YoloFaceBranch):
             while len(jobs) >= per:
                 emb_pending.append(self._embed_launch(imgs, jobs[:per], len(emb_pending)))
                 jobs = jobs[per:]
-            # chunk boundary: queue what is known behind the detections still in flight, so
-            # the device goes from SCRFD straight into ArcFace (measured r02: 3.2 ms of idle
-            # device per C3 step while the host filled the first full batch). Embeddings do
-            # not depend on how faces are batched.
-            if jobs and self._embed_flush > 0 and len(jobs) >= max(1, int(self._embed_flush * per)):
-                emb_pending.append(self._embed_launch(imgs, jobs, len(emb_pending)))
-                jobs = []
+            # chunk boundary: queue whole quanta of what is known behind the detections still
+            # in flight, so the device goes from SCRFD straight into ArcFace (measured r02:
+            # 3.2 ms of idle device per C3 step while the host filled the first full batch).
+            # Embeddings do not depend on how faces are batched.
+            q = min(self._embed_quantum, per)
+            if q > 0 and ci + 1 < len(chunks) and len(jobs) >= q:
+                k = len(jobs) // q * q
+                emb_pending.append(self._embed_launch(imgs, jobs[:k], len(emb_pending)))
+                jobs = jobs[k:]
             lap("embed_launch")
         if jobs:
             emb_pending.append(self._embed_launch(imgs, jobs, len(emb_pending)))
