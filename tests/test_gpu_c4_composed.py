@@ -1,0 +1,135 @@
+"""BASELINE C4 composed: the full per-frame path of main.py:211-353 as bench.py --workload c4
+runs it, in f32 (the parity mode), against the oracles chained the same way.
+
+Frames resident in HBM (bench.synth_frames) -> PersonDetector.detect_device (YOLOv8n) ->
+person boxes clamped to int crops exactly as main.py:231-236 -> FaceEmbedder.extract_batch
+over the crops as device views (SCRFD + ArcFace flip-TTA, one policy instance walking the
+crops in order) -> ReID tower on the same crop views.
+
+* persons: device boxes within 1e-2 px / conf within 1e-4 of oracle/ref_algos.yolo_postprocess
+  on oracle/nets_torch.yolov8_forward heads; the clamped int crops are identical (coordinates
+  within 1e-3 of an integer excepted).
+* faces per crop: oracle/pipeline.OracleFaceEmbedder (every fallback branch, same rot_phase)
+  walks the same crops; identical int boxes per crop, byte-identical chips -> embedding within
+  1e-4, otherwise the chained check (oracle chip of the device landmarks equals the device
+  chip, oracle embedding of it within 1e-4), as tests/test_gpu_bench_config.py does for C3.
+* ReID: unit embeddings of every crop within 1e-4 of oracle/nets_torch.clip_vit_forward
+  (ViT-L/14 width at depth 2, the reduced tower tests/test_gpu_reid.py pins).
+SCRFD-2.5G + IResNet-50 and 2 frames keep the CPU oracle within seconds per crop.
+"""
+import numpy as np
+import pytest
+import torch
+
+import bench
+from oracle import cv_ops
+from oracle import nets_torch as nt
+from oracle import pipeline as op
+from oracle import ref_algos as ra
+from person_capture_amd import face_embedder as fe_mod
+from person_capture_amd.detectors import PersonDetector
+from person_capture_amd.reid_embedder import ReIDEmbedder, clip_weights
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+NFRAMES = 2
+MAX_CROPS = 4
+FACE_CONF = 0.5    # synthetic SCRFD-2.5G: 16-29 faces per person crop of frame 0 at the default conf
+
+
+def _clamp(box, H, W):
+    """main.py:231-236."""
+    x1, y1, x2, y2 = box[:4]
+    x1, y1 = max(0, int(x1)), max(0, int(y1))
+    x2, y2 = min(W - 1, int(x2)), min(H - 1, int(y2))
+    return x1, y1, x2, y2
+
+
+def _near_int(v):
+    return abs(v - round(v)) < 1e-3
+
+
+def _embed(o, chip):
+    e = nt.iresnet_forward(o.p_a, o.depth, nt.arcface_input_from_chips(chip[None])).numpy()
+    ef = nt.iresnet_forward(o.p_a, o.depth, nt.arcface_input_from_chips(chip[None, :, ::-1])).numpy()
+    return ra.arcface_postprocess(e, ef)[0]
+
+
+def test_c4_composed_f32(gpu_ctx, monkeypatch):
+    monkeypatch.setenv("PERSON_CAPTURE_AMD_PRECISION", "f32")
+    monkeypatch.setenv("PERSON_CAPTURE_AMD_ARCFACE", "iresnet50")
+    frames = bench.synth_frames(0, NFRAMES)
+    H, W = frames.shape[1:3]
+    det = PersonDetector("yolov8n.pt", device="cuda:0")
+    fe = fe_mod.FaceEmbedder(ctx="cuda:0", yolo_model="scrfd_2.5g_bnkps", conf=FACE_CONF)
+    fe.debug_chips = True
+    reid = ReIDEmbedder(device="cuda:0", model_name="ViT-L-14-d2")
+    ctx = fe._ctx
+    d = ctx.alloc(frames.nbytes)
+    ctx.upload(frames, d)
+    fsz = frames[0].nbytes
+    devs = [fe_mod._DevImage(d.ptr + i * fsz, H, W, W * 3) for i in range(NFRAMES)]
+
+    # ---- persons ----
+    persons = det.detect_device([(x.ptr, H, W, W * 3) for x in devs], conf=0.35)
+    crops, views = [], []
+    n_boxes = 0
+    for fi, (frame, got) in enumerate(zip(frames, persons)):
+        canvas, (_, _, _, _, Hp, Wp) = ra.yolo_letterbox(frame)
+        x = torch.from_numpy(np.ascontiguousarray(canvas[None].transpose(0, 3, 1, 2)))
+        heads = [t[0].numpy() for t in nt.yolov8_forward(det._params, "n", x)]
+        want = ra.yolo_postprocess(heads, 0.35, 0.45, 40, Hp, Wp, H, W)
+        near = ra.yolo_postprocess(heads, 0.35 - 1e-4, 0.45, 40, Hp, Wp, H, W)
+        assert len(near) == len(want), f"frame {fi}: a person candidate sits at the threshold"
+        assert len(got) == len(want), f"frame {fi}: {len(got)} persons vs oracle {len(want)}"
+        np.testing.assert_allclose(got[:, :4], want[:, :4], atol=1e-2)
+        np.testing.assert_allclose(got[:, 4], want[:, 4], atol=1e-4)
+        for g, w in zip(got, want):
+            n_boxes += 1
+            gi, wi = _clamp(g, H, W), _clamp(w, H, W)
+            for a, b, v in zip(gi, wi, w[:4]):
+                assert a == b or _near_int(float(v)), (fi, gi, wi)
+            x1, y1, x2, y2 = gi
+            if x2 <= x1 + 2 or y2 <= y1 + 2:
+                continue
+            if len(crops) < MAX_CROPS:
+                crops.append(frame[y1:y2, x1:x2])
+                views.append(fe_mod._DevImage(devs[fi].ptr + y1 * W * 3 + x1 * 3, y2 - y1, x2 - x1, W * 3))
+    assert n_boxes >= 2 and len(crops) >= 2
+    print(f"{n_boxes} persons, {len(crops)} crops", flush=True)
+
+    # ---- faces per person crop (one policy instance, crops in order) ----
+    got = fe.extract_batch([None] * len(views), dev_frames=views)
+    o = op.OracleFaceEmbedder(fe._scrfd_params, "2.5g", fe._arc_params, 50, conf=FACE_CONF, rot_phase=id(fe) & 7)
+    n_exact = n_chained = 0
+    for ci, (crop, g) in enumerate(zip(crops, got)):
+        r = o.extract(crop)
+        print(f"crop {ci} {crop.shape[:2]}: {len(g)} faces, oracle {len(r)} ({o.trace})", flush=True)
+        assert len(g) == len(r), f"crop {ci}: {len(g)} faces vs oracle {len(r)}"
+        gs = sorted(g, key=lambda f: tuple(f["bbox"]))
+        rs = sorted(r, key=lambda f: tuple(f["bbox"]))
+        for a, b in zip(gs, rs):
+            assert np.array_equal(a["bbox"], b["bbox"]), (ci, a["bbox"], b["bbox"])
+            if np.array_equal(a["chip"], b["chip"]):
+                assert np.abs(a["feat"] - b["feat"]).max() < TOL, ci
+                assert abs(a["quality"] - b["quality"]) <= 1e-9 * max(1.0, b["quality"])
+                n_exact += 1
+            else:
+                assert np.abs(a["kps5"] - b["kps5"]).max() < 1e-3, ci
+                x1, y1, x2, y2 = a["bbox"]
+                chip = op.chip_for(crop[y1:y2, x1:x2], a["kps5"])
+                assert np.array_equal(chip, a["chip"]), ci
+                assert abs(cv_ops.face_quality(chip) - a["quality"]) <= 1e-9 * max(1.0, a["quality"])
+                assert np.abs(_embed(o, chip) - a["feat"]).max() < TOL, ci
+                n_chained += 1
+    assert (fe._frame_idx, fe._no_face_streak, fe._last_face_idx, fe._rot_cycle) == o.state()[:4]
+
+    # ---- ReID of the same crop views ----
+    feats = reid.extract_device([(v.ptr, v.H, v.W, v.stride) for v in views])
+    xr = torch.stack([nt.clip_preprocess_pil(c) for c in crops])
+    ref = torch.nn.functional.normalize(nt.clip_vit_forward(clip_weights("ViT-L-14-d2", 0), "ViT-L-14-d2", xr),
+                                        dim=1).numpy()
+    assert np.abs(feats - ref).max() < TOL
+    print(f"C4 composed f32: {n_boxes} persons in {NFRAMES} frames, {len(crops)} crops, "
+          f"{n_exact} faces exact + {n_chained} chained, ReID max |d| {np.abs(feats - ref).max():.2e}")
