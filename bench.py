@@ -259,6 +259,10 @@ def main():
                      "launches": conv_launches, "avg_launch_us": round(conv_ms * 1e3 / max(1, conv_launches), 2),
                      "flops_per_launch": round(conv_flops / max(1, conv_launches)),
                      "conv_share_of_step": round(conv_ms * 1e-3 / (t1 - t0), 4),
+                     "streams": 2 if fe._ectx is not fe._ctx else 1,
+                     "streams_note": "ArcFace (embed stream) runs beside SCRFD (detection stream): the conv "
+                                     "event spans of the two overlap, so conv_share_of_step can exceed 1 and a "
+                                     "launch's duration includes the co-running kernels' share of the CUs",
                      "per_net": {name: {"conv_ms_per_step": round(p_["conv_ms"] / args.steps, 3),
                                         "tflops": round(p_["conv_flops"] / (p_["conv_ms"] * 1e-3) / 1e12, 1)
                                         if p_["conv_ms"] > 0 else None}

@@ -68,11 +68,14 @@ def _device_index(ctx: str) -> int:
     return 0
 
 
-def get_context(device_index: int) -> GpuContext:
-    c = _CTX_CACHE.get(device_index)
+def get_context(device_index: int, role: str = "") -> GpuContext:
+    """The shared context (stream) of a device; role "embed" is a second one, on which the
+    face embedder runs chips -> ArcFace -> bank match beside the detections of the main one."""
+    key = (device_index, role) if role else device_index
+    c = _CTX_CACHE.get(key)
     if c is None:
         c = GpuContext(device_index)
-        _CTX_CACHE[device_index] = c
+        _CTX_CACHE[key] = c
     return c
 
 
@@ -226,7 +229,16 @@ class FaceEmbedder(YoloFaceBranch):
         # host phase timers of extract_batch (diagnostics; bench.py prints them)
         self.host_times: Optional[Dict[str, float]] = {} if os.getenv("PERSON_CAPTURE_AMD_HOST_TIMING") else None
         self._scrfd_engines: Dict[int, ScrfdEngine] = {}
-        self._arc = ArcFaceEngine(self._ctx, self._arc_params, self._arc_depth, precision=self.precision,
+        # SCRFD backend: the embed side (warp/resize chips, quality, ArcFace, bank match,
+        # readbacks) runs on a second stream, so a chunk's ArcFace batches execute beside the
+        # detection chunks queued ahead of it instead of behind them (the small late SCRFD
+        # layers and every launch's last partial round leave CUs idle). Its only inputs from
+        # the detection stream are the frames, which are on the device before the host has
+        # the detections that name the faces (the host waited on their fence).
+        # PERSON_CAPTURE_AMD_EMBED_STREAM=0: one stream.
+        two = self.detector_backend == "scrfd" and os.getenv("PERSON_CAPTURE_AMD_EMBED_STREAM", "1") != "0"
+        self._ectx = get_context(self._device_index, "embed") if two else self._ctx
+        self._arc = ArcFaceEngine(self._ectx, self._arc_params, self._arc_depth, precision=self.precision,
                                   max_batch=self._arc_batch)
         self._arc_feat_dim = self._arc.dim
         self._arc_fixed_batch = False
@@ -629,6 +641,7 @@ class FaceEmbedder(YoloFaceBranch):
         for pend in emb_pending:
             self._embed_collect(pend, out)
         self._ctx.sync()
+        self._ectx.sync()
         lap("embed_wait_collect")
         for lst in out:
             lst.sort(key=lambda f: (f['quality'], (f['bbox'][2] - f['bbox'][0]) * (f['bbox'][3] - f['bbox'][1])),
@@ -891,7 +904,8 @@ class FaceEmbedder(YoloFaceBranch):
         """Enqueue crop + align/resize + quality + ArcFace (+ bank match) of at most one
         ArcFace batch of faces, and the readback into pinned memory."""
         m = len(jobs)
-        chips = self._ctx.scratch("chips", m * _ARC_SIDE * _ARC_SIDE * 3)
+        ctx = self._ectx
+        chips = ctx.scratch("chips", m * _ARC_SIDE * _ARC_SIDE * 3)
         chip_sz = _ARC_SIDE * _ARC_SIDE * 3
         has_k = [j for j in range(m) if jobs[j][2] is not None]
         valid = np.zeros((m,), bool)
@@ -931,18 +945,18 @@ class FaceEmbedder(YoloFaceBranch):
                 arr[o:o + len(d)] = d
                 o += len(d)
             assert arr.dtype.itemsize == 96
-            check(self._ctx.lib.pc_warp_affine(self._ctx.handle, arr.ctypes.data_as(C.POINTER(WarpDesc)), len(arr)),
-                  self._ctx.handle, "warp_affine")
+            check(ctx.lib.pc_warp_affine(ctx.handle, arr.ctypes.data_as(C.POINTER(WarpDesc)), len(arr)),
+                  ctx.handle, "warp_affine")
         for j in resize_jobs:
             fi, (xi1, yi1, xi2, yi2), _ = jobs[j]
             im = imgs[fi]
             crop = _DevImage(im.ptr + yi1 * im.stride + xi1 * 3, yi2 - yi1, xi2 - xi1, im.stride)
             self._resize_chip(crop, chips.ptr + j * chip_sz)
-        qbuf = self._ctx.scratch("quality", m * 8)
-        check(self._ctx.lib.pc_face_quality(self._ctx.handle, chips.ptr, m, _ARC_SIDE, qbuf.ptr), self._ctx.handle,
+        qbuf = ctx.scratch("quality", m * 8)
+        check(ctx.lib.pc_face_quality(ctx.handle, chips.ptr, m, _ARC_SIDE, qbuf.ptr), ctx.handle,
               "face_quality")
         do_flip = self._do_flip()
-        fbuf = self._ctx.scratch("feats", m * self._arc_feat_dim * 4)
+        fbuf = ctx.scratch("feats", m * self._arc_feat_dim * 4)
         if (2 * m if do_flip else m) > self._arc.max_batch:
             raise ValueError("embed launch larger than one ArcFace batch")
         self._arc.embed_device(chips.ptr, m, do_flip, fbuf.ptr)
@@ -950,20 +964,20 @@ class FaceEmbedder(YoloFaceBranch):
         dbg = bool(getattr(self, "debug_chips", False))
         fd_bytes = m * 4 if bank is not None else 0
         sizes = [m * 8, m * self._arc_feat_dim * 4, fd_bytes, m * chip_sz if dbg else 0]
-        pin = self._ctx.pinned(f"emb{slot}", sum(sizes))
-        q = self._ctx.download_async(qbuf.ptr, pin, 0, (m,), np.float64)
-        feats = self._ctx.download_async(fbuf.ptr, pin, sizes[0], (m, self._arc_feat_dim), np.float32)
+        pin = ctx.pinned(f"emb{slot}", sum(sizes))
+        q = ctx.download_async(qbuf.ptr, pin, 0, (m,), np.float64)
+        feats = ctx.download_async(fbuf.ptr, pin, sizes[0], (m, self._arc_feat_dim), np.float32)
         fd = None
         if bank is not None:
-            dfd = self._ctx.scratch("fd", m * 4)
-            didx = self._ctx.scratch("fd_idx", m * 4)
-            bank.match_device(fbuf.ptr, m, dfd.ptr, didx.ptr)
-            fd = self._ctx.download_async(dfd.ptr, pin, sizes[0] + sizes[1], (m,), np.float32)
+            dfd = ctx.scratch("fd", m * 4)
+            didx = ctx.scratch("fd_idx", m * 4)
+            bank.match_device(fbuf.ptr, m, dfd.ptr, didx.ptr, ctx=ctx)
+            fd = ctx.download_async(dfd.ptr, pin, sizes[0] + sizes[1], (m,), np.float32)
         chip_h = None
         if dbg:
-            chip_h = self._ctx.download_async(chips.ptr, pin, sizes[0] + sizes[1] + sizes[2],
+            chip_h = ctx.download_async(chips.ptr, pin, sizes[0] + sizes[1] + sizes[2],
                                               (m, _ARC_SIDE, _ARC_SIDE, 3), np.uint8)
-        return self._ctx.fence(f"emb{slot}"), jobs, q, feats, fd, chip_h
+        return ctx.fence(f"emb{slot}"), jobs, q, feats, fd, chip_h
 
     def _embed_collect(self, pend: tuple, out: List[list]) -> None:
         fence, jobs, q, feats, fd, chip_h = pend
@@ -981,7 +995,7 @@ class FaceEmbedder(YoloFaceBranch):
     def _resize_chip(self, crop: _DevImage, d_dst: int) -> None:
         """cv2.resize(face, (112,112), INTER_AREA if max(h,w) > 112 else INTER_LINEAR) (:2458-2460)."""
         p = imageops.resize_plan(crop.H, crop.W, (_ARC_SIDE, _ARC_SIDE), area=max(crop.H, crop.W) > _ARC_SIDE)
-        self._cv_resize(crop, p, d_dst)
+        cv_resize_into(self._ectx, crop, p, d_dst)   # embed stream (chips)
 
     def _upright_by_eye_roll(self, im: _DevImage, box, pts5, d_dst: int, warps: list, resize_jobs: list,
                              j: int) -> None:
@@ -1019,9 +1033,10 @@ class FaceEmbedder(YoloFaceBranch):
         cx, cy = w / 2.0, h / 2.0
         M = np.array([[alpha, beta, (1 - alpha) * cx - beta * cy],
                       [-beta, alpha, beta * cx + (1 - alpha) * cy]], dtype=np.float64)
-        rot = self._ctx.scratch(f"roll{j}", w * h * 3)
+        ectx = self._ectx
+        rot = ectx.scratch(f"roll{j}", w * h * 3)
         d = imageops.warp_desc(src, im.stride, w, h, M.reshape(-1), rot.ptr, out_w=w, out_h=h)
-        check(self._ctx.lib.pc_warp_affine(self._ctx.handle, (WarpDesc * 1)(d), 1), self._ctx.handle, "warp_affine")
+        check(ectx.lib.pc_warp_affine(ectx.handle, (WarpDesc * 1)(d), 1), ectx.handle, "warp_affine")
         pts_h = np.hstack([pts[:5, :2], np.ones((5, 1), dtype=np.float32)])
         pts_rot = (M @ pts_h.T).T.astype(np.float32)
         canon = imageops.canon_5pts(pts_rot)
@@ -1041,28 +1056,32 @@ class FaceEmbedder(YoloFaceBranch):
             return []
         m = len(bgr_list)
         chip_sz = _ARC_SIDE * _ARC_SIDE * 3
-        chips = self._ctx.scratch("enc_chips", m * chip_sz)
+        ctx = self._ectx
+        chips = ctx.scratch("enc_chips", m * chip_sz)
         for i, b in enumerate(bgr_list):
             b = np.ascontiguousarray(b, dtype=np.uint8)
             if b.shape[:2] == (_ARC_SIDE, _ARC_SIDE):
-                self._ctx.upload(b, chips, offset=i * chip_sz)
+                ctx.upload(b, chips, offset=i * chip_sz)
             else:
-                im = self._upload(b, key=f"enc_src{i}")
+                buf = ctx.scratch(f"enc_src{i}", b.nbytes)
+                ctx.upload(b, buf)
+                im = _DevImage(buf.ptr, b.shape[0], b.shape[1], b.strides[0], buf)
                 self._resize_chip(im, chips.ptr + i * chip_sz)
         do_flip = (not getattr(self, "_fast_prescan", False)) or getattr(self, "_prescan_escalate", False)
-        fbuf = self._ctx.scratch("enc_feats", m * self._arc_feat_dim * 4)
+        fbuf = ctx.scratch("enc_feats", m * self._arc_feat_dim * 4)
         per = self._arc.max_batch // 2 if do_flip else self._arc.max_batch
         for s in range(0, m, per):
             k = min(per, m - s)
             self._arc.embed_device(chips.ptr + s * chip_sz, k, do_flip, fbuf.ptr + s * self._arc_feat_dim * 4)
-        return self._ctx.download(fbuf.ptr, (m, self._arc_feat_dim), np.float32)
+        return ctx.download(fbuf.ptr, (m, self._arc_feat_dim), np.float32)
 
     def _face_quality(self, bgr):
         b = np.ascontiguousarray(bgr, dtype=np.uint8)
         if b.shape[0] > 128 or b.shape[1] > 128 or b.shape[0] != b.shape[1]:
             raise ValueError("device face quality supports square chips up to 128 px")
-        d = self._ctx.scratch("q_chip", b.nbytes)
-        self._ctx.upload(b, d)
-        q = self._ctx.scratch("q_out", 8)
-        check(self._ctx.lib.pc_face_quality(self._ctx.handle, d.ptr, 1, b.shape[0], q.ptr), self._ctx.handle)
-        return float(self._ctx.download(q.ptr, (1,), np.float64)[0])
+        ctx = self._ectx
+        d = ctx.scratch("q_chip", b.nbytes)
+        ctx.upload(b, d)
+        q = ctx.scratch("q_out", 8)
+        check(ctx.lib.pc_face_quality(ctx.handle, d.ptr, 1, b.shape[0], q.ptr), ctx.handle)
+        return float(ctx.download(q.ptr, (1,), np.float64)[0])

@@ -103,10 +103,14 @@ class DeviceBank:
         self._buf = self.ctx.alloc(max(b.nbytes, 16))
         if b.size:
             self.ctx.upload(b, self._buf)
+            self.ctx.sync()   # other streams (the face embedder's embed stream) read the rows
 
-    def match_device(self, d_feats: int, n: int, d_fd: int, d_idx: int, feat_dim: int = 512) -> None:
-        """fd[i] = Processor._fd_min(feats[i], bank) for n device feature rows of feat_dim f32."""
+    def match_device(self, d_feats: int, n: int, d_fd: int, d_idx: int, feat_dim: int = 512, ctx=None) -> None:
+        """fd[i] = Processor._fd_min(feats[i], bank) for n device feature rows of feat_dim f32,
+        on the stream of `ctx` (default: the bank's own context; the bank rows are on the
+        device before set() returns, so any stream may read them)."""
         if self.rows and self.dim != feat_dim:
             raise ValueError(f"bank rows have {self.dim} dims, features {feat_dim} (shapes not aligned)")
-        check(self.ctx.lib.pc_bank_match(self.ctx.handle, d_feats, int(n), self._buf.ptr, int(self.rows),
-                                         int(feat_dim), d_fd, d_idx), self.ctx.handle, "bank_match")
+        c = self.ctx if ctx is None else ctx
+        check(c.lib.pc_bank_match(c.handle, d_feats, int(n), self._buf.ptr, int(self.rows),
+                                  int(feat_dim), d_fd, d_idx), c.handle, "bank_match")
