@@ -147,6 +147,10 @@ int pc_ctx_destroy(pc_ctx* ctx);
 const char* pc_last_error(const pc_ctx* ctx);
 int pc_ctx_set_stream(pc_ctx* ctx, void* hip_stream); /* NULL = context-owned stream */
 void* pc_ctx_stream(pc_ctx* ctx);
+/* Re-create the context-owned stream at a HIP stream priority (lower = higher priority,
+ * clamped to the device's range). No reference counterpart: the face embedder's second
+ * (embed) stream is a build-side scheduling choice (two streams). */
+int pc_ctx_set_priority(pc_ctx* ctx, int priority);
 int pc_ctx_sync(pc_ctx* ctx);
 int pc_device_alloc(pc_ctx* ctx, size_t bytes, void** d_out);
 int pc_device_free(pc_ctx* ctx, void* d_ptr);

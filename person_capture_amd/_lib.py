@@ -74,6 +74,7 @@ SIGNATURES = {
     "pc_last_error": ([_P], C.c_char_p),
     "pc_ctx_set_stream": ([_P, _P], _I),
     "pc_ctx_stream": ([_P], _P),
+    "pc_ctx_set_priority": ([_P, _I], _I),
     "pc_ctx_sync": ([_P], _I),
     "pc_device_alloc": ([_P, _SZ, C.POINTER(_P)], _I),
     "pc_device_free": ([_P, _P], _I),

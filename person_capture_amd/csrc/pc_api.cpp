@@ -249,6 +249,23 @@ extern "C" int pc_ctx_set_stream(pc_ctx* c, void* s) {
   return PC_OK;
 }
 extern "C" void* pc_ctx_stream(pc_ctx* c) { return c ? (void*)c->stream : nullptr; }
+// Re-create the context-owned stream at a scheduling priority (HIP convention: lower =
+// higher priority; clamped to hipDeviceGetStreamPriorityRange). Work already queued on the
+// old stream is drained first.
+extern "C" int pc_ctx_set_priority(pc_ctx* c, int priority) {
+  if (!c) return PC_ERR_ARG;
+  int least = 0, greatest = 0;
+  HIPCHK(c, hipDeviceGetStreamPriorityRange(&least, &greatest));
+  const int p = priority < greatest ? greatest : (priority > least ? least : priority);
+  hipStream_t s = nullptr;
+  HIPCHK(c, hipStreamCreateWithPriority(&s, hipStreamNonBlocking, p));
+  HIPCHK(c, hipStreamSynchronize(c->own_stream));
+  const bool own = c->stream == c->own_stream;
+  hipStreamDestroy(c->own_stream);
+  c->own_stream = s;
+  if (own) c->stream = s;
+  return PC_OK;
+}
 extern "C" int pc_ctx_sync(pc_ctx* c) {
   if (!c) return PC_ERR_ARG;
   HIPCHK(c, hipStreamSynchronize(c->stream));

@@ -75,6 +75,9 @@ def get_context(device_index: int, role: str = "") -> GpuContext:
     c = _CTX_CACHE.get(key)
     if c is None:
         c = GpuContext(device_index)
+        prio = os.getenv("PERSON_CAPTURE_AMD_EMBED_PRIORITY", "") if role == "embed" else ""
+        if prio:   # HIP stream priority of the embed stream (lower = higher), e.g. -1
+            c.set_priority(int(prio))
         _CTX_CACHE[key] = c
     return c
 

@@ -183,6 +183,10 @@ class GpuContext:
         check(self.lib.pc_ctx_sync(self.handle), self.handle, "sync")
         self._keep.clear()
 
+    def set_priority(self, priority: int) -> None:
+        """Re-create this context's stream at a HIP priority (lower = higher; clamped)."""
+        check(self.lib.pc_ctx_set_priority(self.handle, int(priority)), self.handle, "set_priority")
+
     @property
     def stream(self) -> int:
         return int(self.lib.pc_ctx_stream(self.handle) or 0)
