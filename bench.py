@@ -119,6 +119,44 @@ def cpu_baseline(frames: np.ndarray, fe, bank: np.ndarray, n_sample: int, n_samp
     return out
 
 
+def _kernel_of(code: float, cfg: float) -> str:
+    """Planner code of a profiled conv launch (pc_net_profile_ops) -> kernel instantiation."""
+    c = int(code)
+    if c >= 200:
+        return f"conv_t2d (2-D block kernel, variant {c - 200})"
+    if c >= 100:
+        return f"conv_fast tile cfg {c - 100} (pc_conv_fast.hip kFastCfgs)"
+    if c >= 0:
+        return f"conv_halo tile {c}"
+    return f"conv_igemm tile cfg {int(cfg)}"
+
+
+def dominant_conv(nets, names) -> dict:
+    """The conv kernel instantiation with the largest total HIP-event time over the timed
+    region (per-launch records of every profiled net), with its algorithmic FLOPs per launch
+    and average launch duration: the roofline line is this kernel's."""
+    agg = {}
+    total = 0.0
+    for n, name in zip(nets, names):
+        for op, kind, ms, fl, code, cfg in n.profile_ops():
+            if fl <= 0:
+                continue
+            k = (name, int(code), int(cfg) if code < 0 else -1)
+            a = agg.setdefault(k, [0, 0.0, 0.0])
+            a[0] += 1
+            a[1] += ms
+            a[2] += fl
+            total += ms
+    if not agg:
+        return {"kernel": None, "code": None, "launches": 0, "avg_us": None, "flops_per_launch": None,
+                "achieved_tflops": 0.0, "share": None}
+    (name, code, cfg), (cnt, ms, fl) = max(agg.items(), key=lambda kv: kv[1][1])
+    return {"kernel": f"{_kernel_of(code, cfg)} in {name}" + (
+                " = conv_fast<f16,256,224,128,4,2,2,1> (ArcFace 14x14x256 layers)" if code == 113 else ""),
+            "code": code, "launches": cnt, "avg_us": round(ms * 1e3 / cnt, 2), "flops_per_launch": round(fl / cnt),
+            "achieved_tflops": round(fl / (ms * 1e-3) / 1e12, 2), "share": round(ms / total, 4)}
+
+
 def load_traffic():
     """HBM bytes per conv launch from the round's rocprofv3 FETCH_SIZE / WRITE_SIZE passes
     (tools/pmc_traffic.py writes bench_traffic.json at the repo root, next to this file, so
@@ -221,6 +259,7 @@ def main():
     _barrier(world)
     elapsed = _max_over_ranks(world, t1 - t0)
     prof = [n.profile_read() for n in nets]
+    dom = dominant_conv(nets, ("scrfd", "arcface"))
     for n in nets:
         n.profile(False)
     if fe.host_times is not None:
@@ -253,9 +292,14 @@ def main():
                    "faces_per_frame": round(nfaces / args.batch, 3), "accepted_faces_per_step": accept,
                    "accepted_faces_per_step_cli_0.32": accept_cli, "bank_planted_rows": n_plant,
                    "parallelism": f"frame-shard x{world} (no collective)"},
-        "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                     "frac": round(achieved / peak, 4), "traffic": traffic,
-                     "kernel": "implicit-GEMM MFMA convs (conv_fast / conv_igemm, SCRFD + ArcFace)",
+        "roofline": {"bound": "mfma", "achieved": dom["achieved_tflops"], "peak": peak, "unit": "TFLOP/s",
+                     "frac": round(dom["achieved_tflops"] / peak, 4),
+                     "traffic": (dominant or {}).get("hbm_bytes_per_launch") if dom["code"] == 113 else None,
+                     "kernel": dom["kernel"], "kernel_launches": dom["launches"],
+                     "kernel_avg_launch_us": dom["avg_us"], "kernel_flops_per_launch": dom["flops_per_launch"],
+                     "kernel_share_of_conv_time": dom["share"],
+                     "conv_family": {"achieved": round(achieved, 2), "frac": round(achieved / peak, 4),
+                                     "traffic_mean_per_launch": traffic},
                      "launches": conv_launches, "avg_launch_us": round(conv_ms * 1e3 / max(1, conv_launches), 2),
                      "flops_per_launch": round(conv_flops / max(1, conv_launches)),
                      "conv_share_of_step": round(conv_ms * 1e-3 / (t1 - t0), 4),
@@ -267,8 +311,10 @@ def main():
                                         "tflops": round(p_["conv_flops"] / (p_["conv_ms"] * 1e-3) / 1e12, 1)
                                         if p_["conv_ms"] > 0 else None}
                                  for name, p_ in zip(("scrfd", "arcface"), prof)},
-                     "traffic_unit": "HBM bytes per conv launch (mean over the family, rocprofv3 PMC)",
-                     "dominant_kernel": dominant},
+                     "traffic_unit": "HBM bytes per launch of the dominant kernel (rocprofv3 FETCH_SIZE x2 + "
+                                     "WRITE_SIZE, bench_traffic.json); conv_family.traffic_mean_per_launch: the mean "
+                                     "over all conv launches",
+                     "dominant_kernel_rocprof": dominant},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
