@@ -217,3 +217,7 @@ def test_stem_and_maxpool(gpu_ctx, prec):
     assert np.abs(gy[..., :28] - Y.permute(0, 2, 3, 1).numpy()).max() < tol
     assert np.all(gy[..., 28:] == 0)
     assert np.abs(gz[..., :28] - Z.permute(0, 2, 3, 1).numpy()).max() < tol
+    # the pool itself is exact: max over the device's own stem output (both precisions;
+    # f16 runs the 8-channel vector pool)
+    Zs = F.max_pool2d(torch.from_numpy(gy).permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1).numpy()
+    assert np.array_equal(gz, Zs)
