@@ -17,6 +17,9 @@
 
 namespace pc {
 
+// 16-pixel groups per wave: weights, bias and slopes are loaded once for all of them
+constexpr int kStemGroupsPerWave = 4;
+
 template <int NPAD>
 __global__ __launch_bounds__(256) void stem_fused(StemParams p, const f16* __restrict__ wpk,
                                                    const float* __restrict__ bias, const float* __restrict__ slope,
@@ -28,66 +31,84 @@ __global__ __launch_bounds__(256) void stem_fused(StemParams p, const f16* __res
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fq = lane >> 4;
-  const long long M = (long long)p.N * p.OH * p.OW;
-  const long long q0 = ((long long)blockIdx.x * 4 + wave) * 16;
-  if (q0 >= M) return;   // whole wave (the image is per wave; no workgroup barrier below)
+  const int M = p.N * p.OH * p.OW;            // host guarantees M < 2^31
+  const int g0 = (blockIdx.x * 4 + wave) * kStemGroupsPerWave;
+  if (g0 * 16 >= M) return;   // whole wave (the image is per wave; no workgroup barrier below)
 
-  // weights: A fragment a = rows a*16 + fr, K fq*8 .. fq*8+7
+  // weights: A fragment a = rows a*16 + fr, K fq*8 .. fq*8+7; bias / slope of this lane's
+  // output channels, all held for the wave's kStemGroupsPerWave pixel groups
   f16x8 wa[TC];
-#pragma unroll
-  for (int a = 0; a < TC; ++a) wa[a] = *reinterpret_cast<const f16x8*>(wpk + (a * 16 + fr) * 32 + fq * 8);
-
-  // the window of this lane's pixel (rows past M gather zeros and are not stored)
-  const long long q = q0 + fr;
-  const int hw = p.OH * p.OW;
-  const int n = (int)(q / hw);
-  const int rem = (int)(q - (long long)n * hw);
-  const int oh = rem / p.OW, ow = rem - (rem / p.OW) * p.OW;
-  const f16* xb = reinterpret_cast<const f16*>(p.x) + (long long)n * p.H * p.W * p.xcs;
-  f16 v[27];
-#pragma unroll
-  for (int t = 0; t < 9; ++t) {
-    const int ih = oh * p.stride - p.pad + t / 3, iw = ow * p.stride - p.pad + t % 3;
-    f16x4 e = {};
-    if (q < M && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W)
-      e = *reinterpret_cast<const f16x4*>(xb + ((long long)ih * p.W + iw) * p.xcs);
-    v[3 * t] = e[0];
-    v[3 * t + 1] = e[1];
-    v[3 * t + 2] = e[2];
-  }
-  f16x8 b;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const f16 z = (f16)0.f;
-    const f16 g3 = 24 + e < 27 ? v[24 + e] : z;
-    b[e] = fq == 0 ? v[e] : (fq == 1 ? v[8 + e] : (fq == 2 ? v[16 + e] : g3));
-  }
-
-  char* my = stg[wave];
+  float bi[TC][4], sl[TC][4];
 #pragma unroll
   for (int a = 0; a < TC; ++a) {
-    f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[a], b, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-    const int ch = a * 16 + fq * 4;   // output rows of this lane: pixel fr, channels ch .. ch+3
-    float o[4];
+    wa[a] = *reinterpret_cast<const f16x8*>(wpk + (a * 16 + fr) * 32 + fq * 8);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      float x = acc[j] + bias[ch + j];
-      x = act_apply(x, p.act, slope ? slope[ch + j] : 0.f);
-      o[j] = ch + j < p.cout ? x : 0.f;   // channel padding stays exactly zero
+      bi[a][j] = bias[a * 16 + fq * 4 + j];
+      sl[a][j] = slope ? slope[a * 16 + fq * 4 + j] : 0.f;
     }
-    *reinterpret_cast<f16x4*>(my + fr * PITCH + ch * 2) = f16x4{(f16)o[0], (f16)o[1], (f16)o[2], (f16)o[3]};
   }
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const unsigned hw = (unsigned)(p.OH * p.OW);
+  const f16* xs = reinterpret_cast<const f16*>(p.x);
+  char* my = stg[wave];
   const int cw8 = cwrite >> 3;   // host guarantees cwrite % 8 == 0
+
+  for (int gi = 0; gi < kStemGroupsPerWave; ++gi) {
+    const int q0 = (g0 + gi) * 16;
+    if (q0 >= M) break;   // wave-uniform
+    // the window of this lane's pixel (rows past M gather zeros and are not stored)
+    const int q = q0 + fr;
+    const unsigned n = (unsigned)q / hw;
+    const unsigned rem = (unsigned)q - n * hw;
+    const int oh = (int)(rem / (unsigned)p.OW), ow = (int)(rem - (unsigned)oh * (unsigned)p.OW);
+    const f16* xb = xs + (size_t)n * p.H * p.W * p.xcs;
+    f16 v[27];
 #pragma unroll
-  for (int k = 0; k < (16 * CH8 + 63) / 64; ++k) {
-    const int idx = lane + k * 64;
-    const int pl = idx / CH8, cq = idx - (idx / CH8) * CH8;
-    if (pl >= 16 || cq >= cw8 || q0 + pl >= M) continue;
-    const f16x8 val = *reinterpret_cast<const f16x8*>(my + pl * PITCH + cq * 16);
-    *reinterpret_cast<f16x8*>(reinterpret_cast<f16*>(p.y) + (q0 + pl) * p.ycs + cq * 8) = val;
+    for (int t = 0; t < 9; ++t) {
+      const int ih = oh * p.stride - p.pad + t / 3, iw = ow * p.stride - p.pad + t % 3;
+      f16x4 e = {};
+      if (q < M && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W)
+        e = *reinterpret_cast<const f16x4*>(xb + ((size_t)ih * p.W + iw) * p.xcs);
+      v[3 * t] = e[0];
+      v[3 * t + 1] = e[1];
+      v[3 * t + 2] = e[2];
+    }
+    f16x8 b;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const f16 z = (f16)0.f;
+      const f16 g3 = 24 + e < 27 ? v[24 + e] : z;
+      b[e] = fq == 0 ? v[e] : (fq == 1 ? v[8 + e] : (fq == 2 ? v[16 + e] : g3));
+    }
+
+    // the previous group's staging reads are done before this group's writes
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int a = 0; a < TC; ++a) {
+      f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[a], b, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      const int ch = a * 16 + fq * 4;   // output rows of this lane: pixel fr, channels ch .. ch+3
+      float o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float x = acc[j] + bi[a][j];
+        x = act_apply(x, p.act, sl[a][j]);
+        o[j] = ch + j < p.cout ? x : 0.f;   // channel padding stays exactly zero
+      }
+      *reinterpret_cast<f16x4*>(my + fr * PITCH + ch * 2) = f16x4{(f16)o[0], (f16)o[1], (f16)o[2], (f16)o[3]};
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int k = 0; k < (16 * CH8 + 63) / 64; ++k) {
+      const int idx = lane + k * 64;
+      const int pl = idx / CH8, cq = idx - (idx / CH8) * CH8;
+      if (pl >= 16 || cq >= cw8 || q0 + pl >= M) continue;
+      const f16x8 val = *reinterpret_cast<const f16x8*>(my + pl * PITCH + cq * 16);
+      *reinterpret_cast<f16x8*>(reinterpret_cast<f16*>(p.y) + (size_t)(q0 + pl) * p.ycs + cq * 8) = val;
+    }
   }
 }
 
@@ -102,8 +123,9 @@ hipError_t stem_fused_launch(const StemParams& p, const void* wpk, const float* 
                              int cwrite, hipStream_t s) {
   const long long M = (long long)p.N * p.OH * p.OW;
   const long long groups = (M + 15) / 16;
-  const long long nwg = (groups + 3) / 4;
-  if (nwg <= 0 || nwg >= (1LL << 31) || p.xcs % 4 || (reinterpret_cast<uintptr_t>(p.y) & 15) ||
+  const long long waves = (groups + kStemGroupsPerWave - 1) / kStemGroupsPerWave;
+  const long long nwg = (waves + 3) / 4;
+  if (nwg <= 0 || M >= (1LL << 31) - 64 * kStemGroupsPerWave || p.xcs % 4 || (reinterpret_cast<uintptr_t>(p.y) & 15) ||
       (reinterpret_cast<uintptr_t>(p.x) & 7))
     return hipErrorInvalidValue;
   const f16* w = reinterpret_cast<const f16*>(wpk);

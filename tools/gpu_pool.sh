@@ -4,7 +4,7 @@
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$ROOT"
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_conv.py tests/test_gpu_scrfd.py tests/test_gpu_face_embedder.py tests/test_gpu_bench_config.py -m gpu -q -x --timeout 300 --timeout-method thread > gpurun_out/pool_tests.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread > gpurun_out/pool_tests.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pool_tests.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 > gpurun_out/bench_pool.log 2>&1
