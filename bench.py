@@ -39,7 +39,8 @@ def _dist_init():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("gloo", init_method="env://", world_size=world, rank=rank)
+        from person_capture_amd.shard import dist_timeout
+        dist.init_process_group("gloo", init_method="env://", world_size=world, rank=rank, timeout=dist_timeout())
     return world, rank, local
 
 
@@ -186,6 +187,9 @@ def main():
                     help="c3: BASELINE configs[2] (the metric's config, default); c4: full path with YOLOv8n "
                          "persons + per-crop SCRFD/ArcFace + CLIP ReID; c5: 4K pre-scan (INTER_AREA 416 wide, "
                          "SCRFD @384, 1 ArcFace forward, 1024-entry bank)")
+    ap.add_argument("--launch-timeout", type=float, default=1500.0,
+                    help="--gpus N self-launch: kill every rank if the job runs longer (seconds)")
+    ap.add_argument("--fail-rank", type=int, default=-1, help=argparse.SUPPRESS)   # launcher test hook
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: exercise the rank launcher, dist init and the timing/reduction protocol only")
     args = ap.parse_args()
@@ -193,7 +197,8 @@ def main():
         # --gpus N without torch.distributed.run: start N fresh rank processes (this process has not
         # touched the GPU) and exit with their status
         from person_capture_amd.shard import spawn_local_ranks
-        sys.exit(spawn_local_ranks([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], args.gpus))
+        sys.exit(spawn_local_ranks([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], args.gpus,
+                                   timeout=args.launch_timeout))
     if args.dry_run:
         return main_dry(args)
     if args.workload != "c3":
@@ -343,6 +348,8 @@ def main_dry(args):
     'processes' its contiguous share of a batch with a host stand-in, then the same
     barrier / max-over-ranks time / sum-over-ranks frames reduction as the real run."""
     from person_capture_amd.shard import shard_indices
+    if args.fail_rank >= 0 and int(os.environ.get("RANK", "0")) == args.fail_rank:
+        sys.exit(1)   # launcher test: this rank dies before the rendezvous
     world, rank, local = _dist_init()
     total = args.batch * max(1, world)
     mine = shard_indices(total, rank, world)

@@ -31,6 +31,10 @@ hipError_t conv_t2d_launch(const ConvParams& p, hipStream_t s);
 int conv_t2d_supported(int cin, int npad, int KH, int KW, int stride, int pad, int act, int out_f32, int ycs,
                        int ycoff);
 int conv_t2d_rows(int npad);
+int conv_chain_fits(int H, int W, int C, int npad, long long ktot);
+hipError_t conv_chain_launch(const void* x, int xcs, void* y, int ycs, const void* blk_dev, int nblk, int N, int H,
+                             int W, long long ktot, int dbg, hipStream_t s);
+size_t conv_chain_block_bytes();
 int stem_fused_ok(int f32, int cin, int cin_true, int KH, int KW, int npad, int cwrite, int ycs, int ycoff);
 hipError_t stem_fused_launch(const StemParams& p, const void* wpk, const float* bias, const float* slope, int npad,
                              int cwrite, hipStream_t s);
@@ -139,6 +143,7 @@ struct pc_ctx {
   int* cand_count = nullptr;
   float* det_scale = nullptr;
   size_t cand_bytes = 0;
+  size_t cand_images = 0;     // images cand_count / det_scale hold
   // large-candidate NMS scratch (scrfd_nms_big): sort keys, anchor -> slot map, kept boxes
   void* nms_big = nullptr;
   size_t nms_big_bytes = 0;
@@ -363,7 +368,15 @@ struct StemPlan {
   float* bias = nullptr;    // [npad]
   float* slope = nullptr;   // [npad] or null
 };
-struct ProfRec { int a, b, kind; double flops; int op = -1; };
+struct ProfRec { int a, b, kind; double flops; int op = -1; int code = -1; };
+// A run of IResNet identity blocks executed by the resident chain kernel
+// (pc_conv_chain.hip): ops [first, first + 2*nblk) of the program.
+struct ChainBlockH { const void* w1; const float* b1; const float* s1; const void* w2; const float* b2; };
+struct ChainPlan {
+  int first = -1, nblk = 0, in_t = -1, out_t = -1;
+  void* d_blk = nullptr;          // ChainBlockH[nblk] on the device
+  double flops_per_image = 0.0;
+};
 
 struct pc_net {
   pc_ctx* ctx = nullptr;
@@ -378,6 +391,9 @@ struct pc_net {
   std::vector<long long> array_count;
   std::vector<ConvPlan> plans;
   std::vector<StemPlan> stems;
+  std::vector<ChainPlan> chains;
+  std::vector<int> chain_at;      // op index -> chain id (first op of a chain) or -1
+  int chain_min_batch = 1 << 30;   // off until PC_CHAIN_MIN (measured crossover pending)
   std::vector<const float*> host_arrays;   // program arrays, valid during pc_net_create only
   void* stem_col = nullptr;   // im2col scratch shared by the stems
   float* partial = nullptr;
@@ -613,6 +629,91 @@ static int plan_stem(pc_net* n, const NetOp& op, StemPlan& st, size_t& col_bytes
   return PC_OK;
 }
 
+// Runs of IResNet identity blocks that the resident chain kernel (pc_conv_chain.hip) can
+// execute as one launch: conv1 = 3x3/s1 over X with the border-class bias and PReLU,
+// conv2 = 3x3/s1 over conv1's output + bias + residual X, 256 channels, images of at
+// most 199 pixels, f16. Every tensor between the chain's first input and its last output
+// must be read only inside the chain (the kernel never writes them).
+static int plan_chains(pc_net* n) {
+  n->chain_at.assign(n->ops.size(), -1);
+  if (n->f32) return PC_OK;
+  if (const char* e = getenv("PC_CHAIN")) if (atoi(e) == 0) return PC_OK;
+  if (const char* e = getenv("PC_CHAIN_MIN")) n->chain_min_batch = std::max(1, atoi(e));
+  if ((size_t)conv_chain_block_bytes() != sizeof(ChainBlockH)) return fail(n->ctx, PC_ERR_HIP, "chain block layout");
+  const int nt = (int)n->tens.size();
+  std::vector<int> uses(nt, 0);
+  for (auto& op : n->ops) {
+    if (op.w[0] == OP_CONV) {
+      for (int s = 0; s < op.w[2]; ++s) uses[op.w[3 + 5 * s]]++;
+      if (op.w[21] >= 0) uses[op.w[21]]++;
+    } else if (op.w[0] == OP_STEM || op.w[0] == OP_MAXPOOL || op.w[0] == OP_UPSAMPLE || op.w[0] == OP_LAYERNORM ||
+               op.w[0] == OP_ATTENTION) {
+      uses[op.w[2]]++;
+    }
+  }
+  for (int o : n->outs) if (o >= 0 && o < nt) uses[o] += 1000;
+  auto is_block = [&](size_t i, int X) -> int {   // output tensor of the block at ops i, i+1, or -1
+    if (i + 1 >= n->ops.size()) return -1;
+    const int* a = n->ops[i].w;
+    const int* b = n->ops[i + 1].w;
+    if (a[0] != OP_CONV || b[0] != OP_CONV || a[2] != 1 || b[2] != 1) return -1;
+    if (a[3] != X || a[4] != 3 || a[5] != 3 || a[6] != 1 || a[7] != 1) return -1;
+    if (a[14] != 256 || a[16] != 256 || a[18] != BIAS_BORDER9 || a[17] < 0 || a[19] < 0 || a[20] != ACT_PRELU ||
+        a[21] >= 0 || a[24] > 1 || a[23] != 0)
+      return -1;
+    const int Y1 = a[1];
+    if (b[3] != Y1 || b[4] != 3 || b[5] != 3 || b[6] != 1 || b[7] != 1) return -1;
+    if (b[14] != 256 || b[16] != 256 || b[18] != BIAS_CHANNEL || b[17] < 0 || b[20] != ACT_NONE || b[21] != X ||
+        b[22] != RES_SAME || b[23] != 0 || b[24] > 1 || a[15] != b[15])
+      return -1;
+    const NetTensor &TX = n->tens[X], &T1 = n->tens[Y1], &T2 = n->tens[b[1]];
+    if (TX.is_f32 || T1.is_f32 || T2.is_f32 || TX.buf < 0 || T2.buf < 0) return -1;
+    if (TX.C != 256 || T1.C != 256 || T2.C != 256 || T1.H != TX.H || T1.W != TX.W || T2.H != TX.H || T2.W != TX.W)
+      return -1;
+    if (!conv_chain_fits(TX.H, TX.W, TX.C, a[14], a[15])) return -1;
+    if (uses[Y1] != 1) return -1;   // conv1's output feeds conv2 only
+    return b[1];
+  };
+  for (size_t i = 0; i + 1 < n->ops.size();) {
+    const int X = n->ops[i].w[0] == OP_CONV ? n->ops[i].w[3] : -1;
+    int out = X >= 0 ? is_block(i, X) : -1;
+    if (out < 0) { ++i; continue; }
+    ChainPlan ch;
+    ch.first = (int)i;
+    ch.in_t = X;
+    ch.nblk = 1;
+    // X is read twice by the first block (conv1 input and residual); later block inputs
+    // must be read by their block only
+    while (uses[out] == 2) {
+      const int nxt = is_block(i + 2 * ch.nblk, out);
+      if (nxt < 0) break;
+      out = nxt;
+      ch.nblk++;
+    }
+    ch.out_t = out;
+    const NetTensor &TX = n->tens[X], &TY = n->tens[out];
+    const bool alias_ok = TX.buf != TY.buf || (TX.cs == TY.cs && TX.coff == TY.coff);
+    if (ch.nblk < 2 || !alias_ok || (TX.cs & 7) || (TY.cs & 7) || (TX.coff & 7) || (TY.coff & 7)) {
+      i += 2 * ch.nblk;
+      continue;
+    }
+    std::vector<ChainBlockH> hb(ch.nblk);
+    for (int k = 0; k < ch.nblk; ++k) {
+      const int* a = n->ops[i + 2 * k].w;
+      const int* b = n->ops[i + 2 * k + 1].w;
+      hb[k] = ChainBlockH{n->arrays[a[13]], (const float*)n->arrays[a[17]], (const float*)n->arrays[a[19]],
+                          n->arrays[b[13]], (const float*)n->arrays[b[17]]};
+      ch.flops_per_image += n->plans[i + 2 * k].flops_per_image + n->plans[i + 2 * k + 1].flops_per_image;
+    }
+    HIPCHK(n->ctx, hipMalloc(&ch.d_blk, hb.size() * sizeof(ChainBlockH)));
+    HIPCHK(n->ctx, hipMemcpy(ch.d_blk, hb.data(), hb.size() * sizeof(ChainBlockH), hipMemcpyHostToDevice));
+    n->chain_at[i] = (int)n->chains.size();
+    n->chains.push_back(ch);
+    i += 2 * ch.nblk;
+  }
+  return PC_OK;
+}
+
 extern "C" int pc_net_create(pc_ctx* c, const void* prog, size_t nbytes, int precision, int max_batch, pc_net** out) {
   if (!c || !prog || !out || max_batch <= 0) return fail(c, PC_ERR_ARG, "pc_net_create: bad arguments");
   *out = nullptr;
@@ -748,6 +849,7 @@ extern "C" int pc_net_create(pc_ctx* c, const void* prog, size_t nbytes, int pre
     }
   }
   n->host_arrays.clear();
+  if (rc == PC_OK) rc = plan_chains(n);
   if (rc == PC_OK && stem_col_bytes) {
     if (hipMalloc(&n->stem_col, stem_col_bytes) != hipSuccess) rc = fail(c, PC_ERR_HIP, "stem im2col workspace");
     else hipMemset(n->stem_col, 0, stem_col_bytes);
@@ -780,6 +882,7 @@ extern "C" int pc_net_destroy(pc_net* n) {
     if (st.slope) hipFree(st.slope);
   }
   if (n->stem_col) hipFree(n->stem_col);
+  for (auto& ch : n->chains) if (ch.d_blk) hipFree(ch.d_blk);
   delete n;
   return PC_OK;
 }
@@ -805,6 +908,32 @@ static int run_ops(pc_net* n, int N) {
   int open_ev = -1;
   for (size_t i = 0; i < n->ops.size(); ++i) {
     const int* w = n->ops[i].w;
+    if (!n->chain_at.empty() && n->chain_at[i] >= 0 && N >= n->chain_min_batch) {
+      // a run of identity blocks as one resident-chain launch (pc_conv_chain.hip)
+      const ChainPlan& ch = n->chains[n->chain_at[i]];
+      ProfRec rec{-1, -1, OP_CONV, ch.flops_per_image * N, (int)i, 300};
+      if (prof) {
+        if (open_ev >= 0) {
+          rec.a = open_ev;
+        } else {
+          int rc = prof_event(n, &rec.a);
+          if (rc) return rc;
+        }
+      }
+      const NetTensor &TX = n->tens[ch.in_t], &TY = n->tens[ch.out_t];
+      int dbg = 0;
+      if (const char* e = getenv("PC_CONV_DBG")) dbg = atoi(e);
+      HIPCHK(c, conv_chain_launch(tensor_ptr(n, ch.in_t), TX.cs, tensor_ptr(n, ch.out_t), TY.cs, ch.d_blk, ch.nblk, N,
+                                  TX.H, TX.W, n->ops[i].w[15], dbg, s));
+      if (prof) {
+        int rc = prof_event(n, &rec.b);
+        if (rc) return rc;
+        n->recs.push_back(rec);
+        open_ev = rec.b;
+      }
+      i += 2 * ch.nblk - 1;
+      continue;
+    }
     ProfRec rec{-1, -1, w[0], w[0] == OP_CONV ? n->plans[i].flops_per_image * N : 0.0, (int)i};
     if (prof) {
       if (open_ev >= 0) {
@@ -890,7 +1019,8 @@ static int run_ops(pc_net* n, int N) {
       const StemPlan& st = n->stems[i];
       const int st_cwrite = std::min(Y.C, st.npad);
       // fused gather + MFMA stem (pc_stem.hip) unless PC_STEM_UNFUSED is set
-      const bool fused = st.use_mfma && !getenv("PC_STEM_UNFUSED") &&
+      // (stem_fused stores f16: an f32 output tensor inside an f16 net takes the unfused path)
+      const bool fused = st.use_mfma && !getenv("PC_STEM_UNFUSED") && !Y.is_f32 &&
                          stem_fused_ok(n->f32, X.C, st.cin_true, p.KH, p.KW, st.npad, st_cwrite, Y.cs, Y.coff) &&
                          X.cs % 4 == 0 && (reinterpret_cast<uintptr_t>(p.x) & 7) == 0 &&
                          (reinterpret_cast<uintptr_t>(p.y) & 15) == 0;
@@ -1016,7 +1146,7 @@ extern "C" int pc_net_profile_ops(pc_net* n, double* out, int max_recs) {
     double* o = out + 6 * k++;
     const bool conv = r.op >= 0 && n->ops[r.op].w[0] == OP_CONV;
     o[0] = r.op; o[1] = r.kind; o[2] = ms; o[3] = r.flops;
-    o[4] = conv ? (n->plans[r.op].t2d >= 0 ? 200 + n->plans[r.op].t2d
+    o[4] = r.code >= 0 ? r.code : conv ? (n->plans[r.op].t2d >= 0 ? 200 + n->plans[r.op].t2d
                   : n->plans[r.op].fast >= 0 ? 100 + n->plans[r.op].fast : n->plans[r.op].halo) : -1;
     o[5] = conv ? n->plans[r.op].cfg : -1;
   }
@@ -1213,14 +1343,24 @@ extern "C" int pc_scrfd_detect(pc_net* net, const pc_letterbox_desc* h, int n, i
   int pcap = 8192;
   while (pcap < cap) pcap <<= 1;
   const size_t cand_need = (size_t)n * cap * 16 * 4;
+  // the candidate rows and the per-image counters are sized independently: a later call
+  // with more images but a smaller D needs fewer rows and more counters
   if (c->cand_bytes < cand_need) {
     if (c->cand) hipFree(c->cand);
+    c->cand = nullptr;
+    c->cand_bytes = 0;
+    HIPCHK(c, hipMalloc((void**)&c->cand, cand_need));
+    c->cand_bytes = cand_need;
+  }
+  if (c->cand_images < (size_t)n) {
     if (c->cand_count) hipFree(c->cand_count);
     if (c->det_scale) hipFree(c->det_scale);
-    HIPCHK(c, hipMalloc((void**)&c->cand, cand_need));
+    c->cand_count = nullptr;
+    c->det_scale = nullptr;
+    c->cand_images = 0;
     HIPCHK(c, hipMalloc((void**)&c->cand_count, (size_t)n * 4 + 256));
     HIPCHK(c, hipMalloc((void**)&c->det_scale, (size_t)n * 4 + 256));
-    c->cand_bytes = cand_need;
+    c->cand_images = n;
   }
   const size_t keys_b = (size_t)n * pcap * 8, map_b = (size_t)n * cap * 4, kept_b = (size_t)n * cap * 16;
   if (c->nms_big_bytes < keys_b + map_b + kept_b) {

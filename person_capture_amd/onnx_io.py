@@ -141,10 +141,25 @@ def _tensor(buf: memoryview, base_dir: Optional[str]) -> Tuple[str, np.ndarray]:
     if ext:
         if base_dir is None:
             raise ValueError(f"tensor {name!r} has external data but the model was not read from a file")
-        with open(os.path.join(base_dir, ext["location"]), "rb") as fh:
-            fh.seek(int(ext.get("offset", 0)))
-            n = int(ext["length"]) if "length" in ext else int(np.prod(dims)) * dt.itemsize
+        loc = ext.get("location", "")
+        # external data must stay inside the model's directory (the onnx package's own
+        # checks, CVE-2022-25882 / CVE-2024-27318): no absolute paths, no escape via '..'
+        # or symlinks
+        if not loc or os.path.isabs(loc):
+            raise ValueError(f"tensor {name!r}: external data location {loc!r} is not a relative path")
+        root = os.path.realpath(base_dir)
+        path = os.path.realpath(os.path.join(root, loc))
+        if os.path.commonpath([root, path]) != root:
+            raise ValueError(f"tensor {name!r}: external data location {loc!r} leaves the model directory")
+        off = int(ext.get("offset", 0))
+        n = int(ext["length"]) if "length" in ext else int(np.prod(dims)) * dt.itemsize
+        if off < 0 or n < 0:
+            raise ValueError(f"tensor {name!r}: negative external data offset/length")
+        with open(path, "rb") as fh:
+            fh.seek(off)
             raw = fh.read(n)
+        if len(raw) != n:
+            raise ValueError(f"tensor {name!r}: external data truncated ({len(raw)} of {n} bytes)")
     if raw is not None:
         arr = np.frombuffer(raw, dt).copy()
     elif dtype in (1,):

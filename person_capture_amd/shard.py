@@ -73,21 +73,60 @@ def _free_port() -> int:
     return port
 
 
-def spawn_local_ranks(cmd: Sequence[str], world: int, env: Optional[dict] = None) -> int:
+def spawn_local_ranks(cmd: Sequence[str], world: int, env: Optional[dict] = None, timeout: Optional[float] = None,
+                      poll_s: float = 0.2, grace_s: float = 5.0) -> int:
     """Start `world` rank processes of `cmd` on this node with the torch.distributed.run
     environment (RANK, LOCAL_RANK, WORLD_SIZE, LOCAL_WORLD_SIZE, MASTER_ADDR=127.0.0.1,
     MASTER_PORT). The caller must not have touched the GPU: the ranks are fresh
-    processes (no exec of the caller). Returns the first non-zero exit code, else 0."""
+    processes (no exec of the caller).
+
+    Fail fast like torchrun: the children are polled together, and the first rank that
+    exits non-zero (or the whole job running past `timeout` seconds) terminates its
+    siblings (SIGTERM, then SIGKILL after `grace_s`) instead of leaving them blocked in
+    the rendezvous or a barrier. Returns that rank's exit code (124 on timeout), else 0."""
     import subprocess
+    import time
     port = _free_port()
     base = dict(os.environ if env is None else env)
+    base.setdefault("PC_DIST_TIMEOUT_S", str(int(timeout)) if timeout else "300")
     procs = []
     for r in range(world):
         e = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
                  GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen(list(cmd), env=e))
-    rcs = [p.wait() for p in procs]
-    return next((rc for rc in rcs if rc != 0), 0)
+    t0 = time.monotonic()
+    failed = 0
+    while True:
+        rcs = [p.poll() for p in procs]
+        bad = [rc for rc in rcs if rc is not None and rc != 0]
+        if bad:
+            failed = bad[0]
+            break
+        if all(rc == 0 for rc in rcs):
+            return 0
+        if timeout is not None and time.monotonic() - t0 > timeout:
+            failed = 124
+            break
+        time.sleep(poll_s)
+    # a rank failed (or the job timed out): take the others down
+    for p in procs:
+        if p.poll() is None:
+            p.terminate()
+    t1 = time.monotonic()
+    while any(p.poll() is None for p in procs) and time.monotonic() - t1 < grace_s:
+        time.sleep(0.05)
+    for p in procs:
+        if p.poll() is None:
+            p.kill()
+            p.wait()
+    return failed
+
+
+def dist_timeout():
+    """Rendezvous / collective timeout of the host process group (gloo): a rank whose
+    peer died returns an error in seconds instead of gloo's 30-minute default."""
+    import datetime
+    return datetime.timedelta(seconds=float(os.environ.get("PC_DIST_TIMEOUT_S", "300")))
 
 
 def device_for_rank(local_rank: int) -> int:

@@ -81,3 +81,37 @@ def test_find_model_file(tmp_path, monkeypatch):
     monkeypatch.setenv("PERSON_CAPTURE_AMD_MODELS", str(tmp_path))
     assert onnx_models.find_model_file("scrfd_10g_bnkps.onnx") == str(f.resolve())
     assert onnx_models.find_model_file("missing_model.onnx") is None
+
+
+def _ext_tensor(name: str, location: str, n: int) -> bytes:
+    """TensorProto (wire format) of a float32 [n] tensor whose bytes live in an external file."""
+    def entry(k, v):
+        return onnx_io._ld(1, k.encode()) + onnx_io._ld(2, v.encode())
+    body = b""
+    body += onnx_io._key(1, 0) + onnx_io._enc_varint(n)          # dims
+    body += onnx_io._key(2, 0) + onnx_io._enc_varint(1)          # data_type FLOAT
+    body += onnx_io._ld(8, name.encode())
+    body += onnx_io._ld(13, entry("location", location))
+    body += onnx_io._ld(13, entry("length", str(4 * n)))
+    body += onnx_io._key(14, 0) + onnx_io._enc_varint(1)         # data_location EXTERNAL
+    return body
+
+
+@pytest.mark.parametrize("loc", ["w.bin", "../escape.bin", "/etc/hostname", "sub/../w.bin"])
+def test_external_data_stays_in_model_dir(tmp_path, loc):
+    """External tensor data is read only from inside the model directory (as the onnx
+    package enforces, CVE-2022-25882 / CVE-2024-27318); a truncated file is an error."""
+    (tmp_path / "m").mkdir()
+    np.arange(4, dtype=np.float32).tofile(tmp_path / "m" / "w.bin")
+    np.arange(4, dtype=np.float32).tofile(tmp_path / "escape.bin")
+    raw = _ext_tensor("w", loc, 4)
+    if loc in ("w.bin", "sub/../w.bin"):
+        if loc.startswith("sub"):
+            (tmp_path / "m" / "sub").mkdir()
+        name, arr = onnx_io._tensor(memoryview(raw), str(tmp_path / "m"))
+        assert name == "w" and np.array_equal(arr, np.arange(4, dtype=np.float32))
+    else:
+        with pytest.raises(ValueError):
+            onnx_io._tensor(memoryview(raw), str(tmp_path / "m"))
+    with pytest.raises(ValueError):
+        onnx_io._tensor(memoryview(_ext_tensor("w", "w.bin", 8)), str(tmp_path / "m"))

@@ -87,3 +87,42 @@ def test_bench_launcher_world2():
     assert len(lines) == 1, r.stdout
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["frames"] == 2 * 5 * 3 and out["local_rank"] == 0
+
+
+def test_bench_launcher_fails_fast():
+    """One of two ranks exits 1 before the rendezvous: the launcher takes the other rank
+    (blocked in init_process_group) down and returns non-zero within seconds, instead of
+    hanging until gloo's timeout."""
+    import subprocess
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    t = time.monotonic()
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run", "--steps", "1",
+                        "--batch", "2", "--fail-rank", "1"], capture_output=True, text=True, timeout=120, env=env)
+    dt = time.monotonic() - t
+    assert r.returncode != 0
+    assert dt < 60, dt
+
+
+def test_spawn_timeout_kills_ranks():
+    import sys
+    import time
+    from person_capture_amd.shard import spawn_local_ranks
+    t = time.monotonic()
+    rc = spawn_local_ranks([sys.executable, "-c", "import time; time.sleep(600)"], 2, timeout=2.0, grace_s=2.0)
+    assert rc == 124 and time.monotonic() - t < 30
+
+
+def test_bench_dry_run_c5_world2():
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run", "--workload",
+                        "c5", "--steps", "2", "--batch", "3"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1 and json.loads(lines[0])["n_gpus"] == 2
