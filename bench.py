@@ -120,9 +120,56 @@ def cpu_baseline(frames: np.ndarray, fe, bank: np.ndarray, n_sample: int, n_samp
     return out
 
 
+def f16_parity(res16, frames, devs, bank_h) -> dict:
+    """Outside the timed region: the same frames through an f32 FaceEmbedder (the parity mode,
+    itself checked against the fp32 CPU oracle in tests/test_gpu_bench_config.py) against the
+    benched f16 results, face by face (nearest box): how many decisions the f16 throughput mode
+    changes. f16 is the precision of the reference's TensorRT engines (face_embedder.py:1058)."""
+    old = os.environ.get("PERSON_CAPTURE_AMD_PRECISION")
+    os.environ["PERSON_CAPTURE_AMD_PRECISION"] = "f32"
+    try:
+        from person_capture_amd.face_embedder import FaceEmbedder
+        from person_capture_amd.match import DeviceBank
+        fe32 = FaceEmbedder(ctx=f"cuda:{_device(int(os.environ.get('LOCAL_RANK', '0')))}",
+                            yolo_model="scrfd_10g_bnkps", conf=0.5)
+        bank32 = DeviceBank(fe32._ctx, bank_h)
+        res32 = fe32.extract_batch([None] * len(devs), dev_frames=devs, bank=bank32)
+        fe32._ctx.sync()
+    finally:
+        if old is None:
+            os.environ.pop("PERSON_CAPTURE_AMD_PRECISION", None)
+        else:
+            os.environ["PERSON_CAPTURE_AMD_PRECISION"] = old
+    n = count_mis = box_mis = acc_mis = acc_mis_45 = 0
+    worst_fd = 0.0
+    near = []
+    for a16, a32 in zip(res16, res32):
+        count_mis += abs(len(a16) - len(a32))
+        for b in a32:
+            n += 1
+            a = min(a16, key=lambda f: int(np.abs(f["bbox"].astype(np.int64) - b["bbox"]).sum())) if a16 else None
+            if a is None:
+                box_mis += 1
+                continue
+            if not np.array_equal(a["bbox"], b["bbox"]):
+                box_mis += 1
+            d = abs(float(a["fd"]) - float(b["fd"]))
+            worst_fd = max(worst_fd, d)
+            if (a["fd"] <= 0.32) != (b["fd"] <= 0.32):
+                acc_mis += 1
+                near.append(round(abs(float(b["fd"]) - 0.32), 5))
+            acc_mis_45 += (a["fd"] <= 0.45) != (b["fd"] <= 0.45)
+    return {"reference": "same frames, f32 parity mode on the device", "faces_f32": n,
+            "face_count_mismatch": count_mis, "box_mismatch": box_mis, "accept_mismatch_0.32": acc_mis,
+            "accept_mismatch_0.45": acc_mis_45, "accept_mismatch_frac_0.32": round(acc_mis / max(1, n), 4),
+            "max_fd_diff": round(worst_fd, 6), "flipped_faces_f32_distance_to_0.32": sorted(near)}
+
+
 def _kernel_of(code: float, cfg: float) -> str:
     """Planner code of a profiled conv launch (pc_net_profile_ops) -> kernel instantiation."""
     c = int(code)
+    if c == 300:
+        return "conv_chain (resident IResNet block chain, pc_conv_chain.hip)"
     if c >= 200:
         return f"conv_t2d (2-D block kernel, variant {c - 200})"
     if c >= 100:
@@ -182,9 +229,11 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=48)
     ap.add_argument("--cpu-sample-1t", type=int, default=4)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-parity", action="store_true", help="skip the f16-vs-f32 decision parity pass")
     ap.add_argument("--precision", default="f16", choices=["f16", "f32"])
-    ap.add_argument("--workload", default="c3", choices=["c3", "c4", "c5"],
-                    help="c3: BASELINE configs[2] (the metric's config, default); c4: full path with YOLOv8n "
+    ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c4", "c5"],
+                    help="c3: BASELINE configs[2] (the metric's config, default); c2: ArcFace-R100 embed only at "
+                         "batch 256 (the north star's MFMA target); c4: full path with YOLOv8n "
                          "persons + per-crop SCRFD/ArcFace + CLIP ReID; c5: 4K pre-scan (INTER_AREA 416 wide, "
                          "SCRFD @384, 1 ArcFace forward, 1024-entry bank)")
     ap.add_argument("--launch-timeout", type=float, default=1500.0,
@@ -201,6 +250,8 @@ def main():
                                    timeout=args.launch_timeout))
     if args.dry_run:
         return main_dry(args)
+    if args.workload == "c2":
+        return main_c2(args)
     if args.workload != "c3":
         return main_other(args)
 
@@ -322,6 +373,8 @@ def main():
                      "dominant_kernel_rocprof": dominant},
         "cpu_baseline": None,
     }
+    if rank == 0 and args.precision == "f16" and not args.no_parity:
+        out["parity"] = f16_parity(res, frames, devs, bank_h)
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(frames, fe, bank_h, args.cpu_sample, args.cpu_sample_1t)
     if rank == 0:
@@ -341,6 +394,78 @@ def _timed(world, ctx, steps, step):
     t1 = time.perf_counter()
     _barrier(world)
     return _max_over_ranks(world, t1 - t0), t1 - t0
+
+
+def main_c2(args):
+    """C2 (BASELINE configs[1]): ArcFace-R100 embed only, batch 256 aligned 112x112 faces, f16,
+    one GPU per rank. One step = pc_arcface_embed over 256 device-resident u8 chips (preprocess
+    -> IResNet-100 -> L2) without flip, i.e. 256 forward rows: the batch the north star's
+    '>= 50 % MFMA at batch 256' is quoted on. The flip-TTA form the reference's
+    _arcface_encode runs (face_embedder.py:1290-1389: 256 faces = 512 rows) is timed beside it
+    (flip_tta). roofline: the whole network's algorithmic FLOPs / step time (all of its MFMA
+    work), plus the dominant kernel's own launch rate."""
+    world, rank, local = _dist_init()
+    local = _device(local)
+    from person_capture_amd import models
+    from person_capture_amd._lib import PC_PREC_F16, PC_PREC_F32
+    from person_capture_amd.engines import ArcFaceEngine
+    from person_capture_amd.runtime import GpuContext
+    B = 256
+    ctx = GpuContext(local)
+    prec = PC_PREC_F16 if args.precision == "f16" else PC_PREC_F32
+    eng = ArcFaceEngine(ctx, models.synth_iresnet(100, seed=0), 100, precision=prec, max_batch=2 * B)
+    chips = np.random.default_rng(20260505 + rank).integers(0, 256, (B, 112, 112, 3), dtype=np.uint8)
+    d_chips = ctx.upload(chips)
+    d_out = ctx.alloc(B * eng.dim * 4)
+    for _ in range(max(1, args.warmup)):
+        eng.embed_device(d_chips.ptr, B, False, d_out.ptr)
+        eng.embed_device(d_chips.ptr, B, True, d_out.ptr)
+    ctx.sync()
+    elapsed, _ = _timed(world, ctx, args.steps, lambda: eng.embed_device(d_chips.ptr, B, False, d_out.ptr))
+    t_flip, _ = _timed(world, ctx, args.steps, lambda: eng.embed_device(d_chips.ptr, B, True, d_out.ptr))
+    # per-launch split of one profiled step (HIP events on the net's stream)
+    eng.net.profile(True)
+    eng.embed_device(d_chips.ptr, B, False, d_out.ptr)
+    dom = dominant_conv([eng.net], ("arcface",))
+    recs = eng.net.profile_ops()
+    eng.net.profile(False)
+    peak = PEAK_F16_TFLOPS if args.precision == "f16" else PEAK_F32_TFLOPS
+    fl = eng.flops_per_forward * B
+    ms = elapsed / args.steps * 1e3
+    net_tf = fl / (ms * 1e-3) / 1e12
+    split = {}
+    for op, kind, t, f, code, cfg in recs:
+        k = _kernel_of(code, cfg) if f > 0 else "other"
+        a = split.setdefault(k, [0, 0.0, 0.0])
+        a[0] += 1; a[1] += t; a[2] += f
+    total_faces = _sum_over_ranks(world, B * args.steps)
+    out = {
+        "metric": "ArcFace-R100 embeddings/sec at batch 256 (C2); MFMA util %",
+        "value": round(total_faces / elapsed, 2), "unit": "faces/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": args.precision,
+        "data": "synthetic (seeded u8 112x112 chips, seeded synthetic IResNet-100 weights)",
+        "config": {"workload": "C2: ArcFace-R100 embed only, batch 256 aligned 112x112 faces (256 forward rows), "
+                               "preprocess + IResNet-100 + L2 on device", "batch": B,
+                   "parallelism": f"replica x{world} (no collective)"},
+        "roofline": {"bound": "mfma", "achieved": round(net_tf, 2), "peak": peak, "unit": "TFLOP/s",
+                     "frac": round(net_tf / peak, 4), "traffic": None,
+                     "scope": "whole IResNet-100 forward: algorithmic conv FLOPs of 256 rows / step time "
+                              f"({fl / 1e12:.3f} TFLOP per step)",
+                     "dominant_kernel": dom,
+                     "per_kernel": {k: {"launches": v[0], "ms": round(v[1], 4),
+                                        "tflops": round(v[2] / (v[1] * 1e-3) / 1e12, 1) if v[1] > 0 and v[2] > 0
+                                        else None} for k, v in sorted(split.items(), key=lambda kv: -kv[1][1])}},
+        "flip_tta": {"faces_per_step": B, "rows": 2 * B, "ms_per_step": round(t_flip / args.steps * 1e3, 4),
+                     "faces_per_s": round(_sum_over_ranks(world, B * args.steps) / t_flip, 2),
+                     "tflops": round(2 * fl / (t_flip / args.steps) / 1e12, 2)},
+        "cpu_baseline": None,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
 
 
 def main_dry(args):

@@ -184,6 +184,11 @@ int pc_net_output(pc_net* net, int index, void** d_ptr, int32_t* h_dims5 /* H, W
 int pc_net_num_outputs(pc_net* net);
 /* algorithmic FLOPs per image (2*MAC over all conv layers) and kernel launches per run */
 int pc_net_stats(pc_net* net, double* h_flops_per_image, int32_t* h_launches);
+/* resident block chains of the net (pc_conv_chain: runs of IResNet identity blocks executed
+ * one image per workgroup): returns their count; *h_min_batch = the batch from which they
+ * are used, *h_images_per_round = images one round of workgroups covers (the CU count).
+ * (No reference counterpart: a scheduling hint for FaceEmbedder's ArcFace batch quantum.) */
+int pc_net_chain_info(pc_net* net, int32_t* h_min_batch, int32_t* h_images_per_round);
 /* capture pc_net_run(batch) into a HIP graph and replay it on later runs of the same batch */
 int pc_net_set_graph(pc_net* net, int enable);
 /* HIP-event timing of every op of every later (non-graph) run; enable resets the counters.

@@ -375,6 +375,8 @@ struct ChainBlockH { const void* w1; const float* b1; const float* s1; const voi
 struct ChainPlan {
   int first = -1, nblk = 0, in_t = -1, out_t = -1;
   void* d_blk = nullptr;          // ChainBlockH[nblk] on the device
+  void* d_wpack = nullptr;        // the blocks' conv weights repacked (layout wl), or null
+  int wl = 0;                     // weight layout the kernel reads (pc_conv_chain.hip WL)
   double flops_per_image = 0.0;
 };
 
@@ -393,7 +395,7 @@ struct pc_net {
   std::vector<StemPlan> stems;
   std::vector<ChainPlan> chains;
   std::vector<int> chain_at;      // op index -> chain id (first op of a chain) or -1
-  int chain_min_batch = 1 << 30;   // off until PC_CHAIN_MIN (measured crossover pending)
+  int chain_min_batch = 32;       // PC_CHAIN_MIN overrides (tuning)
   std::vector<const float*> host_arrays;   // program arrays, valid during pc_net_create only
   void* stem_col = nullptr;   // im2col scratch shared by the stems
   float* partial = nullptr;
@@ -698,11 +700,39 @@ static int plan_chains(pc_net* n) {
       continue;
     }
     std::vector<ChainBlockH> hb(ch.nblk);
+    // weight layout of the kernel's register stream (tuning: PC_CHAIN_WL): 0 the convs'
+    // own [256][ktot] rows; 1 / 2 repacked fragment-major, 1 KiB per (K-step j, channel
+    // group g, row block a) holding W[g*64 + a*16 + (l & 15)][j*32 + (l >> 4)*8 .. +7] at
+    // +16*l, ordered [j][g][a] (1) or [g][a][j] (2)
+    ch.wl = 0;
+    if (const char* e = getenv("PC_CHAIN_WL")) ch.wl = atoi(e) == 2 ? 2 : 0;
+    const size_t cbytes = (size_t)72 * 256 * 64;
+    if (ch.wl) {
+      HIPCHK(n->ctx, hipMalloc(&ch.d_wpack, cbytes * 2 * ch.nblk));
+      const long long ktot = n->ops[i].w[15];
+      std::vector<_Float16> src((size_t)256 * ktot), dst(cbytes / 2);
+      for (int cv = 0; cv < 2 * ch.nblk; ++cv) {
+        const int* w = n->ops[i + cv].w;
+        HIPCHK(n->ctx, hipMemcpy(src.data(), n->arrays[w[13]], src.size() * 2, hipMemcpyDeviceToHost));
+        for (int j = 0; j < 72; ++j)
+          for (int g = 0; g < 4; ++g)
+            for (int a = 0; a < 4; ++a)
+              for (int l = 0; l < 64; ++l) {
+                const _Float16* sp = &src[(size_t)(g * 64 + a * 16 + (l & 15)) * ktot + j * 32 + (l >> 4) * 8];
+                const size_t blk1k = ch.wl == 1 ? ((size_t)j * 4 + g) * 4 + a : ((size_t)g * 4 + a) * 72 + j;
+                _Float16* dp = &dst[(blk1k * 64 + l) * 8];
+                for (int e = 0; e < 8; ++e) dp[e] = sp[e];
+              }
+        HIPCHK(n->ctx, hipMemcpy((char*)ch.d_wpack + cbytes * cv, dst.data(), cbytes, hipMemcpyHostToDevice));
+      }
+    }
     for (int k = 0; k < ch.nblk; ++k) {
       const int* a = n->ops[i + 2 * k].w;
       const int* b = n->ops[i + 2 * k + 1].w;
-      hb[k] = ChainBlockH{n->arrays[a[13]], (const float*)n->arrays[a[17]], (const float*)n->arrays[a[19]],
-                          n->arrays[b[13]], (const float*)n->arrays[b[17]]};
+      const void* w1 = ch.wl ? (const void*)((char*)ch.d_wpack + cbytes * (2 * k)) : n->arrays[a[13]];
+      const void* w2 = ch.wl ? (const void*)((char*)ch.d_wpack + cbytes * (2 * k + 1)) : n->arrays[b[13]];
+      hb[k] = ChainBlockH{w1, (const float*)n->arrays[a[17]], (const float*)n->arrays[a[19]], w2,
+                          (const float*)n->arrays[b[17]]};
       ch.flops_per_image += n->plans[i + 2 * k].flops_per_image + n->plans[i + 2 * k + 1].flops_per_image;
     }
     HIPCHK(n->ctx, hipMalloc(&ch.d_blk, hb.size() * sizeof(ChainBlockH)));
@@ -882,7 +912,10 @@ extern "C" int pc_net_destroy(pc_net* n) {
     if (st.slope) hipFree(st.slope);
   }
   if (n->stem_col) hipFree(n->stem_col);
-  for (auto& ch : n->chains) if (ch.d_blk) hipFree(ch.d_blk);
+  for (auto& ch : n->chains) {
+    if (ch.d_blk) hipFree(ch.d_blk);
+    if (ch.d_wpack) hipFree(ch.d_wpack);
+  }
   delete n;
   return PC_OK;
 }
@@ -921,8 +954,11 @@ static int run_ops(pc_net* n, int N) {
         }
       }
       const NetTensor &TX = n->tens[ch.in_t], &TY = n->tens[ch.out_t];
-      int dbg = 0;
-      if (const char* e = getenv("PC_CONV_DBG")) dbg = atoi(e);
+      int dbg = ch.wl << 8;
+      int mode = 1;   // LDS-DMA weight ring (measured faster than the register stream)
+      if (const char* e = getenv("PC_CHAIN_MODE")) mode = atoi(e) ? 1 : 0;
+      dbg |= mode << 10;
+      if (const char* e = getenv("PC_CONV_DBG")) dbg |= atoi(e) & 7;
       HIPCHK(c, conv_chain_launch(tensor_ptr(n, ch.in_t), TX.cs, tensor_ptr(n, ch.out_t), TY.cs, ch.d_blk, ch.nblk, N,
                                   TX.H, TX.W, n->ops[i].w[15], dbg, s));
       if (prof) {
@@ -1198,6 +1234,15 @@ extern "C" int pc_net_output(pc_net* n, int idx, void** d_ptr, int32_t* dims) {
   if (d_ptr) *d_ptr = tensor_ptr(n, t);
   if (dims) { dims[0] = T.H; dims[1] = T.W; dims[2] = T.C; dims[3] = T.cs; dims[4] = (T.is_f32 || n->f32) ? 1 : 0; }
   return PC_OK;
+}
+extern "C" int pc_net_chain_info(pc_net* n, int32_t* min_batch, int32_t* per_round) {
+  if (!n) return -PC_ERR_ARG;
+  int ncu = 256;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, n->ctx->device) != hipSuccess || ncu <= 0)
+    ncu = 256;
+  if (min_batch) *min_batch = n->chain_min_batch;
+  if (per_round) *per_round = ncu;
+  return (int)n->chains.size();
 }
 extern "C" int pc_net_stats(pc_net* n, double* flops, int32_t* launches) {
   if (!n) return PC_ERR_ARG;

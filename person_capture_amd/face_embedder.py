@@ -225,7 +225,8 @@ class FaceEmbedder(YoloFaceBranch):
         # for the host to fill a full batch. The quantum is the face count whose flip-TTA
         # images fill one round of the dominant 14x14x256 conv's 256x224 tiles over the CUs
         # (256 CUs x 224 px / 196 px per image / 2 images per face = 146); partial rounds
-        # cost a whole round of that layer. 0 = full batches only.
+        # cost a whole round of that layer. 0 = full batches only. (Resident block chains
+        # change the round: see below.)
         self._embed_quantum = int(os.getenv("PERSON_CAPTURE_AMD_EMBED_QUANTUM", "146"))
         # batched speculative fallback passes (TTA / edge pad / pre-scan rotations) per chunk
         self._fb_prefetch = os.getenv("PERSON_CAPTURE_AMD_FALLBACK_PREFETCH", "1") != "0"
@@ -245,6 +246,11 @@ class FaceEmbedder(YoloFaceBranch):
                                   max_batch=self._arc_batch)
         self._arc_feat_dim = self._arc.dim
         self._arc_fixed_batch = False
+        # with resident block chains (one image per CU through the 14x14x256 stage) a round
+        # is one image per CU: 128 flip-TTA faces on 256 CUs
+        nch, _, per_round = self._arc.net.chain_info()
+        if nch > 0 and "PERSON_CAPTURE_AMD_EMBED_QUANTUM" not in os.environ:
+            self._embed_quantum = max(1, per_round // 2)
         # --- SCRFD probe controls (face_embedder.py:473-476) ---
         self.scrfd_tta_scales = (0.75, 0.60)
         self.scrfd_probe_conf_cap = 0.20

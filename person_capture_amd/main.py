@@ -65,6 +65,21 @@ def _write_crop(path: str, bgr: np.ndarray) -> None:
     Image.fromarray(np.ascontiguousarray(bgr[..., ::-1])).save(path, quality=95)
 
 
+def _write_annot(path: str, frame: np.ndarray, person, expanded, face_box, score, fd, rd) -> None:
+    """Annotated frame as main.py:332-345 draws it (person box green, expanded crop box
+    blue, face box red in BGR terms; score text) - PIL stands in for cv2 (absent here)."""
+    from PIL import Image, ImageDraw
+    img = Image.fromarray(np.ascontiguousarray(frame[..., ::-1]))
+    d = ImageDraw.Draw(img)
+    d.rectangle(person, outline=(0, 255, 0), width=2)
+    d.rectangle(expanded, outline=(0, 0, 255), width=2)
+    if face_box is not None:
+        d.rectangle(face_box, outline=(255, 0, 0), width=2)
+    d.text((15, 15), f"score={score:.3f} fd={fd if fd is not None else -1:.3f} rd={rd if rd is not None else -1:.3f}",
+           fill=(255, 255, 255))
+    img.save(path, quality=95)
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument('--video', required=True, help='path to video file')
@@ -84,7 +99,10 @@ def main(argv=None) -> int:
 
     ensure_dir(args.out)
     crops_dir = os.path.join(args.out, 'crops')
+    ann_dir = os.path.join(args.out, 'annot') if args.save_annot else None
     ensure_dir(crops_dir)
+    if ann_dir:
+        ensure_dir(ann_dir)
     det = PersonDetector(model_name=args.yolo, device=args.device)
     face = FaceEmbedder(ctx=args.device)
     reid = ReIDEmbedder(device=args.device)
@@ -179,6 +197,13 @@ def main(argv=None) -> int:
                 crop_img_path = os.path.join(crops_dir, f"f{frame_idx:08d}.jpg")
                 _write_crop(crop_img_path, crop)
                 hit_count += 1
+                if ann_dir:
+                    fbox = None
+                    if bf is not None:
+                        fb = bf['bbox']
+                        fbox = (x1 + int(fb[0]), y1 + int(fb[1]), x1 + int(fb[2]), y1 + int(fb[3]))
+                    _write_annot(os.path.join(ann_dir, f"f{frame_idx:08d}.jpg"), frame, (x1, y1, x2, y2),
+                                 (ex1, ey1, ex2, ey2), fbox, score, fd, rd)
                 writer.writerow(index_row(frame_idx, fps, score, fd, rd, (ex1, ey1, ex2, ey2),
                                           os.path.basename(crop_img_path)))
     print(f"Done. Hits: {hit_count}. Index: {csv_path}")

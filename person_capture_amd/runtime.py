@@ -228,6 +228,14 @@ class Net:
         except Exception:
             pass
 
+    def chain_info(self) -> Tuple[int, int, int]:
+        """(resident block chains, batch from which they run, images per round of workgroups)."""
+        mb, pr = C.c_int32(), C.c_int32()
+        k = self.ctx.lib.pc_net_chain_info(self.handle, C.byref(mb), C.byref(pr))
+        if k < 0:
+            check(-k, self.ctx.handle, "chain_info")
+        return k, mb.value, pr.value
+
     def set_graph(self, enable: bool) -> None:
         check(self.ctx.lib.pc_net_set_graph(self.handle, 1 if enable else 0), self.ctx.handle, "set_graph")
 

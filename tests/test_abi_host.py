@@ -117,3 +117,18 @@ def test_person_reid_ctor_errors_mirror_reference():
         ReIDEmbedder(device="cpu")
     with pytest.raises(RuntimeError):
         clip_cfg("RN50x64")
+
+
+def test_library_has_no_undefined_internal_symbols():
+    """Every kernel stub and internal function the library references is defined in it
+    (a template kernel whose host-side instantiation silently failed leaves an undefined
+    __device_stub__ symbol that only shows up as a dlopen error on the GPU box)."""
+    import shutil
+    import subprocess
+    from person_capture_amd._lib import LIB_PATH
+    nm = shutil.which("nm")
+    if nm is None:
+        pytest.skip("nm not available")
+    out = subprocess.run([nm, "-D", "--undefined-only", str(LIB_PATH)], capture_output=True, text=True).stdout
+    bad = [ln.split()[-1] for ln in out.splitlines() if "_ZN2pc" in ln]
+    assert not bad, bad

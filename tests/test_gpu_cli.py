@@ -22,7 +22,8 @@ def test_cli_c1_plumbing(gpu_ctx, monkeypatch, tmp_path):
     np.save(tmp_path / "ref.npy", ref)
     out = tmp_path / "out"
     rc = cli.main(["--video", "synthetic:10:640x360", "--ref", str(tmp_path / "ref.npy"), "--out", str(out),
-                   "--frame-stride", "1", "--face-thresh", "0.45", "--reid-thresh", "0.38", "--device", "cuda"])
+                   "--frame-stride", "1", "--face-thresh", "0.45", "--reid-thresh", "0.38", "--device", "cuda",
+                   "--save-annot"])
     assert rc == 0
     rows = list(csv.reader(open(out / "index.csv")))
     assert rows[0] == pm.INDEX_HEADER
@@ -33,6 +34,8 @@ def test_cli_c1_plumbing(gpu_ctx, monkeypatch, tmp_path):
         fi, x1, y1, x2, y2 = int(r[0]), int(r[5]), int(r[6]), int(r[7]), int(r[8])
         assert 0 <= fi < 10 and 0 <= x1 < x2 <= 640 and 0 <= y1 < y2 <= 360
         assert r[9] == f"f{fi:08d}.jpg" and r[9] in crops   # one file per frame, as main.py names them
+    # --save-annot: one annotated full frame per accepted hit (main.py:332-345)
+    assert sorted(os.listdir(out / "annot")) == crops
 
 
 def test_sharpness_device_downscale(gpu_ctx):
