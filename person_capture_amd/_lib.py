@@ -97,6 +97,7 @@ SIGNATURES = {
     "pc_net_num_outputs": ([_P], _I),
     "pc_net_stats": ([_P, C.POINTER(C.c_double), C.POINTER(C.c_int32)], _I),
     "pc_net_chain_info": ([_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32)], _I),
+    "pc_net_set_chain_min_batch": ([_P, C.c_int32], _I),
     "pc_net_set_graph": ([_P, _I], _I),
     "pc_net_profile": ([_P, _I], _I),
     "pc_net_profile_read": ([_P, C.POINTER(C.c_double)], _I),

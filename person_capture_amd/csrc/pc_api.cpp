@@ -1244,6 +1244,11 @@ extern "C" int pc_net_chain_info(pc_net* n, int32_t* min_batch, int32_t* per_rou
   if (per_round) *per_round = ncu;
   return (int)n->chains.size();
 }
+extern "C" int pc_net_set_chain_min_batch(pc_net* n, int32_t min_batch) {
+  if (!n) return -PC_ERR_ARG;
+  n->chain_min_batch = min_batch <= 0 ? (1 << 30) : min_batch;
+  return 0;
+}
 extern "C" int pc_net_stats(pc_net* n, double* flops, int32_t* launches) {
   if (!n) return PC_ERR_ARG;
   if (flops) *flops = n->flops_per_image;

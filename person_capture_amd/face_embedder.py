@@ -82,8 +82,8 @@ def get_context(device_index: int, role: str = "") -> GpuContext:
     return c
 
 
-def _precision() -> int:
-    v = os.getenv("PERSON_CAPTURE_AMD_PRECISION", "f16").strip().lower()
+def _precision(var: str = "PERSON_CAPTURE_AMD_PRECISION") -> int:
+    v = os.getenv(var, os.getenv("PERSON_CAPTURE_AMD_PRECISION", "f16")).strip().lower()
     return PC_PREC_F32 if v in ("f32", "fp32", "float32") else PC_PREC_F16
 
 
@@ -175,6 +175,9 @@ class FaceEmbedder(YoloFaceBranch):
         self.det = None
         self.insight_app = None
         self.precision = _precision()
+        # detector precision (default: the embedder's): SCRFD f32 + ArcFace f16 gives the f32
+        # chips (the f16 landmarks move noise-frame chips, bench.py f16_parity attribution)
+        self.det_precision = _precision("PERSON_CAPTURE_AMD_DET_PRECISION")
         self._ctx = get_context(self._device_index)
         self._scrfd_ctx_id = self._device_index
         seed = int(os.getenv("PERSON_CAPTURE_AMD_SEED", "0"))
@@ -246,10 +249,14 @@ class FaceEmbedder(YoloFaceBranch):
                                   max_batch=self._arc_batch)
         self._arc_feat_dim = self._arc.dim
         self._arc_fixed_batch = False
-        # with resident block chains (one image per CU through the 14x14x256 stage) a round
-        # is one image per CU: 128 flip-TTA faces on 256 CUs
-        nch, _, per_round = self._arc.net.chain_info()
-        if nch > 0 and "PERSON_CAPTURE_AMD_EMBED_QUANTUM" not in os.environ:
+        # resident block chains (one image per CU through the 14x14x256 stage) need whole CUs:
+        # beside the detection stream they lose to the per-conv kernels (measured C3 r03: 1705
+        # vs 1925 frames/s), so they run only when ArcFace has the device to itself. A chain
+        # round is one image per CU: 128 flip-TTA faces on 256 CUs.
+        if two and os.getenv("PERSON_CAPTURE_AMD_CHAIN", "auto") == "auto":
+            self._arc.net.set_chain_min_batch(0)
+        nch, min_b, per_round = self._arc.net.chain_info()
+        if nch > 0 and min_b < (1 << 30) and "PERSON_CAPTURE_AMD_EMBED_QUANTUM" not in os.environ:
             self._embed_quantum = max(1, per_round // 2)
         # --- SCRFD probe controls (face_embedder.py:473-476) ---
         self.scrfd_tta_scales = (0.75, 0.60)
@@ -336,7 +343,7 @@ class FaceEmbedder(YoloFaceBranch):
             # heavy fallback sizes (up to 2048) run on single frames: keep their activation
             # buffers at the footprint of a det_batch x 640 engine
             mb = max(1, min(self._det_batch, self._det_batch * 640 * 640 // (D * D)))
-            e = ScrfdEngine(self._ctx, self._scrfd_params, self.scrfd_variant, D=D, precision=self.precision,
+            e = ScrfdEngine(self._ctx, self._scrfd_params, self.scrfd_variant, D=D, precision=self.det_precision,
                             max_batch=mb, max_det=1024)
             self._scrfd_engines[D] = e
         return e

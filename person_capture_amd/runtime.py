@@ -236,6 +236,12 @@ class Net:
             check(-k, self.ctx.handle, "chain_info")
         return k, mb.value, pr.value
 
+    def set_chain_min_batch(self, min_batch: int) -> None:
+        """Batch from which the resident block chains run (<= 0: never)."""
+        k = self.ctx.lib.pc_net_set_chain_min_batch(self.handle, int(min_batch))
+        if k < 0:
+            check(-k, self.ctx.handle, "set_chain_min_batch")
+
     def set_graph(self, enable: bool) -> None:
         check(self.ctx.lib.pc_net_set_graph(self.handle, 1 if enable else 0), self.ctx.handle, "set_graph")
 

@@ -15,7 +15,11 @@ crops in order) -> ReID tower on the same crop views.
   chip, oracle embedding of it within 1e-4), as tests/test_gpu_bench_config.py does for C3.
 * ReID: unit embeddings of every crop within 1e-4 of oracle/nets_torch.clip_vit_forward
   (ViT-L/14 width at depth 2, the reduced tower tests/test_gpu_reid.py pins).
-SCRFD-2.5G + IResNet-50 and 2 frames keep the CPU oracle within seconds per crop.
+* bank match: every face's device fd (DeviceBank, a 64-row bank with 16 planted
+  row) equals oracle/ref_algos.fd_min of its device feature within 1e-5.
+test_c4_composed_f32: SCRFD-2.5G + IResNet-50 + ViT-L/14 at depth 2 over 2 frames (the CPU
+oracle within seconds per crop). test_c4_full_nets_f32: the configured networks, SCRFD-10G +
+IResNet-100 + the full 24-layer ViT-L/14, on the first person crops of one frame.
 """
 import numpy as np
 import pytest
@@ -28,6 +32,7 @@ from oracle import pipeline as op
 from oracle import ref_algos as ra
 from person_capture_amd import face_embedder as fe_mod
 from person_capture_amd.detectors import PersonDetector
+from person_capture_amd.match import DeviceBank
 from person_capture_amd.reid_embedder import ReIDEmbedder, clip_weights
 
 pytestmark = pytest.mark.gpu
@@ -57,19 +62,31 @@ def _embed(o, chip):
 
 
 def test_c4_composed_f32(gpu_ctx, monkeypatch):
-    monkeypatch.setenv("PERSON_CAPTURE_AMD_PRECISION", "f32")
     monkeypatch.setenv("PERSON_CAPTURE_AMD_ARCFACE", "iresnet50")
-    frames = bench.synth_frames(0, NFRAMES)
+    _c4(monkeypatch, "2.5g", 50, "ViT-L-14-d2", NFRAMES, MAX_CROPS)
+
+
+@pytest.mark.timeout(900)
+def test_c4_full_nets_f32(gpu_ctx, monkeypatch):
+    monkeypatch.delenv("PERSON_CAPTURE_AMD_ARCFACE", raising=False)
+    _c4(monkeypatch, "10g", 100, "ViT-L-14", 1, 2)
+
+
+def _c4(monkeypatch, variant, depth, vit, nframes, max_crops):
+    monkeypatch.setenv("PERSON_CAPTURE_AMD_PRECISION", "f32")
+    monkeypatch.setenv("PERSON_CAPTURE_AMD_REID_PRECISION", "f32")
+    frames = bench.synth_frames(0, nframes)
     H, W = frames.shape[1:3]
     det = PersonDetector("yolov8n.pt", device="cuda:0")
-    fe = fe_mod.FaceEmbedder(ctx="cuda:0", yolo_model="scrfd_2.5g_bnkps", conf=FACE_CONF)
+    fe = fe_mod.FaceEmbedder(ctx="cuda:0", yolo_model=f"scrfd_{variant}_bnkps", conf=FACE_CONF)
+    assert fe._arc_depth == depth and fe.scrfd_variant == variant
     fe.debug_chips = True
-    reid = ReIDEmbedder(device="cuda:0", model_name="ViT-L-14-d2")
+    reid = ReIDEmbedder(device="cuda:0", model_name=vit)
     ctx = fe._ctx
     d = ctx.alloc(frames.nbytes)
     ctx.upload(frames, d)
     fsz = frames[0].nbytes
-    devs = [fe_mod._DevImage(d.ptr + i * fsz, H, W, W * 3) for i in range(NFRAMES)]
+    devs = [fe_mod._DevImage(d.ptr + i * fsz, H, W, W * 3) for i in range(nframes)]
 
     # ---- persons ----
     persons = det.detect_device([(x.ptr, H, W, W * 3) for x in devs], conf=0.35)
@@ -93,15 +110,22 @@ def test_c4_composed_f32(gpu_ctx, monkeypatch):
             x1, y1, x2, y2 = gi
             if x2 <= x1 + 2 or y2 <= y1 + 2:
                 continue
-            if len(crops) < MAX_CROPS:
+            if len(crops) < max_crops:
                 crops.append(frame[y1:y2, x1:x2])
                 views.append(fe_mod._DevImage(devs[fi].ptr + y1 * W * 3 + x1 * 3, y2 - y1, x2 - x1, W * 3))
-    assert n_boxes >= 2 and len(crops) >= 2
+    assert len(crops) >= 2
     print(f"{n_boxes} persons, {len(crops)} crops", flush=True)
 
     # ---- faces per person crop (one policy instance, crops in order) ----
+    bank_h = bench.synth_bank(64)
     got = fe.extract_batch([None] * len(views), dev_frames=views)
-    o = op.OracleFaceEmbedder(fe._scrfd_params, "2.5g", fe._arc_params, 50, conf=FACE_CONF, rot_phase=id(fe) & 7)
+    bench.plant_bank(got, bank_h)
+    fe2 = fe_mod.FaceEmbedder(ctx="cuda:0", yolo_model=f"scrfd_{variant}_bnkps", conf=FACE_CONF)
+    fe2.debug_chips = True
+    got = fe2.extract_batch([None] * len(views), dev_frames=views, bank=DeviceBank(fe2._ctx, bank_h))
+    fe = fe2
+    o = op.OracleFaceEmbedder(fe._scrfd_params, variant, fe._arc_params, depth, conf=FACE_CONF,
+                              rot_phase=id(fe) & 7)
     n_exact = n_chained = 0
     for ci, (crop, g) in enumerate(zip(crops, got)):
         r = o.extract(crop)
@@ -111,6 +135,7 @@ def test_c4_composed_f32(gpu_ctx, monkeypatch):
         rs = sorted(r, key=lambda f: tuple(f["bbox"]))
         for a, b in zip(gs, rs):
             assert np.array_equal(a["bbox"], b["bbox"]), (ci, a["bbox"], b["bbox"])
+            assert abs(a["fd"] - ra.fd_min(a["feat"], bank_h)) < 1e-5, ci
             if np.array_equal(a["chip"], b["chip"]):
                 assert np.abs(a["feat"] - b["feat"]).max() < TOL, ci
                 assert abs(a["quality"] - b["quality"]) <= 1e-9 * max(1.0, b["quality"])
@@ -128,8 +153,7 @@ def test_c4_composed_f32(gpu_ctx, monkeypatch):
     # ---- ReID of the same crop views ----
     feats = reid.extract_device([(v.ptr, v.H, v.W, v.stride) for v in views])
     xr = torch.stack([nt.clip_preprocess_pil(c) for c in crops])
-    ref = torch.nn.functional.normalize(nt.clip_vit_forward(clip_weights("ViT-L-14-d2", 0), "ViT-L-14-d2", xr),
-                                        dim=1).numpy()
+    ref = torch.nn.functional.normalize(nt.clip_vit_forward(clip_weights(vit, 0), vit, xr), dim=1).numpy()
     assert np.abs(feats - ref).max() < TOL
-    print(f"C4 composed f32: {n_boxes} persons in {NFRAMES} frames, {len(crops)} crops, "
+    print(f"C4 composed f32 ({variant}, r{depth}, {vit}): {n_boxes} persons in {nframes} frames, {len(crops)} crops, "
           f"{n_exact} faces exact + {n_chained} chained, ReID max |d| {np.abs(feats - ref).max():.2e}")
