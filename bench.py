@@ -280,6 +280,10 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-parity", action="store_true", help="skip the f16-vs-f32 decision parity pass")
     ap.add_argument("--precision", default="f16", choices=["f16", "f32"])
+    ap.add_argument("--frames", default="resident", choices=["resident", "host", "per-frame"],
+                    help="C3 frame source: resident in HBM (the headline), host arrays through extract_batch "
+                         "(H2D inside the timed region), or one extract() per host frame")
+    ap.add_argument("--det-size", type=int, default=640, help="C3 --frames per-frame: extract(imgsz=...)")
     ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c4", "c5"],
                     help="c3: BASELINE configs[2] (the metric's config, default); c2: ArcFace-R100 embed only at "
                          "batch 256 (the north star's MFMA target); c4: full path with YOLOv8n "
@@ -311,7 +315,7 @@ def main():
     os.environ.setdefault("PERSON_CAPTURE_AMD_ARC_BATCH", "512")
     from person_capture_amd._lib import PC_PREC_F32
     from person_capture_amd.face_embedder import FaceEmbedder, _DevImage
-    from person_capture_amd.match import DeviceBank
+    from person_capture_amd.match import DeviceBank, fd_min
 
     fe = FaceEmbedder(ctx=f"cuda:{local}", yolo_model="scrfd_10g_bnkps", conf=0.5)
     frames = synth_frames(rank, args.batch)
@@ -324,9 +328,23 @@ def main():
     bank = DeviceBank(ctx, bank_h)
     ctx.sync()
 
+    host_list = list(frames)
+
     def step():
-        res = fe.extract_batch([None] * args.batch, dev_frames=devs, bank=bank)
-        return res
+        if args.frames == "host":
+            # caller frames in pageable host memory: pinned staging + H2D inside the timed region
+            return fe.extract_batch(host_list, bank=bank)
+        if args.frames == "per-frame":
+            # an unchanged caller (main.py:246, gui_app.py:6045): extract() one host frame at a
+            # time, fd against the bank on the host as the reference's Processor does
+            out = []
+            for f in host_list:
+                faces = fe.extract(f, imgsz=args.det_size)
+                for fc in faces:
+                    fc["fd"] = fd_min(fc["feat"], bank_h)
+                out.append(faces)
+            return out
+        return fe.extract_batch([None] * args.batch, dev_frames=devs, bank=bank)
 
     res = step()
     # plant a quarter of the bank with embeddings of faces the pipeline finds in these frames
@@ -388,7 +406,11 @@ def main():
         "data": "synthetic (seeded u8 1080p frames, seeded synthetic SCRFD-10G/IResNet-100 weights)",
         "config": {"workload": "C3: SCRFD-10G detect + ArcFace-R100 embed (flip-TTA) + cosine match vs "
                                f"{args.bank}-embedding bank, 1080p, batch {args.batch} frames per GPU",
-                   "frames_per_step_per_gpu": args.batch, "det_size": 640, "bank": args.bank,
+                   "frames_per_step_per_gpu": args.batch, "det_size": args.det_size, "bank": args.bank,
+                   "frames": {"resident": "resident in HBM before the timed region",
+                              "host": "pageable host arrays, extract_batch: pinned staging + H2D timed",
+                              "per-frame": "pageable host arrays, one extract() per frame (unchanged callers), "
+                                           "host fd"}[args.frames],
                    "faces_per_frame": round(nfaces / args.batch, 3), "accepted_faces_per_step": accept,
                    "accepted_faces_per_step_cli_0.32": accept_cli, "bank_planted_rows": n_plant,
                    "detector_dtype": "f32" if fe.det_precision == PC_PREC_F32 else "f16",
@@ -418,8 +440,36 @@ def main():
                      "dominant_kernel_rocprof": dominant},
         "cpu_baseline": None,
     }
-    if rank == 0 and args.precision == "f16" and not args.no_parity:
+    if rank == 0 and args.precision == "f16" and not args.no_parity and args.frames == "resident":
         out["parity"] = f16_parity(fe, devs, bank_h)
+        # the same pipeline with the detector in f32 (PERSON_CAPTURE_AMD_DET_PRECISION=f32): f32
+        # landmarks give the f32 chips; its throughput and decisions, measured here too
+        old_dp = os.environ.get("PERSON_CAPTURE_AMD_DET_PRECISION")
+        os.environ["PERSON_CAPTURE_AMD_DET_PRECISION"] = "f32"
+        try:
+            fe_d = FaceEmbedder(ctx=f"cuda:{local}", yolo_model="scrfd_10g_bnkps", conf=0.5)
+        finally:
+            if old_dp is None:
+                os.environ.pop("PERSON_CAPTURE_AMD_DET_PRECISION", None)
+            else:
+                os.environ["PERSON_CAPTURE_AMD_DET_PRECISION"] = old_dp
+        run_d = lambda: fe_d.extract_batch([None] * args.batch, dev_frames=devs, bank=bank)
+        run_d()
+        fe_d._ctx.sync()
+        t0 = time.perf_counter()
+        for _ in range(3):
+            run_d()
+        fe_d._ctx.sync()
+        fe_d._ectx.sync()
+        fps_d = 3 * args.batch / (time.perf_counter() - t0)
+        pd = f16_parity(fe_d, devs, bank_h)
+        out["parity"]["detector_f32_mode"] = {
+            "frames_per_s": round(fps_d, 2), "steps": 3,
+            **{k: pd[k] for k in ("face_count_mismatch", "box_mismatch", "accept_mismatch_0.32",
+                                  "accept_mismatch_0.45", "accept_mismatch_frac_0.32", "max_fd_diff")},
+            "chips_identical": pd["attribution"]["chips_identical"],
+            "note": "SCRFD f32 + ArcFace f16 (env PERSON_CAPTURE_AMD_DET_PRECISION=f32): identical chips, the "
+                    "remaining flips are the f16 ArcFace's"}
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(frames, fe, bank_h, args.cpu_sample, args.cpu_sample_1t)
     if rank == 0:
@@ -572,6 +622,7 @@ def main_other(args):
         # trained detector would. Real weights need no such knob.
         fe.conf = 0.75
         reid = ReIDEmbedder(device=f"cuda:{local}")
+        stats["reid_dtype"] = "f32" if reid._engine.net.precision == 1 else "f16"
         dtuples = [(d.ptr, H, W, W * 3) for d in devs]
 
         def step():

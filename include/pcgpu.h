@@ -154,6 +154,15 @@ int pc_ctx_set_priority(pc_ctx* ctx, int priority);
 int pc_ctx_sync(pc_ctx* ctx);
 int pc_device_alloc(pc_ctx* ctx, size_t bytes, void** d_out);
 int pc_device_free(pc_ctx* ctx, void* d_ptr);
+/* stream-ordered wait: work enqueued on ctx after this call waits for fence f (recorded on any
+ * context of the same device). */
+int pc_ctx_wait_fence(pc_ctx* ctx, void* f);
+/* host frame staging (replaces the per-frame pageable upload of the reference's frame feed,
+ * video_io.py:1093-1135 -> FaceEmbedder.extract): rows of row_bytes, src_stride apart, packed
+ * by up to `threads` host threads into a ring of 4 pinned slots, then one async H2D on the
+ * context stream. The host array may be reused when this returns. */
+int pc_frame_stage(pc_ctx* ctx, void* d_dst, const void* h_src, size_t row_bytes, size_t rows, size_t src_stride,
+                   int threads);
 int pc_copy_h2d(pc_ctx* ctx, void* d_dst, const void* h_src, size_t bytes); /* stream-ordered */
 int pc_copy_d2h(pc_ctx* ctx, void* h_dst, const void* d_src, size_t bytes); /* stream-ordered */
 int pc_copy_d2d(pc_ctx* ctx, void* d_dst, const void* d_src, size_t bytes);

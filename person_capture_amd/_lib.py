@@ -96,6 +96,8 @@ SIGNATURES = {
     "pc_net_output": ([_P, _I, C.POINTER(_P), C.POINTER(C.c_int32)], _I),
     "pc_net_num_outputs": ([_P], _I),
     "pc_net_stats": ([_P, C.POINTER(C.c_double), C.POINTER(C.c_int32)], _I),
+    "pc_ctx_wait_fence": ([_P, _P], _I),
+    "pc_frame_stage": ([_P, _P, _P, C.c_size_t, C.c_size_t, C.c_size_t, C.c_int], _I),
     "pc_net_chain_info": ([_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32)], _I),
     "pc_net_set_chain_min_batch": ([_P, C.c_int32], _I),
     "pc_net_set_graph": ([_P, _I], _I),

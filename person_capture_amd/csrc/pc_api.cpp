@@ -14,6 +14,7 @@
 #include <vector>
 #include <map>
 #include <algorithm>
+#include <thread>
 #include "../../include/pcgpu.h"
 #include "pc_common.h"
 
@@ -159,6 +160,11 @@ struct pc_ctx {
   // CLIP preprocessing tables + horizontal-pass scratch
   void* clip_tmp = nullptr;
   size_t clip_tmp_bytes = 0;
+  // host frame staging (pc_frame_stage): ring of pinned slots, each reused once the H2D
+  // that last read it has completed
+  struct FrameSlot { char* h = nullptr; size_t cap = 0; hipEvent_t ev = nullptr; bool pending = false; };
+  FrameSlot fslots[4];
+  int fslot_next = 0;
 };
 
 static int fail(pc_ctx* c, int code, const std::string& msg) {
@@ -241,6 +247,10 @@ extern "C" int pc_ctx_destroy(pc_ctx* c) {
   if (c->ybig) hipFree(c->ybig);
   if (c->ycount) hipFree(c->ycount);
   if (c->clip_tmp) hipFree(c->clip_tmp);
+  for (auto& fs : c->fslots) {
+    if (fs.h) hipHostFree(fs.h);
+    if (fs.ev) hipEventDestroy(fs.ev);
+  }
   if (c->own_stream) hipStreamDestroy(c->own_stream);
   delete c;
   return PC_OK;
@@ -321,6 +331,64 @@ extern "C" int pc_fence_destroy(pc_ctx* c, void* f) {
   if (f) HIPCHK(c, hipEventDestroy((hipEvent_t)f));
   return PC_OK;
 }
+extern "C" int pc_ctx_wait_fence(pc_ctx* c, void* f) {
+  if (!c || !f) return PC_ERR_ARG;
+  HIPCHK(c, hipStreamWaitEvent(c->stream, (hipEvent_t)f, 0));
+  return PC_OK;
+}
+
+// Host frame -> device through the context's ring of pinned slots: the rows (row_bytes each,
+// src_stride apart: a numpy slice need not be contiguous) are packed into the slot by up to
+// `threads` host threads, then one H2D from the slot is enqueued on the context stream. The
+// caller's array is free again when this returns; the device copy completes in stream order.
+// A pageable hipMemcpyAsync would stage through the runtime's own bounce buffers in
+// ~MB-sized pieces with the calling thread blocked for the whole transfer.
+extern "C" int pc_frame_stage(pc_ctx* c, void* d_dst, const void* h_src, size_t row_bytes, size_t rows,
+                              size_t src_stride, int threads) {
+  if (!c || !d_dst || !h_src || src_stride < row_bytes) return PC_ERR_ARG;
+  const size_t n = row_bytes * rows;
+  if (!n) return PC_OK;
+  auto& fs = c->fslots[c->fslot_next];
+  c->fslot_next = (c->fslot_next + 1) % 4;
+  if (fs.pending) HIPCHK(c, hipEventSynchronize(fs.ev));
+  fs.pending = false;
+  if (fs.cap < n) {
+    if (fs.h) hipHostFree(fs.h);
+    fs.h = nullptr;
+    fs.cap = 0;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipHostMalloc((void**)&fs.h, n, hipHostMallocDefault));
+    fs.cap = n;
+  }
+  if (!fs.ev) HIPCHK(c, hipEventCreateWithFlags(&fs.ev, hipEventDisableTiming));
+  const char* src = (const char*)h_src;
+  auto pack = [&](size_t r0, size_t r1) {
+    if (src_stride == row_bytes) {
+      memcpy(fs.h + r0 * row_bytes, src + r0 * row_bytes, (r1 - r0) * row_bytes);
+    } else {
+      for (size_t r = r0; r < r1; ++r) memcpy(fs.h + r * row_bytes, src + r * src_stride, row_bytes);
+    }
+  };
+  int nt = std::max(1, std::min(threads, 16));
+  if (n < (size_t(2) << 20)) nt = 1;   // below ~2 MB a thread start costs more than it saves
+  if (nt == 1) {
+    pack(0, rows);
+  } else {
+    std::vector<std::thread> pool;
+    const size_t per = (rows + nt - 1) / nt;
+    for (int t = 1; t < nt; ++t) {
+      const size_t r0 = std::min(rows, t * per), r1 = std::min(rows, (t + 1) * per);
+      if (r0 < r1) pool.emplace_back(pack, r0, r1);
+    }
+    pack(0, std::min(rows, per));
+    for (auto& th : pool) th.join();
+  }
+  HIPCHK(c, hipMemcpyAsync(d_dst, fs.h, n, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipEventRecord(fs.ev, c->stream));
+  fs.pending = true;
+  return PC_OK;
+}
+
 extern "C" int pc_copy_h2d(pc_ctx* c, void* d, const void* h, size_t n) {
   if (!c) return PC_ERR_ARG;
   if (n) HIPCHK(c, hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, c->stream));

@@ -245,6 +245,10 @@ class FaceEmbedder(YoloFaceBranch):
         # PERSON_CAPTURE_AMD_EMBED_STREAM=0: one stream.
         two = self.detector_backend == "scrfd" and os.getenv("PERSON_CAPTURE_AMD_EMBED_STREAM", "1") != "0"
         self._ectx = get_context(self._device_index, "embed") if two else self._ctx
+        # host frames (extract / extract_batch without dev_frames) reach the device through the
+        # native pinned staging ring on a copy stream of their own (pc_frame_stage)
+        self._h2d = get_context(self._device_index, "h2d")
+        self._stage_threads = int(os.getenv("PERSON_CAPTURE_AMD_STAGE_THREADS", "4"))
         self._arc = ArcFaceEngine(self._ectx, self._arc_params, self._arc_depth, precision=self.precision,
                                   max_batch=self._arc_batch)
         self._arc_feat_dim = self._arc.dim
@@ -349,12 +353,13 @@ class FaceEmbedder(YoloFaceBranch):
         return e
 
     def _upload(self, bgr: np.ndarray, key: str = "frame") -> _DevImage:
-        a = np.ascontiguousarray(bgr, dtype=np.uint8)
+        a = np.asarray(bgr)
         if a.ndim != 3 or a.shape[2] != 3:
             raise ValueError("expected an HxWx3 BGR uint8 image")
-        buf = self._ctx.scratch(key, a.nbytes)
-        self._ctx.upload(a, buf)
-        return _DevImage(buf.ptr, a.shape[0], a.shape[1], a.strides[0], buf)
+        buf = self._ctx.scratch(key, a.shape[0] * a.shape[1] * 3)
+        self._h2d.stage_frame(a, buf.ptr, self._stage_threads)
+        self._ctx.wait_fence(self._h2d.fence("h2d_up"))
+        return _DevImage(buf.ptr, a.shape[0], a.shape[1], a.shape[1] * 3, buf)
 
     def _detect_batch(self, imgs: Sequence[_DevImage], dyn: int, conf: float):
         eng = self._engine(int(dyn))
@@ -559,12 +564,20 @@ class FaceEmbedder(YoloFaceBranch):
                 out_y.append([] if im is None else self._extract_with_yolo(im, imgsz))
             return out_y
         imgs: List[Optional[_DevImage]] = []
+        host_src: Dict[int, np.ndarray] = {}   # host frames not yet staged (device buffers reserved)
         for i in range(n):
             if dev_frames is not None:
                 imgs.append(dev_frames[i])
             else:
                 f = frames[i]
-                imgs.append(None if f is None or f.size == 0 else self._upload(f, key=f"frame{i}"))
+                if f is None or f.size == 0:
+                    imgs.append(None)
+                    continue
+                if f.ndim != 3 or f.shape[2] != 3:
+                    raise ValueError("expected an HxWx3 BGR uint8 image")
+                buf = self._ctx.scratch(f"frame{i}", f.shape[0] * f.shape[1] * 3)
+                imgs.append(_DevImage(buf.ptr, f.shape[0], f.shape[1], f.shape[1] * 3, buf))
+                host_src[i] = f
         # speculative 0-degree pass for every frame at the det size implied by the current
         # state, enqueued chunk by chunk with its readback into pinned memory; the policy of
         # chunk c (host) then overlaps the device work of the later chunks, and ArcFace
@@ -590,6 +603,13 @@ class FaceEmbedder(YoloFaceBranch):
             nonlocal slot
             if ci >= len(chunks):
                 return
+            staged = [i for i in chunks[ci] if i in host_src]
+            if staged:
+                # host frames of this chunk: pinned staging + H2D on the copy stream, which the
+                # detection stream waits on; the copies of chunk c+1 overlap chunk c's detection
+                for i in staged:
+                    self._h2d.stage_frame(host_src.pop(i), imgs[i].ptr, self._stage_threads)
+                self._ctx.wait_fence(self._h2d.fence(f"h2d{ci % 4}"))
             by_dyn: Dict[int, List[int]] = {}
             for i in chunks[ci]:
                 if spec_dyn[i] is not None:

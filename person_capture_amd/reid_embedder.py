@@ -32,8 +32,11 @@ _WEIGHTS: Dict[Tuple[str, int], dict] = {}
 
 
 def _precision() -> int:
-    v = os.getenv("PERSON_CAPTURE_AMD_REID_PRECISION", os.getenv("PERSON_CAPTURE_AMD_PRECISION", "f16"))
-    return PC_PREC_F32 if v.strip().lower() in ("f32", "fp32", "float32") else PC_PREC_F16
+    """f32 by default: the reference runs encode_image in fp32 (reid_embedder.py:53-55) and
+    no TensorRT engine exists for it. PERSON_CAPTURE_AMD_REID_PRECISION=f16 opts into the
+    f16 tower (narrower than the reference: tests/test_gpu_reid.py bounds it)."""
+    v = os.getenv("PERSON_CAPTURE_AMD_REID_PRECISION", "f32")
+    return PC_PREC_F16 if v.strip().lower() in ("f16", "fp16", "float16", "half") else PC_PREC_F32
 
 
 def clip_weights(name: str, seed: int = 0) -> dict:

@@ -168,6 +168,20 @@ class GpuContext:
         self._keep.append(a)
         return dst
 
+    def stage_frame(self, img: np.ndarray, d_dst: int, threads: int = 4) -> None:
+        """Host image [H][W][C] u8 (row-strided views allowed) -> d_dst packed, through the
+        native pinned staging ring (pc_frame_stage); the array may be reused on return."""
+        if (img.ndim != 3 or img.dtype != np.uint8 or img.strides[2] != 1 or img.strides[1] != img.shape[2]
+                or img.strides[0] < img.shape[1] * img.shape[2]):
+            img = np.ascontiguousarray(img, dtype=np.uint8)
+        row = img.shape[1] * img.shape[2]
+        check(self.lib.pc_frame_stage(self.handle, C.c_void_p(int(d_dst)), C.c_void_p(img.ctypes.data), row,
+                                      img.shape[0], img.strides[0], int(threads)), self.handle, "frame_stage")
+
+    def wait_fence(self, fence: "Fence") -> None:
+        """Work enqueued on this context from now on waits for `fence` (another context's)."""
+        check(self.lib.pc_ctx_wait_fence(self.handle, fence.handle), self.handle, "wait_fence")
+
     def download(self, ptr: int, shape, dtype) -> np.ndarray:
         out = np.empty(shape, dtype=dtype)
         if out.nbytes:
