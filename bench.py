@@ -284,6 +284,9 @@ def main():
                     help="C3 frame source: resident in HBM (the headline), host arrays through extract_batch "
                          "(H2D inside the timed region), or one extract() per host frame")
     ap.add_argument("--det-size", type=int, default=640, help="C3 --frames per-frame: extract(imgsz=...)")
+    ap.add_argument("--face-conf", type=float, default=0.5,
+                    help="C3 SCRFD threshold (the synthetic SCRFD-10G fires on ~1000 anchors of a 1080p noise frame "
+                         "at D=1408 and 0.5; 0.75 gives a handful, as at D=640 and 0.5)")
     ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c4", "c5"],
                     help="c3: BASELINE configs[2] (the metric's config, default); c2: ArcFace-R100 embed only at "
                          "batch 256 (the north star's MFMA target); c4: full path with YOLOv8n "
@@ -317,7 +320,7 @@ def main():
     from person_capture_amd.face_embedder import FaceEmbedder, _DevImage
     from person_capture_amd.match import DeviceBank, fd_min
 
-    fe = FaceEmbedder(ctx=f"cuda:{local}", yolo_model="scrfd_10g_bnkps", conf=0.5)
+    fe = FaceEmbedder(ctx=f"cuda:{local}", yolo_model="scrfd_10g_bnkps", conf=args.face_conf)
     frames = synth_frames(rank, args.batch)
     ctx = fe._ctx
     dframes = ctx.alloc(frames.nbytes)
@@ -406,7 +409,7 @@ def main():
         "data": "synthetic (seeded u8 1080p frames, seeded synthetic SCRFD-10G/IResNet-100 weights)",
         "config": {"workload": "C3: SCRFD-10G detect + ArcFace-R100 embed (flip-TTA) + cosine match vs "
                                f"{args.bank}-embedding bank, 1080p, batch {args.batch} frames per GPU",
-                   "frames_per_step_per_gpu": args.batch, "det_size": args.det_size, "bank": args.bank,
+                   "frames_per_step_per_gpu": args.batch, "det_size": args.det_size, "face_conf": args.face_conf, "bank": args.bank,
                    "frames": {"resident": "resident in HBM before the timed region",
                               "host": "pageable host arrays, extract_batch: pinned staging + H2D timed",
                               "per-frame": "pageable host arrays, one extract() per frame (unchanged callers), "

@@ -436,7 +436,7 @@ struct StemPlan {
   float* bias = nullptr;    // [npad]
   float* slope = nullptr;   // [npad] or null
 };
-struct ProfRec { int a, b, kind; double flops; int op = -1; int code = -1; };
+struct ProfRec { int a, b, kind; double flops; int op = -1; int code = -1; int small = 0; };
 // A run of IResNet identity blocks executed by the resident chain kernel
 // (pc_conv_chain.hip): ops [first, first + 2*nblk) of the program.
 struct ChainBlockH { const void* w1; const float* b1; const float* s1; const void* w2; const float* b2; };
@@ -460,6 +460,8 @@ struct pc_net {
   std::vector<void*> arrays;  // device copies (conv weights in act dtype, others f32)
   std::vector<long long> array_count;
   std::vector<ConvPlan> plans;
+  std::vector<ConvPlan> plans_small;   // tiles for batches <= 2 * small_batch
+  int small_batch = 0;
   std::vector<StemPlan> stems;
   std::vector<ChainPlan> chains;
   std::vector<int> chain_at;      // op index -> chain id (first op of a chain) or -1
@@ -514,7 +516,7 @@ static unsigned tensor_zero_off(const pc_net* n, int t) {
 
 static const int kNumConvCfgs = 14;   // pc_conv.hip launch_rowb
 
-static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl) {
+static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_batch) {
   const int* w = op.w;
   const int out = w[1], nseg = w[2], npad = w[14];
   const int esz = n->f32 ? 4 : 2;
@@ -530,7 +532,7 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl) {
   static const int cfg_bp[kNumConvCfgs] = {128, 64, 256, 128, 128, 256, 128, 256, 128, 256, 512, 256, 512, 128};
   const NetTensor& Y = n->tens[out];
   const long long Mimg = (long long)Y.H * Y.W;
-  const long long M = Mimg * n->max_batch;
+  const long long M = Mimg * plan_batch;   // tile choice for this batch (overflow checks use max_batch)
   auto tiles = [&](int c) { return (M + cfg_bp[c] - 1) / cfg_bp[c] * (npad / cfg_bc[c]); };
   // Tile choice, from single-conv measurements on MI355X (tools/probe_conv.py,
   // DESIGN.md §3.1): 8-wave tiles with 64x64 or 128x64 per wave whenever the grid has
@@ -905,12 +907,18 @@ extern "C" int pc_net_create(pc_ctx* c, const void* prog, size_t nbytes, int pre
   n->host_arrays.assign(narr, nullptr);
   for (int i = 0; i < narr; ++i) n->host_arrays[i] = data + arr[i].first;
   n->plans.resize(n->ops.size());
+  n->small_batch = max_batch > 32 && !getenv("PC_NO_SMALL_PLANS") ? 16 : 0;
+  n->plans_small.resize(n->ops.size());
   n->stems.resize(n->ops.size());
   size_t part = 0, stem_col_bytes = 0;
   for (size_t i = 0; i < n->ops.size() && rc == PC_OK; ++i) {
     const NetOp& op = n->ops[i];
     if (op.w[0] == OP_CONV) {
-      rc = plan_conv(n, op, n->plans[i]);
+      rc = plan_conv(n, op, n->plans[i], max_batch);
+      if (rc) break;
+      // small batches (per-frame extract: one frame's faces, prescan samples) get their own
+      // tile choice: the max-batch tiles would leave most CUs idle
+      if (n->small_batch > 0) rc = plan_conv(n, op, n->plans_small[i], n->small_batch);
       if (rc) break;
       const ConvPlan& pl = n->plans[i];
       if (pl.splitk > 1) part = std::max(part, (size_t)((long long)pl.splitk * pl.M_per_image * max_batch * op.w[14] * 4));
@@ -1048,7 +1056,9 @@ static int run_ops(pc_net* n, int N) {
       }
     }
     if (w[0] == OP_CONV) {
-      const ConvPlan& pl = n->plans[i];
+      const bool small = N <= 2 * n->small_batch;
+      const ConvPlan& pl = small ? n->plans_small[i] : n->plans[i];
+      rec.small = small;
       ConvParams p;
       memset(&p, 0, sizeof(p));
       const NetTensor& Y = n->tens[w[1]];
@@ -1250,9 +1260,10 @@ extern "C" int pc_net_profile_ops(pc_net* n, double* out, int max_recs) {
     double* o = out + 6 * k++;
     const bool conv = r.op >= 0 && n->ops[r.op].w[0] == OP_CONV;
     o[0] = r.op; o[1] = r.kind; o[2] = ms; o[3] = r.flops;
-    o[4] = r.code >= 0 ? r.code : conv ? (n->plans[r.op].t2d >= 0 ? 200 + n->plans[r.op].t2d
-                  : n->plans[r.op].fast >= 0 ? 100 + n->plans[r.op].fast : n->plans[r.op].halo) : -1;
-    o[5] = conv ? n->plans[r.op].cfg : -1;
+    const ConvPlan* pl = conv ? (r.small ? &n->plans_small[r.op] : &n->plans[r.op]) : nullptr;
+    o[4] = r.code >= 0 ? r.code : conv ? (pl->t2d >= 0 ? 200 + pl->t2d : pl->fast >= 0 ? 100 + pl->fast : pl->halo)
+                                       : -1;
+    o[5] = conv ? pl->cfg : -1;
   }
   return k;
 }
