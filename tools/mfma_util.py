@@ -9,6 +9,11 @@ busy fraction of the 1024 SIMDs is MFMA_BUSY / (GRBM_GUI_ACTIVE / 8 x 256 x 4), 
 effective clock of a dispatch is GRBM_GUI_ACTIVE / 8 / its duration. MFMA_BUSY counts
 per-SIMD cycles: 16 per v_mfma_f32_16x16x32_f16, so MFMA_BUSY x 1024 FLOP/cycle is the
 FLOP count the counters saw (a check against the algorithmic FLOPs).
+
+Clock: the GRBM quotient reads high on dispatches shorter than ~0.3 ms (MI355X_MICROARCH.md,
+DVFS note: r02's 3.69 GHz readings), so the effective clock is capped at the 2.4 GHz maximum
+and, below 0.3 ms, the busy fraction is taken against the kernel wall time at that clock
+(MFMA_BUSY / (avg_ns x 2.4 x 1024 SIMDs): a lower bound of the true busy fraction).
 """
 import csv
 import glob
@@ -18,6 +23,7 @@ import sys
 from collections import defaultdict
 
 CUS = 256
+FMAX_GHZ = 2.4
 
 
 def main():
@@ -44,7 +50,7 @@ def main():
                 dur[r.get("Name", "")] = float(r.get("AverageNs", 0) or 0)
     res = {}
     for name, c in rows.items():
-        if not any(t in name for t in ("conv_fast", "conv_igemm", "conv_halo")):
+        if not any(t in name for t in ("conv_fast", "conv_igemm", "conv_halo", "conv_t2d", "conv_chain", "stem")):
             continue
         busy = sum(c.get("SQ_VALU_MFMA_BUSY_CYCLES", [])) / max(1, len(c.get("SQ_VALU_MFMA_BUSY_CYCLES", [])))
         gui = sum(c.get("GRBM_GUI_ACTIVE", [])) / max(1, len(c.get("GRBM_GUI_ACTIVE", [])))
@@ -56,15 +62,27 @@ def main():
         e["counted_tflop_per_dispatch"] = round(busy * 1024 / 1e12, 6)
         if name in dur and dur[name] > 0:
             e["avg_ns"] = dur[name]
-            e["effective_clock_ghz"] = round(gui / 8.0 / dur[name], 3)
+            q = gui / 8.0 / dur[name]
+            e["grbm_clock_quotient_ghz"] = round(q, 3)
+            e["effective_clock_ghz"] = round(min(q, FMAX_GHZ), 3)
+            if dur[name] < 3e5 or q > FMAX_GHZ:
+                # short dispatch: wall time at the maximum clock (lower bound of the busy fraction)
+                e["mfma_util_simd_busy"] = round(busy / (dur[name] * FMAX_GHZ * CUS * 4), 4)
+                e["clock_source"] = "wall time x 2.4 GHz (GRBM quotient unreliable below 0.3 ms)"
+            else:
+                e["clock_source"] = "GRBM_GUI_ACTIVE / 8"
             e["counted_tflops"] = round(busy * 1024 / dur[name] / 1e3, 1)
         res[name] = e
     # time-weighted total over the conv kernels that have durations
-    tb = tg = 0.0
+    tb = tc = 0.0
     for name, e in res.items():
+        if "avg_ns" not in e:
+            continue
+        clk = e["effective_clock_ghz"] if e["clock_source"].startswith("GRBM") else FMAX_GHZ
         tb += e["mfma_busy_cycles"] * e["dispatches"]
-        tg += e["grbm_gui_active"] * e["dispatches"]
-    summary = {"conv_mfma_util_simd_busy": round(tb / (tg / 8.0 * CUS * 4), 4) if tg else None,
+        tc += e["avg_ns"] * clk * CUS * 4 * e["dispatches"]
+    summary = {"conv_mfma_util_simd_busy": round(tb / tc, 4) if tc else None,
+               "note": "time-weighted over the kernels with durations; SIMD-cycles at the capped effective clock",
                "per_kernel": res}
     json.dump(summary, open(out, "w"), indent=1)
     print(json.dumps({"conv_mfma_util_simd_busy": summary["conv_mfma_util_simd_busy"]}))
