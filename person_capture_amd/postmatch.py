@@ -7,16 +7,21 @@ what main.py / gui_app.py run on an accepted person box before writing the crop.
   detect_black_borders                       utils.py:152-197 (gui_app.py:3360 autocrop)
   combine_scores                             main.py:127-144
   index_row / INDEX_HEADER                   main.py:207-209, 344-346 (index.csv format)
+  choose_best_ratio, head_proxy_box          gui_app.py:3147-3328, 1931-1962: the GUI's crop-ratio
+                                             scorer (area, placement, face-fraction templates, head
+                                             containment), SessionConfig defaults in CropScoreConfig
 
 BGR -> gray is OpenCV's fixed-point BT.601 (the same formula the device quality kernel uses).
 """
 from __future__ import annotations
 
+import math
+from dataclasses import dataclass
 from typing import Optional, Sequence, Tuple
 
 import numpy as np
 
-from .utils import parse_ratio
+from .utils import expand_box_to_ratio, parse_ratio
 
 INDEX_HEADER = ['frame', 'time_secs', 'score', 'face_dist', 'reid_dist', 'x1', 'y1', 'x2', 'y2', 'crop_path']
 
@@ -171,3 +176,158 @@ def index_row(frame_idx: int, fps: float, score, fd, rd, box, crop_name: str) ->
     t = frame_idx / fps
     return [frame_idx, f"{t:.3f}", f"{score:.4f}" if score is not None else "", f"{fd:.4f}" if fd is not None else "",
             f"{rd:.4f}" if rd is not None else "", box[0], box[1], box[2], box[3], crop_name]
+
+
+@dataclass
+class CropScoreConfig:
+    """The SessionConfig fields the crop-ratio scorer reads, with their defaults
+    (gui_app.py:431-492)."""
+    crop_face_side_margin_frac: float = 0.30
+    crop_top_headroom_max_frac: float = 0.15
+    tight_face_relax_thresh: float = 0.48
+    tight_face_relax_scale: float = 0.5
+    crop_bottom_min_face_heights: float = 1.5
+    crop_center_weight: float = 0.8
+    face_anchor_down_frac: float = 1.1
+    area_gamma: float = 0.60
+    crop_penalty_weight: float = 3.0
+    area_face_scale_weight: float = 0.70
+    face_target_close_min_frac: float = 0.10
+    face_target_upper: float = 0.20
+    w_upper: float = 1.00
+    face_target_cowboy: float = 0.08
+    w_cowboy: float = 0.70
+    face_target_body: float = 0.03
+    w_body: float = 0.50
+    face_target_close: float = 0.38
+    w_close: float = 1.10
+    face_target_tolerance: float = 0.04
+    lambda_facefrac: float = 2.0
+    square_pull_face_min: float = 0.16
+    square_pull_weight: float = 1.10
+    wide_face_min_frame_frac: float = 0.12
+    wide_face_aspect_limit: float = 1.05
+    wide_face_aspect_penalty_weight: float = 10.0
+    crop_head_side_pad_frac: float = 0.88
+    crop_head_top_pad_frac: float = 0.95
+    crop_head_bottom_pad_frac: float = 0.30
+
+
+def head_proxy_box(face_box, frame_w, frame_h, cfg: CropScoreConfig):
+    """gui_app.py:1931-1962: the face box padded to protect hair/forehead/chin (None if degenerate)."""
+    if face_box is None:
+        return None
+    try:
+        fx1, fy1, fx2, fy2 = [float(v) for v in face_box]
+    except (TypeError, ValueError):
+        return None
+    fw, fh = max(1.0, fx2 - fx1), max(1.0, fy2 - fy1)
+    side = max(0.0, float(cfg.crop_head_side_pad_frac)) * fw
+    hx1, hy1 = max(0.0, fx1 - side), max(0.0, fy1 - max(0.0, float(cfg.crop_head_top_pad_frac)) * fh)
+    hx2 = min(float(frame_w), fx2 + side)
+    hy2 = min(float(frame_h), fy2 + max(0.0, float(cfg.crop_head_bottom_pad_frac)) * fh)
+    if hx2 <= hx1 + 1.0 or hy2 <= hy1 + 1.0:
+        return None
+    return hx1, hy1, hx2, hy2
+
+
+def _placement_penalty(crop, face, cfg: CropScoreConfig) -> float:
+    """Side-margin deficit + excess headroom + missing torso + face off-centre (gui_app.py:3163-3191)."""
+    if face is None:
+        return 0.0
+    cx1, cy1, cx2, cy2 = crop
+    fx1, fy1, fx2, fy2 = face
+    cw, ch = max(1.0, cx2 - cx1), max(1.0, cy2 - cy1)
+    fw, fh = max(1.0, fx2 - fx1), max(1.0, fy2 - fy1)
+    left, right = max(0.0, fx1 - cx1), max(0.0, cx2 - fx2)
+    top, bottom = max(0.0, fy1 - cy1), max(0.0, cy2 - fy2)
+    side_def = max(0.0, float(cfg.crop_face_side_margin_frac) * fw - min(left, right)) / fw
+    head_def = max(0.0, top / ch - float(cfg.crop_top_headroom_max_frac))
+    relax = float(cfg.tight_face_relax_scale) if (fh / ch) >= float(cfg.tight_face_relax_thresh) else 1.0
+    bottom_def = max(0.0, float(cfg.crop_bottom_min_face_heights) * fh * relax - bottom) / fh
+    center_def = math.hypot((0.5 * (fx1 + fx2) - 0.5 * (cx1 + cx2)) / cw, (0.5 * (fy1 + fy2) - 0.5 * (cy1 + cy2)) / ch)
+    return side_def + head_def + bottom_def + float(cfg.crop_center_weight) * center_def
+
+
+def _huber(x: float, delta: float) -> float:
+    ax = abs(x)
+    return 0.5 * ax * ax if ax <= delta else delta * (ax - 0.5 * delta)
+
+
+def _containment_deficit(crop, protect, margin_px: float = 0.0) -> float:
+    """How far (in protect-box widths/heights) the crop cuts into the protected box (gui_app.py:3197-3207)."""
+    if protect is None:
+        return 0.0
+    cx1, cy1, cx2, cy2 = crop
+    px1, py1, px2, py2 = protect
+    m = max(0.0, float(margin_px))
+    dx = max(0.0, (cx1 + m) - px1) + max(0.0, px2 - (cx2 - m))
+    dy = max(0.0, (cy1 + m) - py1) + max(0.0, py2 - (cy2 - m))
+    return dx / max(1.0, px2 - px1) + dy / max(1.0, py2 - py1)
+
+
+def _ratio_score(det_box, rw, rh, frame_w, frame_h, anchor, face_box, head_box, cfg: CropScoreConfig):
+    """Score of one candidate ratio (lower wins) -> (score, expanded box, template loss)."""
+    x1, y1, x2, y2 = det_box
+    hb = 0.0
+    if face_box is not None:   # push the framing down by ~face_anchor_down_frac face heights
+        hb = -float(cfg.face_anchor_down_frac) * (max(1.0, face_box[3] - face_box[1]) / max(1.0, y2 - y1))
+    box = expand_box_to_ratio(x1, y1, x2, y2, rw, rh, frame_w, frame_h, anchor=anchor, head_bias=hb)
+    ex1, ey1, ex2, ey2 = box
+    area = max(1, (ex2 - ex1) * (ey2 - ey1))
+    area_term = pow(float(area) / float(max(1, (x2 - x1) * (y2 - y1))), float(cfg.area_gamma))
+    total = area_term + float(cfg.crop_penalty_weight) * _placement_penalty(box, face_box, cfg)
+    if head_box is not None:   # graded, very large: no candidate may cut the visible head
+        total += 1.0e6 * _containment_deficit(box, head_box, margin_px=1.0)
+    tmpl = 0.0
+    if face_box is not None:
+        fx1, fy1, fx2, fy2 = face_box
+        fw, fh = max(1.0, fx2 - fx1), max(1.0, fy2 - fy1)
+        face_frac = max(1.0, (fx2 - fx1) * (fy2 - fy1)) / max(1.0, float(area))
+        if min(max(0.0, fx1 - ex1), max(0.0, ex2 - fx2)) < float(cfg.crop_face_side_margin_frac) * fw:
+            total += 1e9   # hard side guard: this ratio would cut the face
+        face_scale = max(fw / max(1.0, frame_w), fh / max(1.0, frame_h))
+        total += (max(0.30, 1.0 - float(cfg.area_face_scale_weight) * face_scale) - 1.0) * area_term
+        targets = [(cfg.face_target_upper, cfg.w_upper), (cfg.face_target_cowboy, cfg.w_cowboy),
+                   (cfg.face_target_body, cfg.w_body)]
+        if face_scale >= float(cfg.face_target_close_min_frac):
+            targets.append((cfg.face_target_close, cfg.w_close))
+        delta = float(cfg.face_target_tolerance)
+        tmpl = min(float(w) * _huber(face_frac - float(t), delta) for t, w in targets)
+        total += float(cfg.lambda_facefrac) * tmpl
+        asp = float(rw) / float(rh)
+        if fh / max(1.0, frame_h) > float(cfg.square_pull_face_min):
+            total += float(cfg.square_pull_weight) * (fh / float(frame_h) - float(cfg.square_pull_face_min)) * \
+                abs(asp - 1.0)
+        wide_min = max(1e-6, float(cfg.wide_face_min_frame_frac))
+        wide_limit = max(1.0, float(cfg.wide_face_aspect_limit))
+        if face_scale >= wide_min and asp > wide_limit:
+            total += float(cfg.wide_face_aspect_penalty_weight) * min(4.0, face_scale / wide_min) * (asp - wide_limit)
+    return total, box, tmpl
+
+
+def choose_best_ratio(det_box, ratios: Sequence[str], frame_w, frame_h, anchor=None, face_box=None,
+                      cfg: Optional[CropScoreConfig] = None):
+    """Processor._choose_best_ratio (gui_app.py:3147-3328): expand det_box to every candidate
+    'W:H' ratio and keep the lowest score (first wins ties); unparsable ratios are skipped.
+    Returns (int box, ratio string or None, template loss of the winner)."""
+    cfg = cfg or CropScoreConfig()
+    head_box = head_proxy_box(face_box, frame_w, frame_h, cfg)
+    best, best_ratio, best_score, best_tmpl = None, None, 1e9, 0.0
+    for rs in ratios:
+        try:
+            rw, rh = parse_ratio(rs)
+        except (ValueError, AttributeError, TypeError):
+            continue
+        total, box, tmpl = _ratio_score(det_box, rw, rh, frame_w, frame_h, anchor, face_box, head_box, cfg)
+        if total < best_score:
+            best_score, best_ratio, best_tmpl = total, rs, tmpl
+            best = tuple(int(round(v)) for v in box)
+    if best is None:   # nothing scored below 1e9: the first ratio unbiased, else the detection itself
+        try:
+            rw, rh = parse_ratio(str(ratios[0]))
+            box = expand_box_to_ratio(*det_box, rw, rh, frame_w, frame_h, anchor=anchor, head_bias=0.0)
+            return tuple(int(round(v)) for v in box), str(ratios[0]), 0.0
+        except Exception:
+            return tuple(int(round(v)) for v in det_box), None, 0.0
+    return best, best_ratio, best_tmpl

@@ -287,6 +287,23 @@ class PrescanRunner:
         return spans, st.bank
 
 
+def run_cached(runner: "PrescanRunner", frame_at, video, refs="", cache_dir: str = "prescan_cache",
+               mode: str = "auto", settings=None):
+    """Processor._prescan's cache wrapper (gui_app.py:847-920 around the sampling loop): a hit
+    returns the stored spans and bank without touching a frame; a miss runs the loop and stores
+    its result. `settings`: the SessionConfig-like source of the key (default: the runner's
+    PrescanConfig, other keys at SessionConfig defaults). Returns (spans, bank, hit)."""
+    from . import prescan_cache as pcache
+    meta = pcache.cache_meta(settings if settings is not None else runner.cfg, video, refs, runner.fps, runner.total)
+    root = pcache.cache_root(cache_dir)
+    hit, spans, bank = pcache.load(root, meta, mode)
+    if hit:
+        return spans, bank, True
+    spans, bank = runner.run(frame_at)
+    pcache.save(root, meta, spans, bank, mode)
+    return spans, bank, False
+
+
 def prescan_sequential(face, cfg: PrescanConfig, fps: float, total_frames: int, frame_at, ref_feat=None):
     """The same loop one sample per extract (batch 1): the reference's own order, for tests."""
     r = PrescanRunner(face, cfg, fps, total_frames, ref_feat=ref_feat, batch=1)

@@ -1,0 +1,79 @@
+"""Crop-ratio chooser and pre-scan cache against goldens made by running the reference's own
+Processor methods (tools/gen_golden_r03.py: gui_app.py _choose_best_ratio 3147-3328 with
+_face_head_proxy_box 1931-1962; _prescan_cache_meta / _save_prescan_cache 787-920).
+CPU only."""
+import json
+import os
+
+import numpy as np
+
+from person_capture_amd import prescan_cache as pc
+from person_capture_amd.postmatch import CropScoreConfig, choose_best_ratio
+
+G = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def test_choose_best_ratio_matches_reference():
+    d = np.load(os.path.join(G, "choose_ratio.npz"), allow_pickle=False)
+    sets = json.loads(str(d["ratio_sets"]))
+    for i in range(len(d["set_idx"])):
+        rs = sets[int(d["set_idx"][i])]
+        fw, fh = (int(v) for v in d["frame"][i])
+        det = tuple(int(v) for v in d["det"][i])
+        anchor = None if np.isnan(d["anchor"][i][0]) else tuple(float(v) for v in d["anchor"][i])
+        face = None if np.isnan(d["face"][i][0]) else tuple(float(v) for v in d["face"][i])
+        box, ratio, tl = choose_best_ratio(det, rs, fw, fh, anchor=anchor, face_box=face, cfg=CropScoreConfig())
+        assert tuple(box) == tuple(int(v) for v in d["box"][i]), i
+        assert (-1 if ratio is None else rs.index(ratio)) == int(d["ratio_idx"][i]), i
+        assert tl == float(d["tmpl_loss"][i]), i
+
+
+def test_prescan_cache_keys_match_reference():
+    for case in json.load(open(os.path.join(G, "prescan_cache_keys.json"))):
+        settings = {k: tuple(v) if isinstance(v, list) else v for k, v in case["settings"].items()}
+        meta = pc.cache_meta(settings, case["video"], case["ref"], case["fps"], case["total_frames"])
+        assert meta == case["meta"]
+
+
+def test_prescan_cache_reads_reference_file_and_round_trips(tmp_path):
+    info = json.load(open(os.path.join(G, "prescan_cache_ref.json")))
+    meta = pc.cache_meta({}, info["video"], "", info["fps"], info["total_frames"])
+    assert meta["key"] == info["key"]
+    root = tmp_path / "cache"
+    root.mkdir()
+    ref_file = os.path.join(G, "prescan_cache_ref.npz")
+    (root / f"{meta['key']}.npz").write_bytes(open(ref_file, "rb").read())
+    hit, spans, bank = pc.load(root, meta)
+    assert hit and spans == [tuple(s) for s in info["spans"]] and bank.shape == (5, 512)
+    # our writer produces the same arrays; a different key or mode misses
+    out = pc.save(tmp_path / "mine", meta, spans, bank)
+    with np.load(out, allow_pickle=False) as a, np.load(ref_file, allow_pickle=False) as b:
+        assert sorted(a.files) == sorted(b.files)
+        for k in a.files:
+            assert np.array_equal(a[k], b[k]), k
+    other = pc.cache_meta({"prescan_stride": 12}, info["video"], "", info["fps"], info["total_frames"])
+    assert pc.load(root, other) == (False, [], None)
+    assert pc.load(root, meta, mode="refresh") == (False, [], None)
+    assert pc.save(tmp_path / "off", meta, spans, None, mode="off") is None
+    # no reference bank: has_ref 0 -> None back
+    pc.save(tmp_path / "nb", meta, spans, None)
+    assert pc.load(tmp_path / "nb", meta) == (True, spans, None)
+
+
+def test_run_cached_hit_skips_the_loop(tmp_path):
+    from person_capture_amd.prescan import PrescanConfig, run_cached
+
+    class Runner:
+        cfg, fps, total, calls = PrescanConfig(), 30.0, 600, 0
+
+        def run(self, frame_at):
+            self.calls += 1
+            return [(0, 99)], np.eye(2, 512, dtype=np.float32)
+
+    r = Runner()
+    a = run_cached(r, None, "/nonexistent/v.mp4", "", cache_dir=str(tmp_path))
+    b = run_cached(r, None, "/nonexistent/v.mp4", "", cache_dir=str(tmp_path))
+    assert r.calls == 1 and a[2] is False and b[2] is True
+    assert a[0] == b[0] and np.array_equal(a[1], b[1])
+    r.cfg = PrescanConfig(prescan_stride=12)   # another key: a miss
+    assert run_cached(r, None, "/nonexistent/v.mp4", "", cache_dir=str(tmp_path))[2] is False and r.calls == 2
