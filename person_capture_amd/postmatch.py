@@ -7,6 +7,7 @@ what main.py / gui_app.py run on an accepted person box before writing the crop.
   detect_black_borders                       utils.py:152-197 (gui_app.py:3360 autocrop)
   combine_scores                             main.py:127-144
   index_row / INDEX_HEADER                   main.py:207-209, 344-346 (index.csv format)
+  debug_record / DebugLog                    gui_app.py:8013-8057, 4459-4470: the per-frame debug.jsonl line
   choose_best_ratio, head_proxy_box          gui_app.py:3147-3328, 1931-1962: the GUI's crop-ratio
                                              scorer (area, placement, face-fraction templates, head
                                              containment), SessionConfig defaults in CropScoreConfig
@@ -331,3 +332,48 @@ def choose_best_ratio(det_box, ratios: Sequence[str], frame_w, frame_h, anchor=N
         except Exception:
             return tuple(int(round(v)) for v in det_box), None, 0.0
     return best, best_ratio, best_tmpl
+
+
+# (SessionConfig field, type) of the debug.jsonl "cfg" block in the reference's order (gui_app.py:8024-8044)
+DEBUG_CFG_FIELDS = (
+    ("face_det_conf", float), ("face_det_pad", float), ("face_thresh", float), ("reid_thresh", float),
+    ("face_quality_min", float), ("face_visible_uses_quality", bool), ("prefer_face_when_available", bool),
+    ("require_face_if_visible", bool), ("match_mode", str), ("allow_faceless_when_locked", bool),
+    ("faceless_reid_thresh", float), ("faceless_iou_min", float), ("faceless_persist_frames", int),
+    ("faceless_min_area_frac", float), ("faceless_max_area_frac", float), ("faceless_center_max_frac", float),
+    ("faceless_min_motion_frac", float), ("learn_bank_runtime", bool), ("drop_reid_if_any_face_match", bool),
+)
+
+
+def debug_record(frame: int, persons: int, faces_detected: int, faces_pass_quality: int, any_face_detected: bool,
+                 any_face_visible: bool, min_fd_all, best_face_dist, cfg, candidates) -> dict:
+    """One per-frame debug.jsonl object (gui_app.py:8013-8057). `cfg`: SessionConfig-like object or
+    mapping holding DEBUG_CFG_FIELDS; `candidates`: dicts with fd, rd (None allowed), sharp, box[, reasons]."""
+    get = (lambda k: cfg[k]) if isinstance(cfg, dict) else (lambda k: getattr(cfg, k))
+    opt = lambda v: float(v) if v is not None else None
+    return {
+        "frame": frame, "persons": int(persons), "faces_detected": int(faces_detected),
+        "faces_pass_quality": int(faces_pass_quality), "any_face_detected": bool(any_face_detected),
+        "any_face_visible": bool(any_face_visible), "min_fd_all": opt(min_fd_all), "best_face_dist": opt(best_face_dist),
+        "cfg": {k: t(get(k)) for k, t in DEBUG_CFG_FIELDS},
+        "candidates": [{"fd": opt(c["fd"]), "rd": opt(c["rd"]), "sharp": float(c["sharp"]),
+                        "box": [int(v) for v in c["box"]], "reasons": c.get("reasons", [])} for c in candidates],
+    }
+
+
+class DebugLog:
+    """<dbg_dir>/debug.jsonl: one JSON object per line, flushed per frame (gui_app.py:4459-4470)."""
+
+    def __init__(self, dbg_dir: str):
+        import os
+        os.makedirs(dbg_dir, exist_ok=True)
+        self.f = open(os.path.join(dbg_dir, "debug.jsonl"), "w", encoding="utf-8")
+
+    def write(self, obj: dict) -> None:
+        import json
+        json.dump(obj, self.f, ensure_ascii=False)
+        self.f.write("\n")
+        self.f.flush()
+
+    def close(self) -> None:
+        self.f.close()

@@ -77,3 +77,21 @@ def test_run_cached_hit_skips_the_loop(tmp_path):
     assert a[0] == b[0] and np.array_equal(a[1], b[1])
     r.cfg = PrescanConfig(prescan_stride=12)   # another key: a miss
     assert run_cached(r, None, "/nonexistent/v.mp4", "", cache_dir=str(tmp_path))[2] is False and r.calls == 2
+
+
+def test_debug_record_layout_matches_reference(tmp_path):
+    from person_capture_amd.postmatch import DEBUG_CFG_FIELDS, DebugLog, debug_record
+    lay = json.load(open(os.path.join(G, "debug_record_layout.json")))
+    assert [k for k, _ in DEBUG_CFG_FIELDS] == lay["cfg_keys"]
+    cands = [{"fd": 0.31, "rd": None, "sharp": 12.5, "box": (1.0, 2, 3, 4.0)},
+             {"fd": None, "rd": 0.2, "sharp": 3, "box": [5, 6, 7, 8], "reasons": ["faceless"]}]
+    rec = debug_record(7, 2, 3, 1, True, False, None, 0.31, lay["cfg_defaults"], cands)
+    assert list(rec) == lay["top_keys"] and list(rec["cfg"]) == lay["cfg_keys"]
+    assert rec["cfg"] == lay["cfg_defaults"]
+    assert all(list(c) == lay["candidate_keys"] for c in rec["candidates"])
+    log = DebugLog(str(tmp_path))
+    log.write(rec)
+    log.write(rec)
+    log.close()
+    lines = open(tmp_path / "debug.jsonl", encoding="utf-8").read().splitlines()
+    assert len(lines) == 2 and json.loads(lines[0]) == json.loads(json.dumps(rec))

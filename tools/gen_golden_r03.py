@@ -139,7 +139,20 @@ def main():
                   open(os.path.join(OUT, "prescan_cache_ref.json"), "w"))
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
-    print("wrote choose_ratio.npz, prescan_cache_keys.json, prescan_cache_ref.npz")
+    # ---- debug.jsonl record layout (key order of the dict literal at gui_app.py:8015-8055) ----
+    tree = ast.parse(open(os.path.join(REF, "person_capture", "gui_app.py"), encoding="utf-8").read())
+    lay = None
+    for node in ast.walk(tree):
+        if isinstance(node, ast.Dict) and any(isinstance(k, ast.Constant) and k.value == "faces_pass_quality"
+                                              for k in node.keys):
+            keys = [k.value for k in node.keys]
+            cfg_d = node.values[keys.index("cfg")]
+            cand = node.values[keys.index("candidates")].elt
+            lay = {"top_keys": keys, "cfg_keys": [k.value for k in cfg_d.keys],
+                   "candidate_keys": [k.value for k in cand.keys]}
+    lay["cfg_defaults"] = {k: getattr(cfg, k) for k in lay["cfg_keys"]}
+    json.dump(lay, open(os.path.join(OUT, "debug_record_layout.json"), "w"), indent=0)
+    print("wrote choose_ratio.npz, prescan_cache_keys.json, prescan_cache_ref.npz, debug_record_layout.json")
 
 
 if __name__ == "__main__":
