@@ -284,6 +284,8 @@ def main():
                     help="C3 frame source: resident in HBM (the headline), host arrays through extract_batch "
                          "(H2D inside the timed region), or one extract() per host frame")
     ap.add_argument("--det-size", type=int, default=640, help="C3 --frames per-frame: extract(imgsz=...)")
+    ap.add_argument("--face-model", default="scrfd_10g_bnkps",
+                    help="C3 FaceEmbedder detector (yolov8l-face.pt: the reference default an unchanged main.py gets)")
     ap.add_argument("--face-conf", type=float, default=0.5,
                     help="C3 SCRFD threshold (the synthetic SCRFD-10G fires on ~1000 anchors of a 1080p noise frame "
                          "at D=1408 and 0.5; 0.75 gives a handful, as at D=640 and 0.5)")
@@ -320,7 +322,7 @@ def main():
     from person_capture_amd.face_embedder import FaceEmbedder, _DevImage
     from person_capture_amd.match import DeviceBank, fd_min
 
-    fe = FaceEmbedder(ctx=f"cuda:{local}", yolo_model="scrfd_10g_bnkps", conf=args.face_conf)
+    fe = FaceEmbedder(ctx=f"cuda:{local}", yolo_model=args.face_model, conf=args.face_conf)
     frames = synth_frames(rank, args.batch)
     ctx = fe._ctx
     dframes = ctx.alloc(frames.nbytes)
@@ -364,7 +366,13 @@ def main():
     nfaces = sum(len(r) for r in res)
     accept = sum(1 for r in res for f in r if f["fd"] <= 0.45)
     accept_cli = sum(1 for r in res for f in r if f["fd"] <= 0.32)
-    nets = [fe._engine(640).net, fe._arc.net]
+    if fe.detector_backend == "yolo":
+        det_nets = [e.net for e in fe._yf_engines.values()]
+        net_names = tuple(f"yolo-face{k}" for k in range(len(det_nets))) + ("arcface",)
+    else:
+        det_nets = [e.net for e in fe._scrfd_engines.values()] if args.frames == "per-frame" else [fe._engine(640).net]
+        net_names = tuple("scrfd" if k == 0 else f"scrfd{k}" for k in range(len(det_nets))) + ("arcface",)
+    nets = det_nets + [fe._arc.net]
     if not os.getenv("PC_BENCH_NOPROF"):
         for n in nets:
             n.profile(True)
@@ -380,7 +388,7 @@ def main():
     _barrier(world)
     elapsed = _max_over_ranks(world, t1 - t0)
     prof = [n.profile_read() for n in nets]
-    dom = dominant_conv(nets, ("scrfd", "arcface"))
+    dom = dominant_conv(nets, net_names)
     for n in nets:
         n.profile(False)
     if fe.host_times is not None:
@@ -409,7 +417,7 @@ def main():
         "data": "synthetic (seeded u8 1080p frames, seeded synthetic SCRFD-10G/IResNet-100 weights)",
         "config": {"workload": "C3: SCRFD-10G detect + ArcFace-R100 embed (flip-TTA) + cosine match vs "
                                f"{args.bank}-embedding bank, 1080p, batch {args.batch} frames per GPU",
-                   "frames_per_step_per_gpu": args.batch, "det_size": args.det_size, "face_conf": args.face_conf, "bank": args.bank,
+                   "frames_per_step_per_gpu": args.batch, "det_size": args.det_size, "face_model": args.face_model, "face_conf": args.face_conf, "bank": args.bank,
                    "frames": {"resident": "resident in HBM before the timed region",
                               "host": "pageable host arrays, extract_batch: pinned staging + H2D timed",
                               "per-frame": "pageable host arrays, one extract() per frame (unchanged callers), "
@@ -436,14 +444,15 @@ def main():
                      "per_net": {name: {"conv_ms_per_step": round(p_["conv_ms"] / args.steps, 3),
                                         "tflops": round(p_["conv_flops"] / (p_["conv_ms"] * 1e-3) / 1e12, 1)
                                         if p_["conv_ms"] > 0 else None}
-                                 for name, p_ in zip(("scrfd", "arcface"), prof)},
+                                 for name, p_ in zip(net_names, prof)},
                      "traffic_unit": "HBM bytes per launch of the dominant kernel (rocprofv3 FETCH_SIZE x2 + "
                                      "WRITE_SIZE, bench_traffic.json); conv_family.traffic_mean_per_launch: the mean "
                                      "over all conv launches",
                      "dominant_kernel_rocprof": dominant},
         "cpu_baseline": None,
     }
-    if rank == 0 and args.precision == "f16" and not args.no_parity and args.frames == "resident":
+    if rank == 0 and args.precision == "f16" and not args.no_parity and args.frames == "resident" and \
+            fe.detector_backend == "scrfd":
         out["parity"] = f16_parity(fe, devs, bank_h)
         # the same pipeline with the detector in f32 (PERSON_CAPTURE_AMD_DET_PRECISION=f32): f32
         # landmarks give the f32 chips; its throughput and decisions, measured here too

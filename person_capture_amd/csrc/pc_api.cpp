@@ -460,7 +460,7 @@ struct pc_net {
   std::vector<void*> arrays;  // device copies (conv weights in act dtype, others f32)
   std::vector<long long> array_count;
   std::vector<ConvPlan> plans;
-  std::vector<ConvPlan> plans_small;   // tiles for batches <= 2 * small_batch
+  std::vector<ConvPlan> plans_small;   // tiles chosen for small_batch images, used for N <= 2 * small_batch
   int small_batch = 0;
   std::vector<StemPlan> stems;
   std::vector<ChainPlan> chains;
@@ -907,7 +907,7 @@ extern "C" int pc_net_create(pc_ctx* c, const void* prog, size_t nbytes, int pre
   n->host_arrays.assign(narr, nullptr);
   for (int i = 0; i < narr; ++i) n->host_arrays[i] = data + arr[i].first;
   n->plans.resize(n->ops.size());
-  n->small_batch = max_batch > 32 && !getenv("PC_NO_SMALL_PLANS") ? 16 : 0;
+  n->small_batch = max_batch > 2 && !getenv("PC_NO_SMALL_PLANS") ? std::max(1, std::min(16, max_batch / 4)) : 0;
   n->plans_small.resize(n->ops.size());
   n->stems.resize(n->ops.size());
   size_t part = 0, stem_col_bytes = 0;

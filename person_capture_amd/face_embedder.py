@@ -556,13 +556,13 @@ class FaceEmbedder(YoloFaceBranch):
         self._bank = bank
         self._fb_cache = {}
         n = len(frames) if dev_frames is None else len(dev_frames)
-        if self.detector_backend == "yolo":   # face_embedder.py:1671-2093, frame by frame
-            out_y: List[list] = []
-            for i in range(n):
-                im = dev_frames[i] if dev_frames is not None else (
-                    None if frames[i] is None or frames[i].size == 0 else self._upload(frames[i], key="yf_frame"))
-                out_y.append([] if im is None else self._extract_with_yolo(im, imgsz))
-            return out_y
+        if self.detector_backend == "yolo":   # face_embedder.py:1671-2093
+            if dev_frames is not None:
+                ims = list(dev_frames)
+            else:
+                ims = [None if f is None or f.size == 0 else self._upload(f, key=f"yf_frame{i}")
+                       for i, f in enumerate(frames)]
+            return self._extract_batch_yolo(ims, imgsz)
         imgs: List[Optional[_DevImage]] = []
         host_src: Dict[int, np.ndarray] = {}   # host frames not yet staged (device buffers reserved)
         for i in range(n):

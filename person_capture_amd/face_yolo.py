@@ -47,44 +47,60 @@ def check_imgsz(imgsz: int, stride: int = 32) -> int:
 
 
 class YoloFaceEngine:
-    """YOLOv8-face (Pose head) at one letterbox canvas Hp x Wp, one frame per call."""
+    """YOLOv8-face (Pose head) at one letterbox canvas Hp x Wp, up to max_batch frames per call."""
 
     def __init__(self, ctx: GpuContext, params: dict, scale: str, Hp: int, Wp: int, precision: int = PC_PREC_F16,
-                 max_det: int = 80):
-        self.ctx, self.Hp, self.Wp, self.max_det = ctx, Hp, Wp, max_det
+                 max_det: int = 80, max_batch: int = 1):
+        self.ctx, self.Hp, self.Wp, self.max_det, self.max_batch = ctx, Hp, Wp, max_det, max(1, int(max_batch))
         self.program = models_yolo.compile_yolov8(params, scale, Hp, Wp, nc=1, kpt=(NKPT, 3))
-        self.net = Net(ctx, self.program.serialize(), precision=precision, max_batch=1)
+        self.net = Net(ctx, self.program.serialize(), precision=precision, max_batch=self.max_batch)
 
     def predict(self, frame: Tuple[int, int, int, int], imgsz: int, conf: float, iou: float, max_det: int):
         """One ultralytics predict on a device frame (ptr, H, W, row_stride): returns (xyxy f32 [k][4],
         conf f32 [k], keypoints xy f32 [k][5][2]) in predict order."""
-        ptr, H, W, rs = frame
-        new_w, new_h, top, left, Hp, Wp = models_yolo.letterbox_geometry(H, W, imgsz)
-        if (Hp, Wp) != (self.Hp, self.Wp) or max_det > self.max_det:
-            raise ValueError("frame does not letterbox to this engine's canvas")
-        d = (YoloLetterboxDesc * 1)()
-        d[0].d_src, d[0].H, d[0].W, d[0].row_stride = int(ptr), H, W, rs
-        d[0].new_w, d[0].new_h, d[0].top, d[0].left = new_w, new_h, top, left
-        d[0].scale_x, d[0].scale_y = 1.0 / (float(new_w) / W), 1.0 / (float(new_h) / H)
-        d[0].simd_end = opencv_vresize_simd_end(new_w * 3)
-        d[0].identity = 1 if (new_w, new_h) == (W, H) else 0
-        sc = (YoloScale * 1)()
-        gain, px, py = models_yolo.scale_geometry(Hp, Wp, H, W)
-        sc[0].gain, sc[0].pad_x, sc[0].pad_y, sc[0].W0, sc[0].H0 = gain, float(px), float(py), float(W), float(H)
-        kpad = (C.c_float * 2)((Wp - W * gain) / 2, (Hp - H * gain) / 2)   # scale_coords: pad not rounded
-        dd = self.ctx.scratch("yf_dets", max_det * 5 * 4)
-        dk = self.ctx.scratch("yf_kpts", max_det * NKPT * 3 * 4)
-        dc = self.ctx.scratch("yf_cnt", 8)
-        check(self.ctx.lib.pc_yolo_pose_detect(self.net.handle, d, 1, Hp, Wp, C.c_float(conf), C.c_float(iou), sc,
-                                               kpad, max_det, NKPT, C.c_void_p(dd.ptr), C.c_void_p(dk.ptr),
-                                               C.c_void_p(dc.ptr), None), self.ctx.handle, "yolo_pose_detect")
-        k = int(self.ctx.download(dc.ptr, (1,), np.int32)[0])
-        k = min(k, max_det)
-        if k == 0:
-            return np.zeros((0, 4), np.float32), np.zeros((0,), np.float32), np.zeros((0, NKPT, 2), np.float32)
-        dets = self.ctx.download(dd.ptr, (k, 5), np.float32)
-        kp = self.ctx.download(dk.ptr, (k, NKPT, 3), np.float32)
-        return dets[:, :4].copy(), dets[:, 4].copy(), np.ascontiguousarray(kp[..., :2])
+        return self.predict_many([frame], imgsz, conf, iou, max_det)[0]
+
+    def predict_many(self, frames: Sequence[Tuple[int, int, int, int]], imgsz: int, conf: float, iou: float,
+                     max_det: int) -> List[tuple]:
+        """predict() of several frames that share this canvas: one letterbox + net + decode/NMS
+        launch per max_batch frames, one readback of the counts and one of the detections."""
+        out: List[tuple] = []
+        for s0 in range(0, len(frames), self.max_batch):
+            part = frames[s0:s0 + self.max_batch]
+            n = len(part)
+            d = (YoloLetterboxDesc * n)()
+            sc = (YoloScale * n)()
+            kpad = (C.c_float * (2 * n))()
+            for i, (ptr, H, W, rs) in enumerate(part):
+                new_w, new_h, top, left, Hp, Wp = models_yolo.letterbox_geometry(H, W, imgsz)
+                if (Hp, Wp) != (self.Hp, self.Wp) or max_det > self.max_det:
+                    raise ValueError("frame does not letterbox to this engine's canvas")
+                d[i].d_src, d[i].H, d[i].W, d[i].row_stride = int(ptr), H, W, rs
+                d[i].new_w, d[i].new_h, d[i].top, d[i].left = new_w, new_h, top, left
+                d[i].scale_x, d[i].scale_y = 1.0 / (float(new_w) / W), 1.0 / (float(new_h) / H)
+                d[i].simd_end = opencv_vresize_simd_end(new_w * 3)
+                d[i].identity = 1 if (new_w, new_h) == (W, H) else 0
+                gain, px, py = models_yolo.scale_geometry(Hp, Wp, H, W)
+                sc[i].gain, sc[i].pad_x, sc[i].pad_y, sc[i].W0, sc[i].H0 = gain, float(px), float(py), float(W), float(H)
+                kpad[2 * i], kpad[2 * i + 1] = (Wp - W * gain) / 2, (Hp - H * gain) / 2   # scale_coords: pad not rounded
+            dd = self.ctx.scratch("yf_dets", n * max_det * 5 * 4)
+            dk = self.ctx.scratch("yf_kpts", n * max_det * NKPT * 3 * 4)
+            dc = self.ctx.scratch("yf_cnt", n * 4 + 4)
+            check(self.ctx.lib.pc_yolo_pose_detect(self.net.handle, d, n, self.Hp, self.Wp, C.c_float(conf),
+                                                   C.c_float(iou), sc, kpad, max_det, NKPT, C.c_void_p(dd.ptr),
+                                                   C.c_void_p(dk.ptr), C.c_void_p(dc.ptr), None), self.ctx.handle,
+                  "yolo_pose_detect")
+            cnt = np.minimum(self.ctx.download(dc.ptr, (n,), np.int32), max_det)
+            if cnt.max(initial=0) == 0:
+                out.extend((np.zeros((0, 4), np.float32), np.zeros((0,), np.float32),
+                            np.zeros((0, NKPT, 2), np.float32)) for _ in range(n))
+                continue
+            dets = self.ctx.download(dd.ptr, (n, max_det, 5), np.float32)
+            kp = self.ctx.download(dk.ptr, (n, max_det, NKPT, 3), np.float32)
+            for i in range(n):
+                k = int(cnt[i])
+                out.append((dets[i, :k, :4].copy(), dets[i, :k, 4].copy(), np.ascontiguousarray(kp[i, :k, :, :2])))
+        return out
 
 
 class YoloFaceBranch:
@@ -98,15 +114,33 @@ class YoloFaceBranch:
         self.weights_source["yolo_face"] = f"synthetic:yolov8{self.yolo_scale}-face:seed{seed}"
 
     # ---- ultralytics predict on a device image ----
-    def _yf_predict(self, im, conf: float, imgsz: int, max_det: int, iou: float = 0.7):
-        imgsz = check_imgsz(imgsz)
-        g = models_yolo.letterbox_geometry(im.H, im.W, imgsz)
-        key = (g[4], g[5])
-        eng = self._yf_engines.get(key)
+    def _yf_engine(self, Hp: int, Wp: int) -> YoloFaceEngine:
+        eng = self._yf_engines.get((Hp, Wp))
         if eng is None:
-            eng = YoloFaceEngine(self._ctx, self._yf_params, self.yolo_scale, g[4], g[5], self.precision)
-            self._yf_engines[key] = eng
-        return eng.predict((im.ptr, im.H, im.W, im.stride), imgsz, float(conf), float(iou), int(max_det))
+            # batch capacity for the speculative 0-degree pass of extract_batch; big fallback
+            # canvases keep the activation footprint of a det_batch x 640 x 640 engine
+            mb = max(1, min(self._det_batch, self._det_batch * 640 * 640 // (Hp * Wp)))
+            eng = YoloFaceEngine(self._ctx, self._yf_params, self.yolo_scale, Hp, Wp, self.det_precision, max_batch=mb)
+            self._yf_engines[(Hp, Wp)] = eng
+        return eng
+
+    def _yf_predict(self, im, conf: float, imgsz: int, max_det: int, iou: float = 0.7):
+        return self._yf_predict_many([im], conf, imgsz, max_det, iou)[0]
+
+    def _yf_predict_many(self, ims, conf: float, imgsz: int, max_det: int, iou: float = 0.7) -> List[tuple]:
+        """_yf_predict of several device images: grouped by letterbox canvas, batched per group."""
+        imgsz = check_imgsz(imgsz)
+        out: List[Optional[tuple]] = [None] * len(ims)
+        groups: Dict[Tuple[int, int], List[int]] = {}
+        for i, im in enumerate(ims):
+            g = models_yolo.letterbox_geometry(im.H, im.W, imgsz)
+            groups.setdefault((g[4], g[5]), []).append(i)
+        for (Hp, Wp), idx in groups.items():
+            res = self._yf_engine(Hp, Wp).predict_many([(ims[i].ptr, ims[i].H, ims[i].W, ims[i].stride) for i in idx],
+                                                       imgsz, float(conf), float(iou), int(max_det))
+            for i, r in zip(idx, res):
+                out[i] = r
+        return out
 
     # ---- chips ----
     def _yf_align(self, im, canon: np.ndarray, d_dst: int) -> None:
@@ -208,17 +242,52 @@ class YoloFaceBranch:
         return out
 
     # ---- the YOLO branch of extract (face_embedder.py:1671-2093) ----
-    def _extract_with_yolo(self, im, imgsz: Optional[int] = None) -> List[dict]:
+    @staticmethod
+    def _yf_dyn(imgsz: Optional[int]) -> int:
+        from .face_embedder import _round32
+        dyn = int(imgsz) if (imgsz is not None and imgsz > 0) else 640
+        return _round32(max(320, dyn))
+
+    def _extract_batch_yolo(self, imgs, imgsz: Optional[int]) -> List[list]:
+        """extract() of each frame in order (the branch's own state, _prescan_rr, advances frame by
+        frame), with the 0-degree predicts of all frames batched per canvas up front (their inputs
+        do not depend on any state) and one ArcFace/quality/bank pass over the chips of every frame
+        whose faces came from that 0-degree pass."""
+        dyn = self._yf_dyn(imgsz)
+        live = [i for i, im in enumerate(imgs) if im is not None]
+        first = dict(zip(live, self._yf_predict_many([imgs[i] for i in live], self.conf, dyn, 60, iou=0.30)))
+        cap = sum(len(first[i][0]) for i in live)
+        sink = {"chips": self._ctx.scratch("yf_chips_batch", max(1, cap) * _ARC_SIDE * _ARC_SIDE * 3), "used": 0,
+                "cap": cap, "jobs": []}
+        out: List[Optional[list]] = [[] for _ in imgs]
+        for i in live:
+            sink["frame"] = i
+            r = self._extract_with_yolo(imgs[i], imgsz, first=first[i], sink=sink)
+            out[i] = r   # None: deferred into the sink
+        jobs = sink["jobs"]
+        if jobs:
+            m = sink["used"]
+            faces = self._yf_faces([b for _, boxes in jobs for b in boxes], m, sink["chips"].ptr)
+            k = 0
+            for fi, boxes in jobs:
+                lst = faces[k:k + len(boxes)]
+                k += len(boxes)
+                lst.sort(key=lambda f: (f["quality"], (f["bbox"][2] - f["bbox"][0]) * (f["bbox"][3] - f["bbox"][1])),
+                         reverse=True)
+                out[fi] = lst
+        return [o if o is not None else [] for o in out]
+
+    def _extract_with_yolo(self, im, imgsz: Optional[int] = None, first=None, sink=None) -> Optional[List[dict]]:
         from .face_embedder import _DevImage, _round32
         H0, W0 = im.H, im.W
-        dyn = int(imgsz) if (imgsz is not None and imgsz > 0) else 640
-        dyn = _round32(max(320, dyn))
+        dyn = self._yf_dyn(imgsz)
         L = max(H0, W0)
         heavy_cap = max(int(getattr(self, "_heavy_cap", 2048)), dyn)
         heavy_auto = min(_round32(max(dyn, int(0.75 * L))), heavy_cap)
         heavy_auto_180 = min(_round32(max(dyn, int(0.67 * L))), heavy_cap)
         chip_sz = _ARC_SIDE * _ARC_SIDE * 3
-        xyxy, confs, kps0 = self._yf_predict(im, self.conf, dyn, 60, iou=0.30)
+        xyxy, confs, kps0 = first if first is not None else self._yf_predict(im, self.conf, dyn, 60, iou=0.30)
+        from_first = len(xyxy) > 0
         boxes = [tuple(int(v) for v in b) for b in xyxy]
         if not boxes and not self._fast_prescan:
             for s in (1.25, 1.5):
@@ -247,14 +316,18 @@ class YoloFaceBranch:
         kps = kps0 if len(kps0) else None
         if kps is not None and len(kps) != len(boxes):
             kps = None
-        chips = self._ctx.scratch("yf_chips", len(boxes) * chip_sz)
+        defer = sink is not None and from_first and sink["used"] + len(boxes) <= sink["cap"]
+        if defer:   # chips go to the batch buffer; embedding happens once for all frames
+            base = sink["chips"].ptr + sink["used"] * chip_sz
+        else:
+            base = self._ctx.scratch("yf_chips", len(boxes) * chip_sz).ptr
         faces = []
         for i, (x1, y1, x2, y2) in enumerate(boxes):
             x1, y1 = max(0, x1), max(0, y1)
             x2, y2 = max(x1 + 1, x2), max(y1 + 1, y2)
             x2c, y2c = min(x2, W0), min(y2, H0)
             face = _DevImage(im.ptr + y1 * im.stride + x1 * 3, max(0, y2c - y1), max(0, x2c - x1), im.stride)
-            d_dst = chips.ptr + i * chip_sz
+            d_dst = base + i * chip_sz
             if kps is not None and i < len(kps) and np.isfinite(kps[i]).all():
                 pts = kps[i].astype(np.float32, copy=False)
                 five = imageops.canon_5pts(pts[:5])
@@ -274,7 +347,11 @@ class YoloFaceBranch:
                 if not self._yf_redetect_align_on_rotations(face, d_dst):
                     self._resize_chip(face, d_dst)
             faces.append((x1, y1, x2, y2))
-        out = self._yf_faces(faces, len(faces), chips.ptr)
+        if defer:
+            sink["jobs"].append((sink["frame"], faces))
+            sink["used"] += len(faces)
+            return None
+        out = self._yf_faces(faces, len(faces), base)
         out.sort(key=lambda f: (f["quality"], (f["bbox"][2] - f["bbox"][0]) * (f["bbox"][3] - f["bbox"][1])),
                  reverse=True)
         return out

@@ -122,3 +122,19 @@ def test_default_face_embedder_is_yolov8l_face(gpu_ctx, monkeypatch):
         assert f["feat"].shape == (512,) and abs(float(np.linalg.norm(f["feat"])) - 1.0) < 1e-3
         assert isinstance(f["quality"], float)
     assert fe.extract(None) == [] and fe.extract(np.zeros((0, 0, 3), np.uint8)) == []
+
+
+def test_yolo_face_batch_equals_per_frame(gpu_ctx, monkeypatch):
+    """extract_batch (0-degree predicts batched per canvas, one ArcFace pass over the chips of every
+    frame served by them) returns what extract() frame by frame returns, fallbacks included."""
+    frames = _frames(range(6)) + [None, _frames([9])[0][:200, :250]]
+    fa, _ = _device(monkeypatch, -1.5)
+    fb, _ = _device(monkeypatch, -1.5)
+    a = fa.extract_batch(frames)
+    b = [fb.extract(f) for f in frames]
+    assert sum(len(x) for x in a) >= 6
+    for fi, (x, y) in enumerate(zip(a, b)):
+        assert len(x) == len(y), fi
+        for p, q in zip(x, y):
+            assert np.array_equal(p["bbox"], q["bbox"]) and np.array_equal(p["chip"], q["chip"]), fi
+            assert np.abs(p["feat"] - q["feat"]).max() < 1e-5 and p["quality"] == q["quality"], fi
