@@ -66,25 +66,47 @@ struct LayerNormParams {
 };
 
 constexpr int LN_MAXV = 32;   // C <= 64 * 32 = 2048
+constexpr int LN_NIT = 8;     // 16-byte vectors per lane: C <= 8 * 64 * (16 / sizeof(T))
 
+__device__ __forceinline__ void ln_unpack(const f32x4& r, float* o) { o[0] = r[0]; o[1] = r[1]; o[2] = r[2]; o[3] = r[3]; }
+__device__ __forceinline__ void ln_unpack(const f16x8& r, float* o) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = (float)r[i];
+}
+
+// One wave per token, every lane holding whole 16-byte vectors of the row (vector vi at
+// lane + 64 k): one coalesced load per vector, f32 statistics by wave reduction, one 16-byte
+// store per vector. The first version kept a 32-entry per-channel array with per-entry
+// bounds checks; the compiler hoisted 32 sets of addresses and spilled ~6200 VGPRs to
+// scratch (1.5 ms per ViT-L layernorm of 32 crops instead of ~15 us).
 template <typename T>
-__global__ __launch_bounds__(256) void layernorm_rows(LayerNormParams p) {
+__global__ __launch_bounds__(256) void layernorm_vec(LayerNormParams p) {
+  constexpr int V = 16 / sizeof(T);
+  using VT = typename std::conditional<sizeof(T) == 4, f32x4, f16x8>::type;
   const int lane = threadIdx.x & 63;
-  const long long tok = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int tok = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (tok >= p.M) return;
-  const T* xr = reinterpret_cast<const T*>(p.x) + tok * p.xcs;
-  const float* ar = p.add ? p.add + (long long)(tok % p.rows) * p.C : nullptr;
-  float v[LN_MAXV];
+  const int nv = p.C / V;
+  const T* xr = reinterpret_cast<const T*>(p.x) + (size_t)tok * p.xcs;
+  const float* ar = p.add ? p.add + (size_t)(tok % p.rows) * p.C : nullptr;
+  float v[LN_NIT][V];
   float s = 0.f;
 #pragma unroll
-  for (int j = 0; j < LN_MAXV; ++j) {
-    const int c = j * 64 + lane;
-    v[j] = 0.f;
-    if (c < p.C) {
-      float t = (float)xr[c];
-      if (ar) t += ar[c];
-      v[j] = t;
-      s += t;
+  for (int k = 0; k < LN_NIT; ++k) {
+    const int vi = lane + 64 * k;
+#pragma unroll
+    for (int i = 0; i < V; ++i) v[k][i] = 0.f;
+    if (vi < nv) {
+      ln_unpack(*reinterpret_cast<const VT*>(xr + vi * V), v[k]);
+      if (ar) {
+#pragma unroll
+        for (int i = 0; i < V; i += 4) {
+          const f32x4 t = *reinterpret_cast<const f32x4*>(ar + vi * V + i);
+          v[k][i] += t[0]; v[k][i + 1] += t[1]; v[k][i + 2] += t[2]; v[k][i + 3] += t[3];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < V; ++i) s += v[k][i];
     }
   }
 #pragma unroll
@@ -92,27 +114,77 @@ __global__ __launch_bounds__(256) void layernorm_rows(LayerNormParams p) {
   const float mean = s / (float)p.C;
   float q = 0.f;
 #pragma unroll
-  for (int j = 0; j < LN_MAXV; ++j) {
-    const int c = j * 64 + lane;
-    if (c < p.C) { const float d = v[j] - mean; q += d * d; }
+  for (int k = 0; k < LN_NIT; ++k) {
+    if (lane + 64 * k < nv) {
+#pragma unroll
+      for (int i = 0; i < V; ++i) { const float d = v[k][i] - mean; q += d * d; }
+    }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
   const float rstd = 1.0f / sqrtf(q / (float)p.C + p.eps);
-  T* yr = reinterpret_cast<T*>(p.y) + tok * p.ycs;
+  T* yr = reinterpret_cast<T*>(p.y) + (size_t)tok * p.ycs;
 #pragma unroll
-  for (int j = 0; j < LN_MAXV; ++j) {
-    const int c = j * 64 + lane;
-    if (c < p.C) yr[c] = (T)((v[j] - mean) * rstd * p.gamma[c] + p.beta[c]);
-    else if (c < p.cwrite) yr[c] = (T)0.f;
+  for (int k = 0; k < LN_NIT; ++k) {
+    const int vi = lane + 64 * k;
+    if (vi < nv) {
+      VT o;
+#pragma unroll
+      for (int i = 0; i < V; i += 4) {
+        const f32x4 g = *reinterpret_cast<const f32x4*>(p.gamma + vi * V + i);
+        const f32x4 b = *reinterpret_cast<const f32x4*>(p.beta + vi * V + i);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[i + j] = (T)((v[k][i + j] - mean) * rstd * g[j] + b[j]);
+      }
+      *reinterpret_cast<VT*>(yr + vi * V) = o;
+    }
   }
+  for (int c = p.C + lane; c < p.cwrite; c += 64) yr[c] = (T)0.f;
+}
+
+// Any shape (rows not 16-byte aligned): two passes over the row from memory (L2), no
+// per-lane arrays.
+template <typename T>
+__global__ __launch_bounds__(256) void layernorm_rows(LayerNormParams p) {
+  const int lane = threadIdx.x & 63;
+  const int tok = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (tok >= p.M) return;
+  const T* xr = reinterpret_cast<const T*>(p.x) + (size_t)tok * p.xcs;
+  const float* ar = p.add ? p.add + (size_t)(tok % p.rows) * p.C : nullptr;
+  float s = 0.f;
+  for (int c = lane; c < p.C; c += 64) s += (float)xr[c] + (ar ? ar[c] : 0.f);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  const float mean = s / (float)p.C;
+  float q = 0.f;
+  for (int c = lane; c < p.C; c += 64) {
+    const float d = (float)xr[c] + (ar ? ar[c] : 0.f) - mean;
+    q += d * d;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+  const float rstd = 1.0f / sqrtf(q / (float)p.C + p.eps);
+  T* yr = reinterpret_cast<T*>(p.y) + (size_t)tok * p.ycs;
+  for (int c = lane; c < p.cwrite; c += 64)
+    yr[c] = c < p.C ? (T)(((float)xr[c] + (ar ? ar[c] : 0.f) - mean) * rstd * p.gamma[c] + p.beta[c]) : (T)0.f;
 }
 
 hipError_t layernorm_launch(int f32, const LayerNormParams& p, hipStream_t s) {
   if (p.C > 64 * LN_MAXV || p.cwrite > 64 * LN_MAXV || p.M <= 0) return hipErrorInvalidValue;
   dim3 grid((unsigned)((p.M + 3) / 4));
-  if (f32) hipLaunchKernelGGL(layernorm_rows<float>, grid, dim3(256), 0, s, p);
-  else hipLaunchKernelGGL(layernorm_rows<f16>, grid, dim3(256), 0, s, p);
+  const int V = f32 ? 4 : 8;
+  // the in-place case (y == x) is safe for both kernels: a wave reads its whole row before writing it
+  const bool vec = p.C % V == 0 && p.xcs % V == 0 && p.ycs % V == 0 && p.C / V <= 64 * LN_NIT &&
+                   (reinterpret_cast<uintptr_t>(p.x) % 16) == 0 && (reinterpret_cast<uintptr_t>(p.y) % 16) == 0 &&
+                   (reinterpret_cast<uintptr_t>(p.gamma) % 16) == 0 && (reinterpret_cast<uintptr_t>(p.beta) % 16) == 0 &&
+                   (!p.add || (reinterpret_cast<uintptr_t>(p.add) % 16) == 0);
+  if (vec) {
+    if (f32) hipLaunchKernelGGL(layernorm_vec<float>, grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL(layernorm_vec<f16>, grid, dim3(256), 0, s, p);
+  } else {
+    if (f32) hipLaunchKernelGGL(layernorm_rows<float>, grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL(layernorm_rows<f16>, grid, dim3(256), 0, s, p);
+  }
   return hipGetLastError();
 }
 
