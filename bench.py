@@ -664,6 +664,14 @@ def main_other(args):
         pcfg = PrescanConfig()
         stride = pcfg.prescan_stride
         bank_h = synth_bank(bank_n)
+        # plant a quarter of the bank from faces of the first samples (downscaled as the driver
+        # does) so spans open and the escalated two-forward path is timed too
+        r0 = PrescanRunner(fe, pcfg, 30.0, args.batch * stride, ref_feat=None, batch=args.batch)
+        ims = [r0._downscale(devs[i], i) for i in range(min(16, len(devs)))]
+        fe.set_prescan_fast(True, mode="rr")
+        seed_res = fe.extract_batch([None] * len(ims), dev_frames=ims)
+        fe.set_prescan_fast(False)
+        stats["bank_planted_rows"] = plant_bank(seed_res, bank_h)
 
         def step():
             r = PrescanRunner(fe, pcfg, 30.0, args.batch * stride, ref_feat=bank_h, batch=args.batch)
