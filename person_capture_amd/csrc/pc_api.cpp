@@ -31,7 +31,7 @@ int conv_halo_fits(int cfg, int KH, int KW, int W);
 hipError_t conv_t2d_launch(const ConvParams& p, hipStream_t s);
 int conv_t2d_supported(int cin, int npad, int KH, int KW, int stride, int pad, int act, int out_f32, int ycs,
                        int ycoff);
-int conv_t2d_rows(int npad);
+int conv_t2d_rows(int cin, int npad);
 int conv_chain_fits(int H, int W, int C, int npad, long long ktot);
 hipError_t conv_chain_launch(const void* x, int xcs, void* y, int ycs, const void* blk_dev, int nblk, int N, int H,
                              int W, long long ktot, int dbg, hipStream_t s);
@@ -644,7 +644,7 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
         conv_t2d_supported(X.C, npad, w[4], w[5], w[6], w[7], w[20], Y.is_f32, Y.cs, Y.coff) && w[15] >= 9LL * X.C &&
         (double)X.H * X.W * n->max_batch * X.cs * esz + kZeroTail < 4294967296.0 &&
         (double)M < 2147483647.0) {
-      const int th = conv_t2d_rows(npad);
+      const int th = conv_t2d_rows(X.C, npad);
       const double cover = (double)Y.H * Y.W / ((double)((Y.H + th - 1) / th * th) * ((Y.W + 15) / 16 * 16));
       if (mode == 2 || cover >= 0.75) {
         pl.t2d = 0;

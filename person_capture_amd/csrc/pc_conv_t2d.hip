@@ -27,6 +27,7 @@
 //
 // K order (tap-major, 32-channel chunks, lane group fq = 8-channel slice) is the
 // implicit-GEMM kernels' order, so results are bit-identical to conv_fast's.
+#include <stdlib.h>
 #include "pc_conv_common.h"
 
 namespace pc {
@@ -46,9 +47,14 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, in
   constexpr int NINST = NRP / 16;             // DMA instructions per chunk
   constexpr int BUFB = NCH * NRP * 64;        // one halo buffer
   constexpr int NKS = 9 * NCH;                // 32-element K steps
-  constexpr int TB = 10 * 64;                 // bias classes [9][64] + slopes [64] (f32)
+  constexpr int NPAD_T = 32 * G;
+  constexpr int TB = 10 * NPAD_T;             // bias classes [9][npad] + slopes [npad] (f32)
   static_assert(NRP % 16 == 0 && P % 8 == 0 && P >= TW + 2 && (TP == 4 || TP == 8), "halo geometry");
-  static_assert(2 * BUFB + TB * 4 + TH * 16 * (64 * G + 16) <= 163840, "LDS");
+  // output staging: its own LDS area, or (when the two halo buffers leave no room) the block's
+  // own halo buffer, free once every wave is past the K loop's closing barrier
+  constexpr bool ALIAS = 2 * BUFB + TB * 4 + TH * 16 * (64 * G + 16) > 163840;
+  static_assert(2 * BUFB + TB * 4 + (ALIAS ? 0 : TH * 16 * (64 * G + 16)) <= 163840, "LDS");
+  static_assert(!ALIAS || TH * 16 * (64 * G + 16) <= BUFB, "staging in a halo buffer");
   static_assert(NW % G == 0, "wave roles");
 
   // two halo buffers as two objects: the compiler then sees that a ds_read of one
@@ -61,7 +67,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, in
   constexpr int NPAD = 32 * G, PITCH = NPAD * 2 + 16, BPIX = TH * TW, CH8 = NPAD / 8;
   constexpr int SIT = BPIX * CH8 / (64 * NW);   // 16-byte chunks per thread per block
   static_assert(SIT * 64 * NW == BPIX * CH8, "staging split");
-  __shared__ __attribute__((aligned(16))) char stg[BPIX * PITCH];
+  __shared__ __attribute__((aligned(16))) char stg_own[ALIAS ? 16 : BPIX * PITCH];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -120,9 +126,9 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, in
   dma(tile, hbuf0);
 
   // epilogue tables: bias of border class c (BIAS_BORDER9; BIAS_CHANNEL: every class the
-  // same row) at [c*64 + ch], negative-side slopes at [576 + ch] (PReLU a, ReLU 0, none 1)
+  // same row) at [c*npad + ch], negative-side slopes at [9*npad + ch] (PReLU a, ReLU 0, none 1)
   for (int i = threadIdx.x; i < TB; i += 64 * NW) {
-    const int c = i & 63, cls = i >> 6;
+    const int cls = i / NPAD_T, c = i - cls * NPAD_T;
     float v = 0.f;
     if (c < p.npad) {
       if (cls < 9) {
@@ -168,7 +174,8 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, in
 
   f32x4 acc[TC][TP];
   // one block: multiply from `cur` while the next block's halo goes into `oth`
-  auto block = [&](const char* cur, char* oth) __attribute__((always_inline)) {
+  auto block = [&](char* cur, char* oth) __attribute__((always_inline)) {
+    char* stg = ALIAS ? cur : stg_own;
     const int nxt = tile + t_step;
     if (nxt < t_hi && !(p.dbg & 1)) dma(nxt, oth);   // dbg (tuning only): 1 no halo DMA
 
@@ -258,7 +265,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, in
     f32x4 sl[TC];
     const int cc = !border ? 0 : (ox == 0 ? 0 : (ox >= W - 1 ? 2 : 1));
 #pragma unroll
-    for (int a = 0; a < TC; ++a) sl[a] = *reinterpret_cast<const f32x4*>(tab + 576 + g * 32 + a * 16 + chq);
+    for (int a = 0; a < TC; ++a) sl[a] = *reinterpret_cast<const f32x4*>(tab + 9 * NPAD_T + g * 32 + a * 16 + chq);
     // finishing: the planner sends only the piecewise-linear activations here (none /
     // ReLU / PReLU: one select with the per-channel negative slope of the table, 1 / 0 /
     // a), so the act-before / act-after-residual order is a select, not a branch
@@ -279,7 +286,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, in
 #pragma unroll
       for (int a = 0; a < TC; ++a) {
         const int ch = g * 32 + a * 16 + chq;
-        const f32x4 bt = *reinterpret_cast<const f32x4*>(tab + (rc * 3 + cc) * 64 + ch);
+        const f32x4 bt = *reinterpret_cast<const f32x4*>(tab + (rc * 3 + cc) * NPAD_T + ch);
         float v[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -313,6 +320,8 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, in
         }
       }
     }
+    // aliased staging: the next block's DMA targets this buffer; every wave must be done reading it
+    if constexpr (ALIAS) bar();
     tile = nxt;
   };
   for (;;) {
@@ -327,18 +336,44 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, in
 // host side
 // ---------------------------------------------------------------------------
 
-// (Cin, npad) pairs the kernel is instantiated for, piecewise-linear activations, f16
-// output in whole 16-byte pixel chunks; 0 if the conv cannot run on it
+// (Cin, npad) -> instantiation: NCH 32-channel input chunks, G 32-channel output groups,
+// NW waves, TP output rows per wave (a block is TP*NW/G rows x 16 pixels). The wide shapes
+// (Cin/npad 96 and 128: SCRFD's 80x80x96 trunk, IResNet's 28x28x128 stage) hold 216 / 288
+// weight registers per wave, so they run one wave per SIMD: 3 waves for 96 output channels
+// (one SIMD idle), 4 for 128. SCRFD-10G 80x80x96 (N 64): 200 -> 134 us per conv, the net
+// 6.24 -> 5.62 ms (r03o).
+struct T2dShape { int nch, g, nw, tp; };
+static bool t2d_shape(int cin, int npad, T2dShape* sh) {
+  const bool wide = !getenv("PC_T2D_NARROW");   // tuning: the round-2 shapes only
+  if (cin == 32 && npad == 32) *sh = {1, 1, 8, 4};
+  else if (cin == 32 && npad == 64) *sh = {1, 2, 8, 4};
+  else if (cin == 64 && npad == 64) *sh = {2, 2, 4, 8};
+  else if (wide && cin == 96 && npad == 96) *sh = {3, 3, 3, 4};
+  else if (wide && cin == 64 && npad == 96) *sh = {2, 3, 3, 8};
+  // 128 channels measured slower than conv_fast's 128x256 tile (IResNet 28x28x128 b256: 101.8
+  // vs 96.0 us per conv, r03o): opt-in only
+  else if (wide && cin == 128 && npad == 128 && getenv("PC_T2D_128")) *sh = {4, 4, 4, atoi(getenv("PC_T2D_128")) == 8 ? 8 : 4};
+  else return false;
+  return true;
+}
+
+// piecewise-linear activations, f16 output in whole 16-byte pixel chunks; 0 if the conv
+// cannot run on it
 int conv_t2d_supported(int cin, int npad, int KH, int KW, int stride, int pad, int act, int out_f32, int ycs,
                        int ycoff) {
   if (KH != 3 || KW != 3 || stride != 1 || pad != 1) return 0;
   if (act != ACT_NONE && act != ACT_RELU && act != ACT_PRELU) return 0;
   if (out_f32 || (ycs & 7) || (ycoff & 7)) return 0;
-  return (cin == 32 && (npad == 32 || npad == 64)) || (cin == 64 && npad == 64);
+  T2dShape sh;
+  return t2d_shape(cin, npad, &sh) ? 1 : 0;
 }
 
-// output rows per block for npad (the block is TH x 16 pixels)
-int conv_t2d_rows(int npad) { return npad == 32 ? 32 : 16; }
+// output rows per block (the block is TH x 16 pixels)
+int conv_t2d_rows(int cin, int npad) {
+  T2dShape sh;
+  if (!t2d_shape(cin, npad, &sh)) return 16;
+  return sh.tp * sh.nw / sh.g;
+}
 
 template <int NCH, int G, int NW, int TP>
 static hipError_t launch_t2d(const ConvParams& p, hipStream_t s) {
@@ -366,8 +401,13 @@ hipError_t conv_t2d_launch(const ConvParams& p, hipStream_t s) {
     return hipErrorInvalidValue;
   // Cin 64: the 144 weight registers leave no room for a second wave per SIMD, so 4
   // waves of 8 rows each (a block is 16 x 16 pixels either way)
-  if (S.C == 32) return p.npad == 32 ? launch_t2d<1, 1, 8, 4>(p, s) : launch_t2d<1, 2, 8, 4>(p, s);
-  return launch_t2d<2, 2, 4, 8>(p, s);
+  T2dShape sh;
+  t2d_shape(S.C, p.npad, &sh);
+  if (sh.nch == 1) return p.npad == 32 ? launch_t2d<1, 1, 8, 4>(p, s) : launch_t2d<1, 2, 8, 4>(p, s);
+  if (sh.nch == 2 && sh.g == 2) return launch_t2d<2, 2, 4, 8>(p, s);
+  if (sh.nch == 2) return launch_t2d<2, 3, 3, 8>(p, s);
+  if (sh.nch == 3) return launch_t2d<3, 3, 3, 4>(p, s);
+  return sh.tp == 8 ? launch_t2d<4, 4, 4, 8>(p, s) : launch_t2d<4, 4, 4, 4>(p, s);
 }
 
 }  // namespace pc

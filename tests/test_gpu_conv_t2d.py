@@ -55,6 +55,7 @@ def _build(case, rng):
 def _run(gpu_ctx, monkeypatch, P, xin, N, mode):
     from person_capture_amd.runtime import Net
     monkeypatch.setenv("PC_CONV_T2D", mode)
+    monkeypatch.setenv("PC_T2D_128", "1")   # the opt-in 128-channel shape is tested too
     net = Net(gpu_ctx, P.serialize(), precision=PC_PREC_F16, max_batch=N)
     d = gpu_ctx.upload(xin.astype(np.float16))
     net.run(d.ptr, N)
@@ -83,6 +84,13 @@ CASES = [
     (4, 80, 80, 64, 64, pg.ACT_RELU, pg.BIAS_CHANNEL, 1, 1, 0),       # SCRFD stage shape
     (2, 160, 160, 32, 32, pg.ACT_RELU, pg.BIAS_CHANNEL, 0, 0, 0),     # SCRFD stem shape (half size)
     (8, 56, 56, 64, 64, pg.ACT_NONE, pg.BIAS_CHANNEL, 1, 0, 0),       # IResNet stage 1
+    # wide shapes (one wave per SIMD, 216 / 288 weight registers)
+    (2, 80, 80, 96, 96, pg.ACT_RELU, pg.BIAS_CHANNEL, 1, 1, 0),       # SCRFD-10G 80x80x96 block conv2
+    (3, 23, 37, 96, 80, pg.ACT_RELU, pg.BIAS_CHANNEL, 0, 0, 0),       # ragged, cout < npad 96
+    (2, 40, 40, 64, 96, pg.ACT_RELU, pg.BIAS_CHANNEL, 0, 0, 0),       # 64 -> 96
+    (3, 28, 28, 128, 128, pg.ACT_PRELU, pg.BIAS_BORDER9, 0, 0, 0),    # IResNet 28x28x128 conv1
+    (4, 28, 28, 128, 128, pg.ACT_NONE, pg.BIAS_CHANNEL, 1, 0, 0),     # IResNet 28x28x128 conv2 + residual
+    (2, 13, 50, 128, 120, pg.ACT_RELU, pg.BIAS_CHANNEL, 0, 0, 0),     # ragged, cout < npad 128
 ]
 
 
