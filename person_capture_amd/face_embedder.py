@@ -294,6 +294,7 @@ class FaceEmbedder(YoloFaceBranch):
         self.state_trace: Optional[list] = None
         self._fb_cache: Dict[tuple, tuple] = {}
         self.fb_stats = [0, 0]   # fallback detections served by the batched prefetch / run one by one
+        self.fb_kind_stats: Dict[str, List[int]] = {}   # the same per view kind ("tta", "pad", "rot")
         if self.detector_backend == "scrfd":
             self.scrfd = self._engine(640)
             if callable(progress):
@@ -372,10 +373,13 @@ class FaceEmbedder(YoloFaceBranch):
         exactly these parameters, else now (make() builds the view image on the device)."""
         key = (im.ptr, im.H, im.W, im.stride) + tuple(view) + (int(dyn), float(conf))
         hit = self._fb_cache.pop(key, None)
+        per = self.fb_kind_stats.setdefault(view[0], [0, 0])
         if hit is not None:
             self.fb_stats[0] += 1
+            per[0] += 1
             return hit
         self.fb_stats[1] += 1
+        per[1] += 1
         return self._detect_once(make(), dyn, conf)
 
     def _fb_run(self, jobs: list) -> None:
@@ -387,6 +391,64 @@ class FaceEmbedder(YoloFaceBranch):
             res = self._engine(D).detect_frames([(g.ptr, g.H, g.W, g.stride) for _, g in lst], thresh=cf)
             for (key, _), r in zip(lst, res):
                 self._fb_cache[key] = r
+
+    def _prefetch_rotations_normal(self, idx: List[int], imgs, spec_dyn: list, still_empty: set, scratch_img) -> None:
+        """Normal-mode rotation passes (face_embedder.py:2330-2433) of the chunk's frames that stay
+        empty after TTA and edge pad: the gate is simulated over the chunk (frame counter, last
+        face index; rotations assumed to find nothing), then stage by stage over the frames still
+        empty — per degree 90 / 270 / 180 the probe and the heavy passes at 1280 / 1536, a frame
+        leaving the plan at its first hit, as the policy does."""
+        fi, last = self._frame_idx, self._last_face_idx
+        plan = []
+        for i in idx:
+            if imgs[i] is None or spec_dyn[i] is None:
+                continue
+            fi += 1
+            if i not in still_empty:
+                last = fi   # faces at 0 degrees or in the TTA / pad passes
+                continue
+            if self.rot_adaptive:
+                need = (fi - last) <= self.rot_after_hit_frames or ((fi + (id(self) & 7)) % self.rot_every_n) == 0
+            else:
+                need = True
+            if need:
+                plan.append(i)
+        if not plan:
+            return
+        probe_conf = max(0.02, float(getattr(self, "_probe_conf", 0.02)))
+        pad = 24
+        pending = list(plan)
+        for deg in (90, 270, 180):
+            if not pending:
+                break
+            conf_deg = max(0.10, float(self.conf) * (0.8 if deg in (90, 270) else 0.6))
+            jobs = []
+            for i in pending:
+                im = imgs[i]
+                probe_dyn = _round32(max(320, min(spec_dyn[i], int(getattr(self, "_prescan_probe_imgsz", 384)))))
+                img_r = scratch_img("rot", i, lambda k: self._dev_rotate_pad(im, deg, 0, key=k))
+                jobs.append(((im.ptr, im.H, im.W, im.stride, "rot", deg, 0, probe_dyn, float(probe_conf)), img_r,
+                             probe_dyn, probe_conf))
+            self._fb_run(jobs)
+            heavy_img = {i: scratch_img("rot", i, lambda k, im=imgs[i]: self._dev_rotate_pad(im, deg, pad, key=k))
+                         for i in pending}
+            left = list(pending)
+            for stage in range(2):
+                jobs = []
+                for i in left:
+                    im, dyn = imgs[i], spec_dyn[i]
+                    sizes = []
+                    for base in (max(dyn, 1280), max(dyn, 1536)):
+                        if _round32(base) not in sizes:
+                            sizes.append(_round32(base))
+                    if stage < len(sizes):
+                        jobs.append(((im.ptr, im.H, im.W, im.stride, "rot", deg, pad, sizes[stage], float(conf_deg)),
+                                     heavy_img[i], sizes[stage], conf_deg))
+                self._fb_run(jobs)
+                hit = {j[0][:4] for j in jobs if len(self._fb_cache.get(j[0], ((),))[0])}
+                left = [i for i in left if (imgs[i].ptr, imgs[i].H, imgs[i].W, imgs[i].stride) not in hit]
+            # a hit at this degree ends the frame's rotation passes (dets found -> break)
+            pending = left
 
     def _empty_at_0(self, im: _DevImage, first) -> bool:
         bb, kp = first
@@ -439,6 +501,9 @@ class FaceEmbedder(YoloFaceBranch):
                     jobs.append(((im.ptr, im.H, im.W, im.stride, "pad", pad, spec_dyn[i], float(probe_conf)), img_p,
                                  spec_dyn[i], probe_conf))
             self._fb_run(jobs)
+            pending = [i for i in pending if not any(len(self._fb_cache.get(j[0], ((),))[0]) for j in jobs
+                                                     if j[0][:4] == (imgs[i].ptr, imgs[i].H, imgs[i].W, imgs[i].stride))]
+            self._prefetch_rotations_normal(idx, imgs, spec_dyn, set(pending), scratch_img)
             return
         if self.rot_adaptive:
             return   # rotation gating depends on the sequential hit history

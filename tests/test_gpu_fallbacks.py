@@ -187,8 +187,9 @@ def test_scrfd_fallback_branches(gpu_ctx, monkeypatch):
     o.rot_every_n, o.rot_after_hit_frames = 3, 6
     frames = fallback_sequence()
     got, ref, traces = _run(fe, o, frames)
-    print("branches:", sorted(traces), "fallback detections prefetched/inline:", fe.fb_stats)
+    print("branches:", sorted(traces), "fallback detections prefetched/inline:", fe.fb_stats, fe.fb_kind_stats)
     assert fe.fb_stats[0] > 0   # the batched speculative prefetch served some of them
+    assert fe.fb_kind_stats["rot"][0] > 0   # normal-mode rotation passes too (gate simulated per chunk)
     for b in ("tta0.75", "tta0.6", "tta1.25", "edgepad", "rot90", "rot270", "rot180", "eyeroll",
               "size512", "size1280", "size1536"):
         assert b in traces, b
