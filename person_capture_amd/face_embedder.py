@@ -24,9 +24,14 @@ Weights: scrfd_*_bnkps.onnx and arcface_r100.onnx (glintr100 / w600k_r50) are lo
 where the reference's _ensure_file looks (plus PERSON_CAPTURE_AMD_MODELS) and mapped by
 onnx_models.py; when they are absent (the reference would download them; there is no
 network here) seeded synthetic weights of the same architectures stand in
-(person_capture_amd/models.py) and `weights_source` says so. Backends that are not on this build's hot path
-(YOLOv8-face detector, OpenCLIP embeddings) raise RuntimeError at construction,
-as the reference does for unavailable backends.
+(person_capture_amd/models.py) and `weights_source` says so.
+
+The YOLOv8-face backend (the reference default, Y8F_DEFAULT) runs too: face_yolo.py
+(YOLOv8 Pose program on the device, the branch policy of face_embedder.py:1671-2093 on the
+host, 0-degree predicts batched across frames in extract_batch). The OpenCLIP face-embedding
+backend (use_arcface=False) is not on this build's hot path and raises RuntimeError at
+construction, as the reference does for unavailable backends. Host frames reach the device
+through the native pinned staging ring (pc_frame_stage) on a copy stream.
 """
 from __future__ import annotations
 

@@ -175,7 +175,8 @@ def test_c3_bench_config_parity_f32(gpu_ctx, monkeypatch, c3_frames, c3_oracle):
                         "decision_flips_outside_1e-2": int(e2e_flip)})
     assert n_fallback <= 2
     assert n_exact + n_chained >= 4 * NFRAMES
-    assert e2e_flip == 0 and max(e2e_fd, default=0) < 1e-2
+    # measured r03 (profiles/r03_parity_c3_f32.json): 332 chained faces, max |dfd| 6.6e-4
+    assert e2e_flip == 0 and max(e2e_fd, default=0) < 2e-3
     assert n_acc > 0 and n_rej > 0
 
 
