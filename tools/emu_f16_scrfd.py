@@ -17,12 +17,21 @@ from person_capture_amd import models
 _conv = F.conv2d
 
 
-def run(p, x, keep32=lambda i: False, w16=True, a16=True):
+def _split(t):
+    hi = t.half().float()
+    return hi, (t - hi).half().float()
+
+
+def run(p, x, keep32=lambda i: False, w16=True, a16=True, x3=False):
     i = [0]
 
     def conv(inp, w, b=None, *a, **k):
         j = i[0]
         i[0] += 1
+        if x3:   # f16x3: hi*hi + lo*hi + hi*lo, f32 accumulation (the dropped lo*lo ~2^-22)
+            xh, xl = _split(inp)
+            wh, wl = _split(w)
+            return _conv(xh, wh, b, *a, **k) + _conv(xl, wh, None, *a, **k) + _conv(xh, wl, None, *a, **k)
         if not keep32(j):
             if a16:
                 inp = inp.half().float()
@@ -71,6 +80,8 @@ def main():
     print(f"{'activations only f16':26s}: {err(out)}", flush=True)
     out, _ = run(p, x, a16=False)
     print(f"{'weights only f16':26s}: {err(out)}", flush=True)
+    out, _ = run(p, x, x3=True)
+    print(f"{'f16x3 (hi/lo split)':26s}: {err(out)}", flush=True)
 
 
 if __name__ == "__main__":
