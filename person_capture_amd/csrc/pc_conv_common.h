@@ -204,7 +204,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, f32x4 (&acc)[
 // - bias (per channel or border class), activation, residual, zeroed channel
 // padding - and stores them with one 16-byte (f16) or two (f32) stores, so each
 // pixel row of the tile leaves as contiguous bytes and no load waits behind a store.
-template <typename T, int BC, int BP, int WC, int WP, int EPI_MAX = 131072>
+template <typename T, int BC, int BP, int WC, int WP, int EPI_MAX = 131072, int RGMAX = 8>
 __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, f32x4 (&acc)[BC / WC / 16][BP / WP / 16],
                                                   int c0, int p0, int wr, int wc, int lane, char* smem) {
   constexpr int NW = WC * WP, NT = 64 * NW;
@@ -300,8 +300,13 @@ __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, f32x4 (&a
       // these stay within the 256 registers of a 2-waves-per-SIMD kernel)
       using RV = typename std::conditional<ESZ == 2, f16x8, f32x4>::type;
       constexpr int RN = ESZ == 2 ? 1 : 2;
+      // r03: all rows of the pass at once when they are few (IT <= RGMAX): with RG = 1 the
+      // 256x224 tile's 7 rows per pass were 14 dependent residual round trips per tile
+      // (most of its ~11 us epilogue)
       constexpr int RG0 = (NPASS == 2 ? 2 : 4) < IT ? (NPASS == 2 ? 2 : 4) : IT;
-      constexpr int RG = IT % RG0 == 0 ? RG0 : (IT % 2 == 0 ? 2 : 1);
+      // (f16 tiles below 256x256 only: the f32 and the largest f16 instantiations spill with it)
+      constexpr int RGM = (ESZ == 2 && BC * BP < 65536) ? RGMAX : 0;
+      constexpr int RG = IT <= RGM ? IT : (IT % RG0 == 0 ? RG0 : (IT % 2 == 0 ? 2 : 1));
       static_assert(IT % RG == 0, "residual groups");
 #pragma unroll 1
       for (int kg = 0; kg < IT; kg += RG) {

@@ -9,7 +9,8 @@ import numpy as np
 
 from person_capture_amd import models
 from person_capture_amd import program as pg
-from person_capture_amd._lib import PC_PREC_F16
+import os
+from person_capture_amd._lib import PC_PREC_F16, PC_PREC_F32
 from person_capture_amd.runtime import GpuContext, Net
 
 
@@ -33,9 +34,10 @@ def main():
         P = models.compile_iresnet(models.synth_iresnet(100, seed=0, calibrate=False), 100)
     else:
         P = models.compile_scrfd(models.synth_scrfd("10g", seed=0, calibrate=False), "10g", 640)
-    net = Net(ctx, P.serialize(), PC_PREC_F16, max_batch=B)
+    prec = PC_PREC_F32 if os.environ.get('PROBE_F32') else PC_PREC_F16
+    net = Net(ctx, P.serialize(), prec, max_batch=B)
     H, W, Cc = P.dims(P.input)
-    x = np.zeros((B, H, W, Cc), np.float16)
+    x = np.zeros((B, H, W, Cc), np.float32 if prec == PC_PREC_F32 else np.float16)
     x[..., :3] = np.random.default_rng(0).standard_normal((B, H, W, 3))
     d = ctx.upload(x)
     for _ in range(3):
