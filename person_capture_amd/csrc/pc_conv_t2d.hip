@@ -39,7 +39,9 @@ __device__ __forceinline__ void t2d_read_frags(const char* a0, f16x8* fb, std::i
 }
 // NCH: 32-channel input chunks (Cin = 32*NCH); G: 32-channel output groups (npad = 32*G);
 // NW waves, each owning TP output rows of 16 pixels x 32 output channels.
-template <int NCH, int G, int NW, int TP>
+// NBUF 3: three halo buffers, block i+2's halo is requested while block i is multiplied (the
+// DMA of one block of small TH does not hide behind one block's K loop).
+template <int NCH, int G, int NW, int TP, int NBUF = 2>
 __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, int ntx, int ntiles) {
   constexpr int TW = 16, P = 24, TC = 2;
   constexpr int TH = TP * NW / G;             // output rows per block
@@ -52,8 +54,10 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, in
   static_assert(NRP % 16 == 0 && P % 8 == 0 && P >= TW + 2 && (TP == 4 || TP == 8), "halo geometry");
   // output staging: its own LDS area, or (when the two halo buffers leave no room) the block's
   // own halo buffer, free once every wave is past the K loop's closing barrier
-  constexpr bool ALIAS = 2 * BUFB + TB * 4 + TH * 16 * (64 * G + 16) > 163840;
-  static_assert(2 * BUFB + TB * 4 + (ALIAS ? 0 : TH * 16 * (64 * G + 16)) <= 163840, "LDS");
+  static_assert(NBUF == 2 || NBUF == 3, "halo buffers");
+  constexpr bool ALIAS = NBUF * BUFB + TB * 4 + TH * 16 * (64 * G + 16) > 163840;
+  static_assert(NBUF == 2 || !ALIAS, "three halo buffers need their own staging area");
+  static_assert(NBUF * BUFB + TB * 4 + (ALIAS ? 0 : TH * 16 * (64 * G + 16)) <= 163840, "LDS");
   static_assert(!ALIAS || TH * 16 * (64 * G + 16) <= BUFB, "staging in a halo buffer");
   static_assert(NW % G == 0, "wave roles");
 
@@ -61,6 +65,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, in
   // cannot alias the LDS-DMA into the other and does not drain vmcnt before it
   __shared__ __attribute__((aligned(16))) char hbuf0[BUFB];
   __shared__ __attribute__((aligned(16))) char hbuf1[BUFB];
+  __shared__ __attribute__((aligned(16))) char hbuf2[NBUF == 3 ? BUFB : 16];
   __shared__ __attribute__((aligned(16))) float tab[TB];
   // output staging: [pixel][npad] f16 rows, pitch padded by 16 B (conflict-free 8-byte
   // fragment writes, 16-byte aligned row reads)
@@ -124,6 +129,9 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, in
 
   int tile = t_first;
   dma(tile, hbuf0);
+  if constexpr (NBUF == 3) {
+    if (tile + t_step < t_hi) dma(tile + t_step, hbuf1);
+  }
 
   // epilogue tables: bias of border class c (BIAS_BORDER9; BIAS_CHANNEL: every class the
   // same row) at [c*npad + ch], negative-side slopes at [9*npad + ch] (PReLU a, ReLU 0, none 1)
@@ -177,7 +185,13 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, in
   auto block = [&](char* cur, char* oth) __attribute__((always_inline)) {
     char* stg = ALIAS ? cur : stg_own;
     const int nxt = tile + t_step;
-    if (nxt < t_hi && !(p.dbg & 1)) dma(nxt, oth);   // dbg (tuning only): 1 no halo DMA
+    // NBUF 2: the next block's halo into `oth` now; NBUF 3: block i+1's halo is already in
+    // flight, block i+2's goes into `oth` after this block's residual loads (so the wait at
+    // the end of the K loop can leave it outstanding)
+    const bool dma2 = NBUF == 3 && nxt + t_step < t_hi && !(p.dbg & 1);
+    if constexpr (NBUF == 2) {
+      if (nxt < t_hi && !(p.dbg & 1)) dma(nxt, oth);   // dbg (tuning only): 1 no halo DMA
+    }
 
     int n, ty, tx;
     decode(tile, n, ty, tx);
@@ -213,6 +227,9 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, in
       }
     }
 
+    if constexpr (NBUF == 3) {
+      if (dma2) dma(nxt + t_step, oth);
+    }
 #pragma unroll
     for (int a = 0; a < TC; ++a)
 #pragma unroll
@@ -257,8 +274,19 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, in
       __builtin_amdgcn_sched_barrier(0);
     });
 
-    // next halo landed (own DMAs; also the residual) and every wave is done with `cur`
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // next halo landed (own DMAs; also the residual) and every wave is done with `cur`;
+    // NBUF 3: block i+2's DMA (issued last; every wave issued at least NDMA / NW of it) may
+    // stay in flight
+    if constexpr (NBUF == 3) {
+      if (dma2) {
+        static_assert(NDMA / NW <= 63, "vmcnt range");
+        asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NDMA / NW) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     bar();
 
     // ---- epilogue: bias (per channel / border class), activation, residual, padding ----
@@ -324,11 +352,22 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, in
     if constexpr (ALIAS) bar();
     tile = nxt;
   };
-  for (;;) {
-    block(hbuf0, hbuf1);
-    if (tile >= t_hi) break;
-    block(hbuf1, hbuf0);
-    if (tile >= t_hi) break;
+  if constexpr (NBUF == 3) {
+    for (;;) {
+      block(hbuf0, hbuf2);
+      if (tile >= t_hi) break;
+      block(hbuf1, hbuf0);
+      if (tile >= t_hi) break;
+      block(hbuf2, hbuf1);
+      if (tile >= t_hi) break;
+    }
+  } else {
+    for (;;) {
+      block(hbuf0, hbuf1);
+      if (tile >= t_hi) break;
+      block(hbuf1, hbuf0);
+      if (tile >= t_hi) break;
+    }
   }
 }
 
@@ -342,14 +381,15 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, in
 // weight registers per wave, so they run one wave per SIMD: 3 waves for 96 output channels
 // (one SIMD idle), 4 for 128. SCRFD-10G 80x80x96 (N 64): 200 -> 134 us per conv, the net
 // 6.24 -> 5.62 ms (r03o).
-struct T2dShape { int nch, g, nw, tp; };
+struct T2dShape { int nch, g, nw, tp, nbuf = 2; };
 static bool t2d_shape(int cin, int npad, T2dShape* sh) {
   const bool wide = !getenv("PC_T2D_NARROW");   // tuning: the round-2 shapes only
+  const bool la = getenv("PC_T2D_NBUF3") != nullptr;   // tuning: two-block halo lookahead
   if (cin == 32 && npad == 32) *sh = {1, 1, 8, 4};
-  else if (cin == 32 && npad == 64) *sh = {1, 2, 8, 4};
-  else if (cin == 64 && npad == 64) *sh = {2, 2, 4, 8};
-  else if (wide && cin == 96 && npad == 96) *sh = {3, 3, 3, 4};
-  else if (wide && cin == 64 && npad == 96) *sh = {2, 3, 3, 8};
+  else if (cin == 32 && npad == 64) *sh = {1, 2, 8, 4, la ? 3 : 2};
+  else if (cin == 64 && npad == 64) *sh = la ? T2dShape{2, 2, 4, 4, 3} : T2dShape{2, 2, 4, 8};
+  else if (wide && cin == 96 && npad == 96) *sh = {3, 3, 3, 4, la ? 3 : 2};
+  else if (wide && cin == 64 && npad == 96) *sh = {2, 3, 3, 8, la ? 3 : 2};
   // 128 channels measured slower than conv_fast's 128x256 tile (IResNet 28x28x128 b256: 101.8
   // vs 96.0 us per conv, r03o): opt-in only
   else if (wide && cin == 128 && npad == 128 && getenv("PC_T2D_128")) *sh = {4, 4, 4, atoi(getenv("PC_T2D_128")) == 8 ? 8 : 4};
@@ -375,7 +415,7 @@ int conv_t2d_rows(int cin, int npad) {
   return sh.tp * sh.nw / sh.g;
 }
 
-template <int NCH, int G, int NW, int TP>
+template <int NCH, int G, int NW, int TP, int NBUF = 2>
 static hipError_t launch_t2d(const ConvParams& p, hipStream_t s) {
   static int ncu = 0;
   if (!ncu) {
@@ -389,7 +429,7 @@ static hipError_t launch_t2d(const ConvParams& p, hipStream_t s) {
   const long long nt = (long long)p.N * nty * ntx;
   if (nt <= 0 || nt >= (1LL << 31)) return hipErrorInvalidValue;
   const int grid = (int)std::min<long long>(nt, ncu);
-  hipLaunchKernelGGL((conv_t2d<NCH, G, NW, TP>), dim3(grid), dim3(64 * NW), 0, s, p, nty, ntx, (int)nt);
+  hipLaunchKernelGGL((conv_t2d<NCH, G, NW, TP, NBUF>), dim3(grid), dim3(64 * NW), 0, s, p, nty, ntx, (int)nt);
   return hipGetLastError();
 }
 
@@ -403,10 +443,12 @@ hipError_t conv_t2d_launch(const ConvParams& p, hipStream_t s) {
   // waves of 8 rows each (a block is 16 x 16 pixels either way)
   T2dShape sh;
   t2d_shape(S.C, p.npad, &sh);
-  if (sh.nch == 1) return p.npad == 32 ? launch_t2d<1, 1, 8, 4>(p, s) : launch_t2d<1, 2, 8, 4>(p, s);
-  if (sh.nch == 2 && sh.g == 2) return launch_t2d<2, 2, 4, 8>(p, s);
-  if (sh.nch == 2) return launch_t2d<2, 3, 3, 8>(p, s);
-  if (sh.nch == 3) return launch_t2d<3, 3, 3, 4>(p, s);
+  const bool b3 = sh.nbuf == 3;
+  if (sh.nch == 1)
+    return p.npad == 32 ? launch_t2d<1, 1, 8, 4>(p, s) : (b3 ? launch_t2d<1, 2, 8, 4, 3>(p, s) : launch_t2d<1, 2, 8, 4>(p, s));
+  if (sh.nch == 2 && sh.g == 2) return b3 ? launch_t2d<2, 2, 4, 4, 3>(p, s) : launch_t2d<2, 2, 4, 8>(p, s);
+  if (sh.nch == 2) return b3 ? launch_t2d<2, 3, 3, 8, 3>(p, s) : launch_t2d<2, 3, 3, 8>(p, s);
+  if (sh.nch == 3) return b3 ? launch_t2d<3, 3, 3, 4, 3>(p, s) : launch_t2d<3, 3, 3, 4>(p, s);
   return sh.tp == 8 ? launch_t2d<4, 4, 4, 8>(p, s) : launch_t2d<4, 4, 4, 4>(p, s);
 }
 
