@@ -460,7 +460,7 @@ struct pc_net {
   std::vector<void*> arrays;  // device copies (conv weights in act dtype, others f32)
   std::vector<long long> array_count;
   std::vector<ConvPlan> plans;
-  std::vector<ConvPlan> plans_small;   // tiles chosen for small_batch images, used for N <= 2 * small_batch
+  std::vector<ConvPlan> plans_small;   // tiles chosen for small_batch images, used for N <= small_batch
   int small_batch = 0;
   std::vector<StemPlan> stems;
   std::vector<ChainPlan> chains;
@@ -1056,7 +1056,7 @@ static int run_ops(pc_net* n, int N) {
       }
     }
     if (w[0] == OP_CONV) {
-      const bool small = N <= 2 * n->small_batch;
+      const bool small = N <= n->small_batch;   // (N up to 2x measured worse: SCRFD at 32 of 64)
       const ConvPlan& pl = small ? n->plans_small[i] : n->plans[i];
       rec.small = small;
       ConvParams p;
