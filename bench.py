@@ -133,7 +133,7 @@ def cpu_baseline(frames: np.ndarray, fe, bank: np.ndarray, n_sample: int, n_samp
     return out
 
 
-def f16_parity(fe16, devs, bank_h) -> dict:
+def f16_parity(fe16, devs, bank_h, conf: float = 0.5) -> dict:
     """Outside the timed region: the same frames through an f32 FaceEmbedder (the parity mode,
     itself checked against the fp32 CPU oracle in tests/test_gpu_bench_config.py) against the
     f16 throughput mode, face by face (nearest box): how many decisions f16 changes, and where
@@ -160,7 +160,7 @@ def f16_parity(fe16, devs, bank_h) -> dict:
         os.environ[k] = "f32"
     try:
         fe32 = FaceEmbedder(ctx=f"cuda:{_device(int(os.environ.get('LOCAL_RANK', '0')))}",
-                            yolo_model="scrfd_10g_bnkps", conf=0.5)
+                            yolo_model="scrfd_10g_bnkps", conf=conf)
         res32 = run(fe32, DeviceBank(fe32._ctx, bank_h))
         chips16 = [f["chip"] for r in res16 for f in r]
         e32_on16 = fe32._arc.embed(np.stack(chips16), flip=True) if chips16 else np.zeros((0, 512), np.float32)
@@ -212,6 +212,39 @@ def f16_parity(fe16, devs, bank_h) -> dict:
                 "note": "arcface_only: f16 fd vs the f32 ArcFace on the f16 pass's own chips; the rest of the "
                         "difference enters through the SCRFD f16 landmarks (a different aligned chip; the "
                         "bench frames are u8 noise, so a sub-pixel landmark shift resamples the chip)"}}
+
+
+def smooth_parity(fe16, frames: np.ndarray, bank_rows: int) -> dict:
+    """The f16-vs-f32 comparison on the bench frames low-pass filtered (Gaussian, sigma 1.5 px):
+    u8 noise frames resample to unrelated chips under a sub-pixel landmark shift, smooth
+    frames (like camera images) do not. Same planted-bank construction, own bank."""
+    from scipy.ndimage import gaussian_filter
+    from person_capture_amd.face_embedder import _DevImage
+    from person_capture_amd.match import DeviceBank
+    sm = np.empty_like(frames)
+    for i, f in enumerate(frames):   # blur, then restore contrast about the noise mean 127.5
+        g = gaussian_filter(f.astype(np.float32), sigma=(1.5, 1.5, 0))
+        sm[i] = np.clip(np.rint(128.0 + 2.5 * (g - 127.5)), 0, 255).astype(np.uint8)
+    ctx = fe16._ctx
+    d = ctx.alloc(sm.nbytes)
+    ctx.upload(sm, d)
+    fsz = sm[0].nbytes
+    H, W = sm.shape[1:3]
+    devs = [_DevImage(d.ptr + i * fsz, H, W, W * 3) for i in range(len(sm))]
+    bank_h = synth_bank(bank_rows)
+    conf0 = fe16.conf
+    fe16.conf = 0.8   # the synthetic SCRFD fires on ~380 anchors of a smooth 1080p frame at 0.5, ~6 at 0.8
+    try:
+        first = fe16.extract_batch([None] * len(devs), dev_frames=devs, bank=DeviceBank(ctx, bank_h))
+        plant_bank(first, bank_h)
+        r = f16_parity(fe16, devs, bank_h, conf=0.8)
+    finally:
+        fe16.conf = conf0
+    r.pop("flipped_faces_f32_distance_to_0.32", None)
+    r["frames"] = "bench frames, Gaussian sigma 1.5 px, contrast x2.5 about 127.5; SCRFD conf 0.8"
+    ctx.sync()
+    d.free()
+    return r
 
 
 def _kernel_of(code: float, cfg: float) -> str:
@@ -482,6 +515,7 @@ def main():
             "chips_identical": pd["attribution"]["chips_identical"],
             "note": "SCRFD f32 + ArcFace f16 (env PERSON_CAPTURE_AMD_DET_PRECISION=f32): identical chips, the "
                     "remaining flips are the f16 ArcFace's"}
+        out["parity"]["smooth_frames"] = smooth_parity(fe, frames, args.bank)
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(frames, fe, bank_h, args.cpu_sample, args.cpu_sample_1t)
     if rank == 0:
