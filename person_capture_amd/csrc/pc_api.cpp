@@ -39,6 +39,7 @@ size_t conv_chain_block_bytes();
 int stem_fused_ok(int f32, int cin, int cin_true, int KH, int KW, int npad, int cwrite, int ycs, int ycoff);
 hipError_t stem_fused_launch(const StemParams& p, const void* wpk, const float* bias, const float* slope, int npad,
                              int cwrite, hipStream_t s);
+hipError_t splitk_finish_launch(int f32, const ConvParams& p, hipStream_t s);
 hipError_t splitk_reduce_launch(int f32, const float* part, int splitk, int M, int npad, int cout, const float* bias,
                                 const float* slope, int act, void* y, int ycs, int out_f32, hipStream_t s);
 hipError_t stem_launch(int f32, const StemParams& p, hipStream_t s);
@@ -516,7 +517,7 @@ static unsigned tensor_zero_off(const pc_net* n, int t) {
 
 static const int kNumConvCfgs = 14;   // pc_conv.hip launch_rowb
 
-static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_batch) {
+static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_batch, bool small = false) {
   const int* w = op.w;
   const int out = w[1], nseg = w[2], npad = w[14];
   const int esz = n->f32 ? 4 : 2;
@@ -650,6 +651,26 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
         pl.t2d = 0;
         pl.fast = -1;
         pl.halo = -1;
+      }
+    }
+  }
+  // small-batch plan: a long-K conv of a few images fills a fraction of the CUs (a 14x14x256
+  // conv of 12 rows: 56 workgroups of 2304-long K) - split K over the generic kernel so the
+  // grid covers them; the partials are finished by splitk_finish with the full epilogue.
+  // Opt-in (PC_SMALL_SPLITK=1): split-K sums in another order, so a frame's results would
+  // depend on the batch it ran in, and extract() / extract_batch() are bit-identical by
+  // contract (tests/test_gpu_face_embedder.py::test_extract_single_matches_batch).
+  if (small && pl.splitk == 1 && !n->f32 && getenv("PC_SMALL_SPLITK")) {
+    const long long t = tiles(cfg);
+    const int ktiles = (int)(w[15] * esz / rowb);
+    if (t < 192 && ktiles >= 16) {
+      int sk = (int)std::min<long long>(8, std::max<long long>(2, 384 / std::max<long long>(1, t)));
+      sk = std::min(sk, ktiles / 4);
+      if (sk >= 2) {
+        pl.splitk = sk;
+        pl.fast = pl.halo = pl.t2d = -1;
+        pl.cfg = cfg;
+        pl.rowb = rowb;
       }
     }
   }
@@ -918,8 +939,11 @@ extern "C" int pc_net_create(pc_ctx* c, const void* prog, size_t nbytes, int pre
       if (rc) break;
       // small batches (per-frame extract: one frame's faces, prescan samples) get their own
       // tile choice: the max-batch tiles would leave most CUs idle
-      if (n->small_batch > 0) rc = plan_conv(n, op, n->plans_small[i], n->small_batch);
+      if (n->small_batch > 0) rc = plan_conv(n, op, n->plans_small[i], n->small_batch, true);
       if (rc) break;
+      if (n->small_batch > 0 && n->plans_small[i].splitk > 1)
+        part = std::max(part, (size_t)((long long)n->plans_small[i].splitk * n->plans_small[i].M_per_image *
+                                       n->small_batch * op.w[14] * 4));
       const ConvPlan& pl = n->plans[i];
       if (pl.splitk > 1) part = std::max(part, (size_t)((long long)pl.splitk * pl.M_per_image * max_batch * op.w[14] * 4));
       const NetTensor& Y = n->tens[op.w[1]];
@@ -1111,8 +1135,7 @@ static int run_ops(pc_net* n, int N) {
         HIPCHK(c, conv_launch(n->f32, pl.rowb, pl.cfg, p, s));
       }
       if (pl.splitk > 1) {
-        HIPCHK(c, splitk_reduce_launch(n->f32, n->partial, pl.splitk, p.M, p.npad, p.cout, p.bias, p.slope, p.act,
-                                       p.y, p.ycs, p.out_f32, s));
+        HIPCHK(c, splitk_finish_launch(n->f32, p, s));
       }
     } else if (w[0] == OP_STEM) {
       StemParams p;

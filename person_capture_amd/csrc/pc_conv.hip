@@ -291,6 +291,54 @@ __global__ void splitk_reduce(const float* __restrict__ part, int splitk, int M,
   else reinterpret_cast<T*>(y)[(long long)pix * ycs + ch] = (T)s;
 }
 
+// Sum split-K partials and finish with the conv's full epilogue (bias per channel or border
+// class, PReLU / ReLU / SiLU / GELU before or after the residual, same-pixel or nearest-up2
+// residual, zero channel padding): the small-batch plans split long-K convs of a few images
+// over K so the grid covers the CUs (r03). One thread per output element.
+template <typename T>
+__global__ void splitk_finish(ConvParams p) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long total = (long long)p.M * p.cwrite;
+  if (i >= total) return;
+  const int pix = (int)(i / p.cwrite);
+  const int ch = (int)(i - (long long)pix * p.cwrite);
+  float v = 0.f;
+  if (ch < p.cout) {
+    for (int z = 0; z < p.splitk; ++z) v += p.partial[((long long)z * p.M + pix) * p.npad + ch];
+    const int hw = p.OH * p.OW;
+    const int n = pix / hw, rem = pix - n * hw;
+    const int oh = rem / p.OW, ow = rem - oh * p.OW;
+    if (p.bias_mode == BIAS_CHANNEL) {
+      v += p.bias[ch];
+    } else if (p.bias_mode == BIAS_BORDER9) {
+      const ConvSeg& S = p.seg[0];
+      const int ih0 = oh * S.stride - S.pad, iw0 = ow * S.stride - S.pad;
+      const int rc = ih0 < 0 ? 0 : (ih0 + S.KH - 1 >= S.H ? 2 : 1);
+      const int cc = iw0 < 0 ? 0 : (iw0 + S.KW - 1 >= S.W ? 2 : 1);
+      v += p.bias[(rc * 3 + cc) * p.npad + ch];
+    }
+    const float sl = p.act == ACT_PRELU ? p.slope[ch] : 0.f;
+    if (!p.act_after_res) v = act_apply(v, p.act, sl);
+    if (p.res_mode != RES_NONE) {
+      const long long rpix = p.res_mode == RES_UP2 ? ((long long)n * p.rH + (oh >> 1)) * p.rW + (ow >> 1)
+                                                   : (long long)pix;
+      v += (float)reinterpret_cast<const T*>(p.res)[rpix * p.rcs + ch];
+    }
+    if (p.act_after_res) v = act_apply(v, p.act, sl);
+  }
+  if (p.out_f32) reinterpret_cast<float*>(p.y)[(long long)pix * p.ycs + ch] = v;
+  else reinterpret_cast<T*>(p.y)[(long long)pix * p.ycs + ch] = (T)v;
+}
+
+hipError_t splitk_finish_launch(int f32, const ConvParams& p, hipStream_t s) {
+  const long long total = (long long)p.M * p.cwrite;
+  if (total <= 0 || p.splitk < 1) return hipErrorInvalidValue;
+  dim3 grid((unsigned)((total + 255) / 256));
+  if (f32) hipLaunchKernelGGL(splitk_finish<float>, grid, dim3(256), 0, s, p);
+  else hipLaunchKernelGGL(splitk_finish<f16>, grid, dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
 // Direct 3x3 conv for stems: input NHWC with exactly 4 (padded) channels, one
 // thread per output pixel, the whole [cout][3][3][4] filter bank in LDS. The
 // 36-value input patch stays in registers (compile-time indexed).
