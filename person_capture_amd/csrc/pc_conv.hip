@@ -80,10 +80,16 @@ __global__ __launch_bounds__(64 * WC * WP, 1) void conv_igemm(ConvParams p) {
   }
   // current segment, cached in scalars
   const char* sx;
+  // MUBUF LDS-DMA (a pending FLAT global_load_lds counts in lgkmcnt and forces lgkmcnt(0)
+  // before the fragment reads' consumers)
+  __amdgpu_buffer_rsrc_t xrs;
+  const __amdgpu_buffer_rsrc_t wrs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.w), (short)0, (int)0xffffffff, 0x00020000);
   int sH, sW, scs, sKH, sKW, sstr, spad, scblk;
   unsigned szero;
   auto load_seg = [&](const ConvSeg& S) __attribute__((always_inline)) {
     sx = reinterpret_cast<const char*>(S.x);
+    xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(S.x), (short)0, (int)0xffffffff, 0x00020000);
     sH = S.H; sW = S.W; scs = S.cs;
     sKH = S.KH; sKW = S.KW; sstr = S.stride; spad = S.pad;
     scblk = S.cblk; szero = S.zero_off;
@@ -155,17 +161,18 @@ __global__ __launch_bounds__(64 * WC * WP, 1) void conv_igemm(ConvParams p) {
 
   auto stage = [&](auto bufc, int ktl) __attribute__((always_inline)) {
     constexpr int buf = decltype(bufc)::value;
-    const char* xb = sx + cb * (BKE * ESZ);
-    const char* wb = reinterpret_cast<const char*>(p.w) + (long long)ktl * (BKE * ESZ);
+    const int xso = cb * (BKE * ESZ), wso = ktl * (BKE * ESZ);
     static_for<NI>([&](auto ic) __attribute__((always_inline)) {
       constexpr int i = decltype(ic)::value;
       const int g = i * NW + wave;
       if (g < NTOT) {
         unsigned off = g * RPI < BC ? woff[i] : xcur[i];
         asm volatile("" : "+v"(off));   // keep the 32-bit offset in-block (SGPR base + VGPR offset form)
-        const char* src = (g * RPI < BC ? wb : xb) + off;
         char* dst = smem + buf * BUF + g * 1024;
-        __builtin_amdgcn_global_load_lds((gptr_t)src, (lds_ptr_t)dst, 16, 0, 0);
+        if (g * RPI < BC)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_ptr_t)dst, 16, off, wso, 0, 0);
+        else
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)dst, 16, off, xso, 0, 0);
       }
     });
   };

@@ -88,8 +88,15 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
   // current issue segment (scalars)
   const char* sx;
   int sH, sW, scs, sKW, scblk;
+  // buffer resources over the whole 32-bit offset range (every offset is < 4 GiB by the
+  // planner's 32-bit offset rule, so the range check never fires)
+  auto rsrc = [&](const void* base) __attribute__((always_inline)) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)0xffffffff, 0x00020000);
+  };
+  __amdgpu_buffer_rsrc_t xrs;
   auto load_seg = [&](const ConvSeg& S) __attribute__((always_inline)) {
     sx = reinterpret_cast<const char*>(S.x);
+    xrs = rsrc(sx);
     sH = S.H; sW = S.W; scs = S.cs; sKW = S.KW; scblk = S.cblk;
     const int hw = p.OH * p.OW;
     static_for<NIB>([&](auto ic) __attribute__((always_inline)) {
@@ -109,20 +116,23 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
   load_seg(p.seg[0]);
   int iseg = 0, ith = 0, itw = 0, icb = 0;
   const int seg0_kh = p.seg[0].KH;
-  const char* wsrc = reinterpret_cast<const char*>(p.w);
+  const __amdgpu_buffer_rsrc_t wrs = rsrc(p.w);
 
   // DMA of the current iterator position (K-tile index kt) into ring slot `slot`
   auto issue = [&](auto slotc, int kt) __attribute__((always_inline)) {
     constexpr int slot = decltype(slotc)::value;
-    const char* wb = wsrc + (long long)kt * ROWB;
+    // MUBUF LDS-DMA (buffer_load ... lds), not FLAT global_load_lds: a pending FLAT op
+    // counts in lgkmcnt too, so the compiler waited lgkmcnt(0) before the first MFMA of
+    // every K-tile instead of counting the fragment reads
+    const int wso = kt * ROWB;
     static_for<NIA>([&](auto ic) __attribute__((always_inline)) {
       constexpr int i = decltype(ic)::value;
       unsigned off = woff[i];
       asm volatile("" : "+v"(off));
-      __builtin_amdgcn_global_load_lds((gptr_t)(wb + off), (lds_ptr_t)(smem + slot * BUF + (i * NW + wave) * 1024),
-                                       16, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_ptr_t)(smem + slot * BUF + (i * NW + wave) * 1024), 16, off,
+                                               wso, 0, 0);
     });
-    const char* xb = sx + icb * ROWB;
+    const int xso = icb * ROWB;
     const unsigned tapoff = (unsigned)((ith * sW + itw) * scs * ESZ);
     static_for<NIB>([&](auto ic) __attribute__((always_inline)) {
       constexpr int i = decltype(ic)::value;
@@ -131,7 +141,7 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
       asm volatile("" : "+v"(off));
       const int dst = (NB % NW == 0 || i * NW + wave < NB) ? slot * BUF + BC * ROWB + (i * NW + wave) * 1024
                                                            : RING + wave * 1024;
-      __builtin_amdgcn_global_load_lds((gptr_t)(xb + off), (lds_ptr_t)(smem + dst), 16, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)(smem + dst), 16, off, xso, 0, 0);
     });
   };
   // advance the issue iterator by one K-tile (no-op once the last tile was issued)
@@ -162,9 +172,43 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
   const int sw = (fr >> 1) & (CHUNKS - 1);
   const unsigned a_row = (wr * WTC + fr) * ROWB;
   const unsigned b_row = (BC + wc * WTP + fr) * ROWB;
+  // Pinned two-k-substep schedule (f16, 128-byte K rows, two register sets fit beside the
+  // accumulators): the 11 fragment reads of k-substep 0 go out first, the reads of k-substep 1
+  // are interleaved one per MFMA with k-substep 0's MFMAs, and every MFMA waits (counted
+  // lgkmcnt, inserted by the compiler from the pinned order) only for its own two fragments.
+  // The compiler's own schedule waited lgkmcnt(0) for all of a substep's reads at the tile
+  // start and again halfway through it (A fragments re-read into the same registers), which
+  // exposed the LDS latency twice per K-tile on top of the barrier.
+  constexpr bool PINNED = ESZ == 2 && KSTEPS == 2 && 2 * (TC + TP) * 4 + TC * TP * 4 <= 200;
+  auto compute_pinned = [&](auto slotc) __attribute__((always_inline)) {
+    constexpr int slot = decltype(slotc)::value;
+    const char* base = smem + slot * BUF;
+    f16x8 fa[2][TC], fb[2][TP];
+    auto rd = [&](int ks, int i) __attribute__((always_inline)) {   // read i: A0, B0..B(TP-1), A1..A(TC-1)
+      const unsigned ko = ((ks * 4 + (lane >> 4)) ^ sw) << 4;
+      if (i == 0) fa[ks][0] = *reinterpret_cast<const f16x8*>(base + a_row + ko);
+      else if (i <= TP) fb[ks][i - 1] = *reinterpret_cast<const f16x8*>(base + b_row + ko + (i - 1) * 16 * ROWB);
+      else fa[ks][i - TP] = *reinterpret_cast<const f16x8*>(base + a_row + ko + (i - TP) * 16 * ROWB);
+    };
+    static_for<TC + TP>([&](auto ic) __attribute__((always_inline)) { rd(0, decltype(ic)::value); });
+    __builtin_amdgcn_sched_barrier(0);
+    static_for<2>([&](auto kc) __attribute__((always_inline)) {
+      constexpr int ks = decltype(kc)::value;
+      static_for<TC * TP>([&](auto mc) __attribute__((always_inline)) {
+        constexpr int m = decltype(mc)::value, a = m / TP, b = m % TP;
+        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[ks][a], fb[ks][b], acc[a][b], 0, 0, 0);
+        if constexpr (ks == 0 && m < TC + TP) rd(1, m);
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    });
+  };
   auto compute = [&](auto slotc) __attribute__((always_inline)) {
     constexpr int slot = decltype(slotc)::value;
     const char* base = smem + slot * BUF;
+    if constexpr (PINNED) {
+      compute_pinned(slotc);
+      return;
+    }
 #pragma unroll
     for (int ks = 0; ks < KSTEPS; ++ks) {
       if constexpr (ESZ == 2) {

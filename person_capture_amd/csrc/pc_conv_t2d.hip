@@ -80,7 +80,11 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, in
   const int g = wave % G, pg = wave / G;      // output-channel group, pixel-row group
   const int fr = lane & 15, fq = lane >> 4;
   const ConvSeg& S = p.seg[0];
-  const char* xs = reinterpret_cast<const char*>(S.x);
+  // MUBUF LDS-DMA over the input (buffer_load ... lds): a pending FLAT global_load_lds also
+  // counts in lgkmcnt, which made the compiler wait lgkmcnt(0) before nearly every MFMA
+  // (125 such waits for 144 MFMAs) instead of counting the fragment reads
+  const __amdgpu_buffer_rsrc_t xrs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(S.x), (short)0, (int)0xffffffff, 0x00020000);
   const unsigned xrow = (unsigned)S.cs * 2u;
   const int H = S.H, W = S.W;
 
@@ -121,8 +125,8 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, in
         const unsigned pix = (unsigned)((n * H + iy) * W + ix);
         unsigned off = ok ? pix * xrow + sc : S.zero_off + sc;
         asm volatile("" : "+v"(off));
-        __builtin_amdgcn_global_load_lds((gptr_t)(xs + j * 64 + off),
-                                         (lds_ptr_t)(dst + j * NRP * 64 + gi * 1024), 16, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)(dst + j * NRP * 64 + gi * 1024), 16, off, j * 64, 0,
+                                                 0);
       }
     });
   };

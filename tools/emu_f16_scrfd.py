@@ -22,7 +22,7 @@ def _split(t):
     return hi, (t - hi).half().float()
 
 
-def run(p, x, keep32=lambda i: False, w16=True, a16=True, x3=False):
+def run(p, x, keep32=lambda i: False, w16=True, a16=True, x3=False, w2=False):
     i = [0]
 
     def conv(inp, w, b=None, *a, **k):
@@ -32,6 +32,10 @@ def run(p, x, keep32=lambda i: False, w16=True, a16=True, x3=False):
             xh, xl = _split(inp)
             wh, wl = _split(w)
             return _conv(xh, wh, b, *a, **k) + _conv(xl, wh, None, *a, **k) + _conv(xh, wl, None, *a, **k)
+        if w2:   # weights hi + lo, activations stored f16: x16*W_hi + x16*W_lo (2x K)
+            xh = inp.half().float()
+            wh, wl = _split(w)
+            return _conv(xh, wh, b, *a, **k) + _conv(xh, wl, None, *a, **k)
         if not keep32(j):
             if a16:
                 inp = inp.half().float()
@@ -80,6 +84,8 @@ def main():
     print(f"{'activations only f16':26s}: {err(out)}", flush=True)
     out, _ = run(p, x, a16=False)
     print(f"{'weights only f16':26s}: {err(out)}", flush=True)
+    out, _ = run(p, x, w2=True)
+    print(f"{'f16 acts, W hi+lo (2x K)':26s}: {err(out)}", flush=True)
     out, _ = run(p, x, x3=True)
     print(f"{'f16x3 (hi/lo split)':26s}: {err(out)}", flush=True)
 
