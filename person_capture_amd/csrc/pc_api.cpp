@@ -614,14 +614,14 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
     }
     if ((double)npad * w[15] * esz >= 4294967296.0) ok = false;
     if (ok) {
-      static const double cost[] = {1.0, 1.12, 1.12, 1.3, 1.3, 1.3, 1.15, 1.45, 1.3, 1.0, 0.9, 1.3, 1.6, 1.0};
-      static const int occ[] = {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 1, 1, 1};   // workgroups per CU
+      static const double cost[] = {1.0, 1.12, 1.12, 1.3, 1.3, 1.3, 1.15, 1.45, 1.3, 1.0, 0.9, 1.3, 1.6, 1.0, 1.0};
+      static const int occ[] = {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 1, 1, 1, 2};   // workgroups per CU
       int best = -1, best_rowb = rowb;
       double best_t = 0;
       for (int k = 0; k < conv_fast_num_cfgs(); ++k) {
         int bc = 0, bp = 0;
         conv_fast_tile(k, &bc, &bp);
-        const int rb = k == 10 ? 64 : rowb;   // cfg 10 runs on 64-byte K rows only
+        const int rb = (k == 10 || k == 14) ? 64 : rowb;   // cfgs 10 and 14 run on 64-byte K rows only
         if (npad % bc || !conv_fast_valid(k, rb)) continue;
         if (force > 0 && k != force - 1) continue;
         const long long t = (M + bp - 1) / bp * (npad / bc);

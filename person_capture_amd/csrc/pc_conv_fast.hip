@@ -179,11 +179,11 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
   // The compiler's own schedule waited lgkmcnt(0) for all of a substep's reads at the tile
   // start and again halfway through it (A fragments re-read into the same registers), which
   // exposed the LDS latency twice per K-tile on top of the barrier.
-  constexpr bool PINNED = ESZ == 2 && KSTEPS == 2 && 2 * (TC + TP) * 4 + TC * TP * 4 <= 200;
+  constexpr bool PINNED = ESZ == 2 && KSTEPS <= 2 && NW % 4 == 0 && KSTEPS * (TC + TP) * 4 + TC * TP * 4 <= 200;
   auto compute_pinned = [&](auto slotc) __attribute__((always_inline)) {
     constexpr int slot = decltype(slotc)::value;
     const char* base = smem + slot * BUF;
-    f16x8 fa[2][TC], fb[2][TP];
+    f16x8 fa[KSTEPS][TC], fb[KSTEPS][TP];
     auto rd = [&](int ks, int i) __attribute__((always_inline)) {   // read i: A0, B0..B(TP-1), A1..A(TC-1)
       const unsigned ko = ((ks * 4 + (lane >> 4)) ^ sw) << 4;
       if (i == 0) fa[ks][0] = *reinterpret_cast<const f16x8*>(base + a_row + ko);
@@ -192,12 +192,12 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
     };
     static_for<TC + TP>([&](auto ic) __attribute__((always_inline)) { rd(0, decltype(ic)::value); });
     __builtin_amdgcn_sched_barrier(0);
-    static_for<2>([&](auto kc) __attribute__((always_inline)) {
+    static_for<KSTEPS>([&](auto kc) __attribute__((always_inline)) {
       constexpr int ks = decltype(kc)::value;
       static_for<TC * TP>([&](auto mc) __attribute__((always_inline)) {
         constexpr int m = decltype(mc)::value, a = m / TP, b = m % TP;
         acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[ks][a], fb[ks][b], acc[a][b], 0, 0, 0);
-        if constexpr (ks == 0 && m < TC + TP) rd(1, m);
+        if constexpr (ks + 1 < KSTEPS && m < TC + TP) rd(ks + 1, m);
         __builtin_amdgcn_sched_barrier(0);
       });
     });
@@ -311,6 +311,7 @@ static const FastCfg kFastCfgs[] = {
     {96, 384, 6},    // 11: 1x6 waves, 96x64 per wave (96-channel trunks at 64-byte K rows)
     {32, 256, 2},    // 12: 1x2 waves, 32x128 per wave (detector heads, npad 32)
     {256, 224, 8},   // 13: 4x2 waves, 64x112 per wave: 50176-pixel layers (b256 14x14) fill 224 CUs
+    {128, 224, 4},   // 14: 2x2 waves, 64x112 per wave, ROWB 64 only, 3 stages, 2 workgroups per CU
 };
 static const int kNumFastCfgs = sizeof(kFastCfgs) / sizeof(kFastCfgs[0]);
 
@@ -354,6 +355,9 @@ static hipError_t launch_fast_t(const ConvParams& p, int cfg, hipStream_t s) {
     case 11: return launch_fast_cfg<T, 96, 384, ROWB, 1, 6, ROWB == 128 ? 2 : 4>(p, s);
     case 12: return launch_fast_cfg<T, 32, 256, ROWB, 1, 2, ROWB == 128 ? 3 : 4>(p, s);
     case 13: return launch_fast_cfg<T, 256, 224, ROWB, 4, 2, ROWB == 128 ? 2 : 4>(p, s);
+    case 14:
+      if constexpr (ROWB == 64) return launch_fast_cfg<T, 128, 224, 64, 2, 2, 3, 2>(p, s);
+      else return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }
 }
@@ -362,7 +366,7 @@ static hipError_t launch_fast_t(const ConvParams& p, int cfg, hipStream_t s) {
 int conv_fast_valid(int cfg, int rowb) {
   if (cfg < 0 || cfg >= kNumFastCfgs || (rowb != 64 && rowb != 128)) return 0;
   const FastCfg& c = kFastCfgs[cfg];
-  if (cfg == 10 && rowb != 64) return 0;   // sized for 2 workgroups per CU at 64-byte K rows
+  if ((cfg == 10 || cfg == 14) && rowb != 64) return 0;   // sized for 2 workgroups per CU at 64-byte K rows
   const int rpi = 1024 / rowb;
   return (c.bc / rpi) % c.nw == 0 && c.bp % rpi == 0;
 }

@@ -59,7 +59,7 @@ CASES = [
 
 
 ALL_CFGS = ([None] + [f"{c}{r}" for c in range(14) for r in ("", ":64")] + [f"h{k}" for k in range(5)]
-            + [f"f{k}{r}" for k in range(14) for r in ("", ":64")])
+            + [f"f{k}{r}" for k in range(15) for r in ("", ":64")])
 
 
 def _set_cfg(monkeypatch, cfg):
