@@ -208,15 +208,21 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, in
     f16x4 rv[TP][TC];
     // (addresses of pixels outside the image are clamped, not branched around: a load
     // under a divergent branch merges into a phi that waits for it right there)
+    // Row part of the address is wave-uniform (scalar math, 64-bit), the lane part a 24-bit
+    // multiply (pixel column x pixel stride < 2^32): the per-lane 64-bit multiply chains of the
+    // first version were a large share of the kernel's VALU work. Lanes past the image read
+    // column 0 of the row (their values are never stored).
     if (has_res) {
+      const bool up2 = p.res_mode == RES_UP2;
+      const unsigned rcs = (unsigned)p.rcs;
+      const unsigned lcol = (unsigned)(colok ? (up2 ? ox >> 1 : ox) : 0);
+      const unsigned loff = __umul24(lcol, rcs);
 #pragma unroll
       for (int t = 0; t < TP; ++t) {
         const int oy = oy0 + t;
-        const bool ok = colok && oy < H;
-        const int qy = ok ? oy : 0, qx = ok ? ox : 0;
-        const long long rpix = p.res_mode == RES_UP2 ? ((long long)n * p.rH + (qy >> 1)) * p.rW + (qx >> 1)
-                                                     : ((long long)n * H + qy) * W + qx;
-        const f16* rp = reinterpret_cast<const f16*>(p.res) + rpix * p.rcs;
+        const int qy = oy < H ? oy : 0;
+        const long long rrow = up2 ? ((long long)n * p.rH + (qy >> 1)) * p.rW : ((long long)n * H + qy) * W;
+        const f16* rp = reinterpret_cast<const f16*>(p.res) + rrow * p.rcs + loff;
 #pragma unroll
         for (int a = 0; a < TC; ++a) {
           const int ch = g * 32 + a * 16 + chq;
@@ -336,14 +342,18 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, in
     __syncthreads();
     if (!(p.dbg & 4)) {   // dbg 4 (tuning only): no stores
       const int cw8 = (p.cwrite + 7) >> 3;
+      // block origin (uniform, 64-bit) + lane offset in 32 bits (one image's elements < 2^32)
+      f16* const yblk = reinterpret_cast<f16*>(p.y) + (((long long)n * H + ty * TH) * W + tx * TW) * p.ycs;
+      const unsigned ycs = (unsigned)p.ycs;
 #pragma unroll
       for (int k = 0; k < SIT; ++k) {
         const int idx = threadIdx.x + k * 64 * NW;
         const int pl = idx / CH8, cq = idx - (idx / CH8) * CH8;
-        const int oy = ty * TH + pl / TW, oxx = tx * TW + (pl & (TW - 1));
+        const int ry = pl / TW, rx = pl & (TW - 1);
+        const int oy = ty * TH + ry, oxx = tx * TW + rx;
         if (oy >= H || oxx >= W || cq >= cw8) continue;
         const f16x8 val = *reinterpret_cast<const f16x8*>(stg + pl * PITCH + cq * 16);
-        f16* yp = reinterpret_cast<f16*>(p.y) + (((long long)n * H + oy) * W + oxx) * p.ycs + cq * 8;
+        f16* yp = yblk + (__umul24((unsigned)(ry * W + rx), ycs) + (unsigned)(cq * 8));
         if (cq * 8 + 8 <= p.cwrite) {
           *reinterpret_cast<f16x8*>(yp) = val;
         } else {
