@@ -11,7 +11,9 @@ import ctypes as C
 import os
 from pathlib import Path
 
-LIB_PATH = Path(__file__).resolve().parent / "lib" / "libpcgpu.so"
+# PC_LIB_PATH: an alternative build of the same library (interleaved A/B runs of two
+# builds on one box, tools/gpu_run.sh "ab"), so the in-tree library is never swapped
+LIB_PATH = Path(os.environ.get("PC_LIB_PATH") or Path(__file__).resolve().parent / "lib" / "libpcgpu.so")
 
 PC_OK = 0
 PC_PREC_F16 = 0

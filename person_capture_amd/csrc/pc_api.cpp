@@ -15,6 +15,8 @@
 #include <map>
 #include <algorithm>
 #include <thread>
+#include <mutex>
+#include <system_error>
 #include "../../include/pcgpu.h"
 #include "pc_common.h"
 
@@ -166,6 +168,7 @@ struct pc_ctx {
   struct FrameSlot { char* h = nullptr; size_t cap = 0; hipEvent_t ev = nullptr; bool pending = false; };
   FrameSlot fslots[4];
   int fslot_next = 0;
+  std::mutex fslot_mu;   // one context may be shared by FaceEmbedders on several host threads
 };
 
 static int fail(pc_ctx* c, int code, const std::string& msg) {
@@ -349,6 +352,7 @@ extern "C" int pc_frame_stage(pc_ctx* c, void* d_dst, const void* h_src, size_t 
   if (!c || !d_dst || !h_src || src_stride < row_bytes) return PC_ERR_ARG;
   const size_t n = row_bytes * rows;
   if (!n) return PC_OK;
+  std::lock_guard<std::mutex> lock(c->fslot_mu);   // the slot ring and its stream order
   auto& fs = c->fslots[c->fslot_next];
   c->fslot_next = (c->fslot_next + 1) % 4;
   if (fs.pending) HIPCHK(c, hipEventSynchronize(fs.ev));
@@ -377,11 +381,18 @@ extern "C" int pc_frame_stage(pc_ctx* c, void* d_dst, const void* h_src, size_t 
   } else {
     std::vector<std::thread> pool;
     const size_t per = (rows + nt - 1) / nt;
+    size_t done = std::min(rows, per);   // rows [0, done) are this thread's; the rest as threads start
     for (int t = 1; t < nt; ++t) {
       const size_t r0 = std::min(rows, t * per), r1 = std::min(rows, (t + 1) * per);
-      if (r0 < r1) pool.emplace_back(pack, r0, r1);
+      if (r0 >= r1) continue;
+      try {
+        pool.emplace_back(pack, r0, r1);
+      } catch (const std::system_error&) {   // no thread available: pack the rest here
+        pack(r0, rows);
+        break;
+      }
     }
-    pack(0, std::min(rows, per));
+    pack(0, done);
     for (auto& th : pool) th.join();
   }
   HIPCHK(c, hipMemcpyAsync(d_dst, fs.h, n, hipMemcpyHostToDevice, c->stream));
@@ -1348,7 +1359,14 @@ extern "C" int pc_net_chain_info(pc_net* n, int32_t* min_batch, int32_t* per_rou
 }
 extern "C" int pc_net_set_chain_min_batch(pc_net* n, int32_t min_batch) {
   if (!n) return -PC_ERR_ARG;
-  n->chain_min_batch = min_batch <= 0 ? (1 << 30) : min_batch;
+  const int v = min_batch <= 0 ? (1 << 30) : min_batch;
+  if (v != n->chain_min_batch) {
+    // captured graphs replay the launch schedule of their capture (chain or per-conv)
+    hipStreamSynchronize(n->ctx->stream);
+    for (auto& kv : n->graphs) hipGraphExecDestroy(kv.second);
+    n->graphs.clear();
+  }
+  n->chain_min_batch = v;
   return 0;
 }
 extern "C" int pc_net_stats(pc_net* n, double* flops, int32_t* launches) {

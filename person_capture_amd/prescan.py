@@ -27,6 +27,7 @@ refinement re-scan (:1670-) which reuses this same per-sample step at a finer st
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Callable, List, Optional, Sequence, Tuple
 
@@ -294,14 +295,37 @@ def run_cached(runner: "PrescanRunner", frame_at, video, refs="", cache_dir: str
     its result. `settings`: the SessionConfig-like source of the key (default: the runner's
     PrescanConfig, other keys at SessionConfig defaults). Returns (spans, bank, hit)."""
     from . import prescan_cache as pcache
-    meta = pcache.cache_meta(settings if settings is not None else runner.cfg, video, refs, runner.fps, runner.total)
+    if settings is None:
+        settings = _runner_settings(runner)
+    meta = pcache.cache_meta(settings, video, refs, runner.fps, runner.total)
     root = pcache.cache_root(cache_dir)
     hit, spans, bank = pcache.load(root, meta, mode)
     if hit:
         return spans, bank, True
     spans, bank = runner.run(frame_at)
-    pcache.save(root, meta, spans, bank, mode)
+    try:   # a read-only or full cache dir must not lose the computed result (gui_app.py:919)
+        pcache.save(root, meta, spans, bank, mode)
+    except Exception as e:   # noqa: BLE001 - the reference logs and continues the same way
+        runner.cache_error = f"{type(e).__name__}: {e}"
     return spans, bank, False
+
+
+def _runner_settings(runner: "PrescanRunner") -> dict:
+    """Cache-key settings of a runner: its PrescanConfig fields plus the face backend that
+    actually ran (face_model / use_arcface are key fields, gui_app.py:821-825), so caches of
+    different detectors never collide."""
+    from dataclasses import asdict
+    s = asdict(runner.cfg)
+    face = getattr(runner, "face", None)
+    model = getattr(face, "detector_backend", None)
+    if model == "scrfd" or model is None:
+        variant = getattr(face, "scrfd_variant", "10g")
+        model = {"10g": "scrfd_10g_bnkps", "2.5g": "scrfd_2.5g_bnkps"}.get(variant, f"scrfd_{variant}")
+    elif model == "yolo":   # the model name the FaceEmbedder was built with
+        model = os.path.basename(str(getattr(face, "_scrfd_model_path", "") or "yolov8-face"))
+    s["face_model"] = model
+    s["use_arcface"] = bool(getattr(face, "use_arcface", True))
+    return s
 
 
 def prescan_sequential(face, cfg: PrescanConfig, fps: float, total_frames: int, frame_at, ref_feat=None):

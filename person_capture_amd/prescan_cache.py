@@ -112,7 +112,7 @@ def load(root: Path, meta: dict, mode: str = "auto") -> Tuple[bool, List[Tuple[i
                 if f.size > 0:
                     feat = f.reshape(f.shape[0], -1) if f.ndim >= 2 else f.reshape(1, -1)
             return True, spans, feat
-    except (OSError, ValueError, KeyError):
+    except Exception:   # any damaged file is a miss, as gui_app.py:880 treats it
         return False, [], None
 
 

@@ -79,6 +79,59 @@ def test_run_cached_hit_skips_the_loop(tmp_path):
     assert run_cached(r, None, "/nonexistent/v.mp4", "", cache_dir=str(tmp_path))[2] is False and r.calls == 2
 
 
+def test_cache_damaged_file_is_a_miss_and_save_failure_keeps_result(tmp_path):
+    """gui_app.py:880/919 catch every exception: a truncated .npz is a miss, and a cache
+    directory that cannot be written still returns the freshly computed result."""
+    from person_capture_amd.prescan import PrescanConfig, run_cached
+
+    meta = pc.cache_meta({}, "/nonexistent/v.mp4", "", 30.0, 600)
+    root = tmp_path / "c"
+    out = pc.save(root, meta, [(0, 9)], np.eye(2, 512, dtype=np.float32))
+    data = open(out, "rb").read()
+    for cut in (0, 10, len(data) // 2):
+        open(out, "wb").write(data[:cut])
+        assert pc.load(root, meta) == (False, [], None)
+
+    class Runner:
+        cfg, fps, total, calls = PrescanConfig(), 30.0, 600, 0
+
+        def run(self, frame_at):
+            self.calls += 1
+            return [(0, 99)], np.eye(2, 512, dtype=np.float32)
+
+    blocker = tmp_path / "file_not_dir"
+    blocker.write_text("x")   # the cache "directory" is a file: mkdir / open fail
+    r = Runner()
+    spans, bank, hit = run_cached(r, None, "/nonexistent/v.mp4", "", cache_dir=str(blocker / "sub"))
+    assert not hit and spans == [(0, 99)] and bank.shape == (2, 512) and r.calls == 1
+    assert "Error" in r.cache_error
+
+
+def test_cache_key_follows_the_face_backend(tmp_path):
+    """The key records the detector that ran (face_model is a key field, gui_app.py:821)."""
+    from person_capture_amd.prescan import PrescanConfig, _runner_settings
+
+    class Face:
+        detector_backend, scrfd_variant, use_arcface = "scrfd", "10g", True
+
+    class Runner:
+        cfg, fps, total, face = PrescanConfig(), 30.0, 600, Face()
+
+    keys = set()
+    for backend, variant, path in (("scrfd", "10g", ""), ("scrfd", "2.5g", ""), ("yolo", "10g", "yolov8l-face")):
+        r = Runner()
+        r.face = Face()
+        r.face.detector_backend, r.face.scrfd_variant, r.face._scrfd_model_path = backend, variant, path
+        s = _runner_settings(r)
+        keys.add(pc.cache_meta(s, "/nonexistent/v.mp4", "", 30.0, 600)["key"])
+    assert len(keys) == 3
+    r = Runner()
+    assert _runner_settings(r)["face_model"] == "scrfd_10g_bnkps"
+    # the default SCRFD-10G runner keys like the reference's SessionConfig defaults
+    assert pc.cache_meta(_runner_settings(r), "/x.mp4", "", 30.0, 600)["key"] == \
+        pc.cache_meta(PrescanConfig(), "/x.mp4", "", 30.0, 600)["key"]
+
+
 def test_debug_record_layout_matches_reference(tmp_path):
     from person_capture_amd.postmatch import DEBUG_CFG_FIELDS, DebugLog, debug_record
     lay = json.load(open(os.path.join(G, "debug_record_layout.json")))
