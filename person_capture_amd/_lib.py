@@ -18,6 +18,14 @@ LIB_PATH = Path(os.environ.get("PC_LIB_PATH") or Path(__file__).resolve().parent
 PC_OK = 0
 PC_PREC_F16 = 0
 PC_PREC_F32 = 1
+# host-side mode (not a pc_net_create precision): an f16 net running the f16x3 split program
+# (models.compile_scrfd(split=True)) - f32-class detections on f16 MFMA
+PC_PREC_F16X3 = 2
+
+
+def net_precision(mode: int) -> int:
+    """The pc_net_create precision of a host precision mode."""
+    return PC_PREC_F16 if mode == PC_PREC_F16X3 else mode
 
 _lib = None
 

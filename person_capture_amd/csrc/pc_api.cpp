@@ -32,8 +32,8 @@ int conv_halo_tile(int cfg, int* bc, int* bp);
 int conv_halo_fits(int cfg, int KH, int KW, int W);
 hipError_t conv_t2d_launch(const ConvParams& p, hipStream_t s);
 int conv_t2d_supported(int cin, int npad, int KH, int KW, int stride, int pad, int act, int out_f32, int ycs,
-                       int ycoff);
-int conv_t2d_rows(int cin, int npad);
+                       int ycoff, int split);
+int conv_t2d_rows(int cin, int npad, int split);
 int conv_chain_fits(int H, int W, int C, int npad, long long ktot);
 hipError_t conv_chain_launch(const void* x, int xcs, void* y, int ycs, const void* blk_dev, int nblk, int N, int H,
                              int W, long long ktot, int dbg, hipStream_t s);
@@ -438,12 +438,15 @@ extern "C" int pc_memset(pc_ctx* c, void* d, int v, size_t n) {
 enum { OP_CONV = 1, OP_STEM = 2, OP_MAXPOOL = 3, OP_UPSAMPLE = 4, OP_LAYERNORM = 5, OP_ATTENTION = 6 };
 
 struct NetBuf { long long elems; int is_f32; void* d = nullptr; };
-struct NetTensor { int buf, H, W, C, cs, coff, is_f32; };
+// split: f16x3 tensor (detector precision mode): C physical channels = [hi | lo],
+// C / 2 each; the lo half of a pixel is C / 2 elements after its hi half
+struct NetTensor { int buf, H, W, C, cs, coff, is_f32, split; };
 struct NetOp { int w[32]; };
 struct ConvPlan { int rowb, cfg, splitk, halo = -1, fast = -1, t2d = -1; long long M_per_image; double flops_per_image; };
 // A stem (tiny Cin) runs as im2col + a 1x1 MFMA conv over 32-element K rows.
 struct StemPlan {
   int use_mfma = 0, npad = 0, cfg = 0, rowb = 0, cin_true = 0;
+  int split = 0;            // f16x3 output: w is [npad][64] = W_hi | W_lo (fused stem only)
   void* w = nullptr;        // [npad][32] act dtype
   float* bias = nullptr;    // [npad]
   float* slope = nullptr;   // [npad] or null
@@ -533,11 +536,17 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
   const int out = w[1], nseg = w[2], npad = w[14];
   const int esz = n->f32 ? 4 : 2;
   int rowb = 128;
+  bool any_split = n->tens[out].split != 0 || (w[21] >= 0 && n->tens[w[21]].split);
   for (int s = 0; s < nseg; ++s) {
     const NetTensor& X = n->tens[w[3 + 5 * s]];
-    if ((X.C * esz) % 128) rowb = 64;
-    if ((X.C * esz) % 64) return fail(n->ctx, PC_ERR_FORMAT, "conv input channels not a multiple of the K tile");
+    // a split input's K tile must not straddle its hi and lo halves: the tile divides C / 2
+    const int cl = X.split ? X.C / 2 : X.C;
+    any_split = any_split || X.split;
+    if ((cl * esz) % 128) rowb = 64;
+    if ((cl * esz) % 64) return fail(n->ctx, PC_ERR_FORMAT, "conv input channels not a multiple of the K tile");
     if ((size_t)X.C * esz + 128 > kZeroTail) return fail(n->ctx, PC_ERR_FORMAT, "conv input wider than the zero tail");
+    if (X.split && (n->f32 || X.is_f32 || X.cs != X.C))
+      return fail(n->ctx, PC_ERR_FORMAT, "split tensors are dense f16 [hi | lo] pixels of an f16 net");
   }
   // tile configuration (pc_conv.hip launch_rowb): channel tile BC must divide npad
   static const int cfg_bc[kNumConvCfgs] = {128, 128, 64, 64, 96, 32, 32, 128, 256, 256, 64, 96, 32, 128};
@@ -581,7 +590,7 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
     const char* e = getenv("PC_CONV_HALO");
     // a forced igemm tile (PC_CONV_CFG) without PC_CONV_HALO means "test that tile"
     const int force = e ? atoi(e) : (getenv("PC_CONV_CFG") ? 0 : -1);
-    const bool ok = nseg == 1 && pl.splitk == 1 && st == 1 && KH == KW && pd * 2 + 1 == KH && X.H == Y.H &&
+    const bool ok = !any_split && nseg == 1 && pl.splitk == 1 && st == 1 && KH == KW && pd * 2 + 1 == KH && X.H == Y.H &&
                     X.W == Y.W && KH * KW <= 32 && (double)M * X.cs * esz < 4294967296.0 - 65536.0 && force != 0;
     if (ok) {
       auto htiles = [&](int hc) {
@@ -652,11 +661,17 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
     const char* e = getenv("PC_CONV_T2D");
     const int mode = e ? atoi(e) : ((getenv("PC_CONV_CFG") || getenv("PC_CONV_HALO") || getenv("PC_CONV_FAST")) ? 0 : 1);
     const NetTensor& X = n->tens[w[3]];
-    if (mode > 0 && !n->f32 && nseg == 1 && pl.splitk == 1 && X.H == Y.H && X.W == Y.W &&
-        conv_t2d_supported(X.C, npad, w[4], w[5], w[6], w[7], w[20], Y.is_f32, Y.cs, Y.coff) && w[15] >= 9LL * X.C &&
+    // split (f16x3): split input -> split output (and split residual, if any) only
+    const int sp = X.split ? 1 : 0;
+    const bool split_ok = !sp ? !any_split
+                              : (Y.split && (w[21] < 0 || n->tens[w[21]].split) && Y.C / 2 >= 8 && (Y.C / 2) % 8 == 0);
+    const int cin_l = sp ? X.C / 2 : X.C;
+    if (mode > 0 && !n->f32 && nseg == 1 && pl.splitk == 1 && X.H == Y.H && X.W == Y.W && split_ok &&
+        conv_t2d_supported(cin_l, npad, w[4], w[5], w[6], w[7], w[20], Y.is_f32, Y.cs, Y.coff, sp) &&
+        w[15] >= (sp ? 27LL : 9LL) * cin_l &&
         (double)X.H * X.W * n->max_batch * X.cs * esz + kZeroTail < 4294967296.0 &&
         (double)M < 2147483647.0) {
-      const int th = conv_t2d_rows(X.C, npad);
+      const int th = conv_t2d_rows(cin_l, npad, sp);
       const double cover = (double)Y.H * Y.W / ((double)((Y.H + th - 1) / th * th) * ((Y.W + 15) / 16 * 16));
       if (mode == 2 || cover >= 0.75) {
         pl.t2d = 0;
@@ -671,7 +686,7 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
   // Opt-in (PC_SMALL_SPLITK=1): split-K sums in another order, so a frame's results would
   // depend on the batch it ran in, and extract() / extract_batch() are bit-identical by
   // contract (tests/test_gpu_face_embedder.py::test_extract_single_matches_batch).
-  if (small && pl.splitk == 1 && !n->f32 && getenv("PC_SMALL_SPLITK")) {
+  if (small && pl.splitk == 1 && !n->f32 && !any_split && getenv("PC_SMALL_SPLITK")) {
     const long long t = tiles(cfg);
     const int ktiles = (int)(w[15] * esz / rowb);
     if (t < 192 && ktiles >= 16) {
@@ -685,7 +700,10 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
       }
     }
   }
-  if (Y.C > npad) return fail(n->ctx, PC_ERR_FORMAT, "conv output tensor wider than npad");
+  if ((Y.split ? Y.C / 2 : Y.C) > npad) return fail(n->ctx, PC_ERR_FORMAT, "conv output tensor wider than npad");
+  if (Y.split && (Y.is_f32 || Y.cs != Y.C || (Y.C / 2) % 8))
+    return fail(n->ctx, PC_ERR_FORMAT, "split conv output must be a dense f16 [hi | lo] tensor");
+  if (pl.splitk > 1 && any_split) return fail(n->ctx, PC_ERR_FORMAT, "split-K over split tensors");
   return PC_OK;
 }
 
@@ -696,11 +714,14 @@ static int plan_stem(pc_net* n, const NetOp& op, StemPlan& st, size_t& col_bytes
   const int KH = w[3], KW = w[4], cout = w[8], cin_true = w[13] > 0 ? w[13] : 3;
   const NetTensor& X = n->tens[w[2]];
   const NetTensor& Y = n->tens[w[1]];
-  if (getenv("PC_STEM_DIRECT") || KH * KW * cin_true > 32 || X.C != 4) return PC_OK;   // direct kernel
+  if (Y.split && (n->f32 || KH * KW * cin_true > 32 || X.C != 4 || Y.is_f32))
+    return fail(n->ctx, PC_ERR_FORMAT, "split stem output needs the fused f16 stem");
+  if (!Y.split && (getenv("PC_STEM_DIRECT") || KH * KW * cin_true > 32 || X.C != 4)) return PC_OK;   // direct kernel
   const int esz = n->f32 ? 4 : 2;
   st.use_mfma = 1;
   st.cin_true = cin_true;
-  st.npad = (std::max(cout, Y.C) + 31) / 32 * 32;
+  st.split = Y.split;
+  st.npad = (std::max(cout, Y.split ? Y.C / 2 : Y.C) + 31) / 32 * 32;
   st.rowb = 32 * esz;   // one K-tile of exactly 32 elements
   const long long M = (long long)Y.H * Y.W * n->max_batch;
   st.cfg = st.npad % 128 == 0 ? 7 : (st.npad % 64 == 0 ? 10 : 12);
@@ -716,6 +737,18 @@ static int plan_stem(pc_net* n, const NetOp& op, StemPlan& st, size_t& col_bytes
     const float* hs = reinterpret_cast<const float*>(n->host_arrays[w[10]]);
     for (int co = 0; co < cout; ++co) sl[co] = hs[co];
   }
+  if (st.split) {   // rows of 64: K 0-31 W_hi, 32-63 W_lo = f16(W - W_hi)
+    std::vector<_Float16> h((size_t)st.npad * 64);
+    for (int co = 0; co < st.npad; ++co)
+      for (int k = 0; k < 32; ++k) {
+        const float v = wf[(size_t)co * 32 + k];
+        const _Float16 hi = (_Float16)v;
+        h[(size_t)co * 64 + k] = hi;
+        h[(size_t)co * 64 + 32 + k] = (_Float16)(v - (float)hi);
+      }
+    HIPCHK(n->ctx, hipMalloc(&st.w, h.size() * 2));
+    HIPCHK(n->ctx, hipMemcpy(st.w, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+  } else {
   HIPCHK(n->ctx, hipMalloc(&st.w, wf.size() * esz));
   if (n->f32) {
     HIPCHK(n->ctx, hipMemcpy(st.w, wf.data(), wf.size() * 4, hipMemcpyHostToDevice));
@@ -723,6 +756,7 @@ static int plan_stem(pc_net* n, const NetOp& op, StemPlan& st, size_t& col_bytes
     std::vector<_Float16> h(wf.size());
     for (size_t k = 0; k < wf.size(); ++k) h[k] = (_Float16)wf[k];
     HIPCHK(n->ctx, hipMemcpy(st.w, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+  }
   }
   HIPCHK(n->ctx, hipMalloc((void**)&st.bias, st.npad * 4));
   HIPCHK(n->ctx, hipMemcpy(st.bias, b.data(), st.npad * 4, hipMemcpyHostToDevice));
@@ -872,7 +906,7 @@ extern "C" int pc_net_create(pc_ctx* c, const void* prog, size_t nbytes, int pre
     n->bufs.push_back(b);
   }
   for (int i = 0; i < nten; ++i, pos += 8) {
-    NetTensor t{P[pos], P[pos + 1], P[pos + 2], P[pos + 3], P[pos + 4], P[pos + 5], P[pos + 6]};
+    NetTensor t{P[pos], P[pos + 1], P[pos + 2], P[pos + 3], P[pos + 4], P[pos + 5], P[pos + 6], P[pos + 7] & 1};
     n->tens.push_back(t);
   }
   std::vector<std::pair<long long, long long>> arr;
@@ -889,6 +923,24 @@ extern "C" int pc_net_create(pc_ctx* c, const void* prog, size_t nbytes, int pre
   }
   const float* data = (const float*)(P + pos);
   const size_t ndata = nw - pos;
+  // f16x3 split tensors: f16 nets only; only convs, the fused stem and the max
+  // pool read or write them
+  for (auto& t : n->tens)
+    if (t.split && (n->f32 || t.is_f32 || t.buf < 0 || t.C % 16 || t.cs != t.C)) {
+      delete n;
+      return fail(c, PC_ERR_FORMAT, "split tensor: f16 net, dense [hi | lo] activation buffer");
+    }
+  for (auto& op : n->ops) {
+    const int k = op.w[0];
+    auto bad = [&](int t) { return t >= 0 && t < (int)n->tens.size() && n->tens[t].split; };
+    if ((k == OP_MAXPOOL && (n->tens[op.w[1]].split != n->tens[op.w[2]].split ||
+                             (n->tens[op.w[2]].split && n->tens[op.w[1]].C != n->tens[op.w[2]].C))) ||
+        ((k == OP_UPSAMPLE || k == OP_LAYERNORM || k == OP_ATTENTION) && (bad(op.w[1]) || bad(op.w[2]))) ||
+        (k == OP_STEM && bad(op.w[2]))) {
+      delete n;
+      return fail(c, PC_ERR_FORMAT, "op cannot read or write split tensors");
+    }
+  }
   // which arrays are conv weights (uploaded in the activation dtype)
   std::vector<int> is_w(narr, 0);
   for (auto& op : n->ops)
@@ -1108,6 +1160,10 @@ static int run_ops(pc_net* n, int N) {
         S.H = X.H; S.W = X.W; S.C = X.C; S.cs = X.cs;
         S.KH = w[4 + 5 * sg]; S.KW = w[5 + 5 * sg]; S.stride = w[6 + 5 * sg]; S.pad = w[7 + 5 * sg];
         S.cblk = X.C / bke;
+        if (X.split) {   // virtual channel blocks [hi, lo, hi] (pc_common.h ConvSeg::vwrap)
+          S.vwrap = S.cblk;
+          S.cblk = S.cblk / 2 * 3;
+        }
         S.kt = S.KH * S.KW * S.cblk;
         kt += S.kt;
       }
@@ -1116,7 +1172,8 @@ static int run_ops(pc_net* n, int N) {
       p.N = N; p.OH = Y.H; p.OW = Y.W; p.M = N * Y.H * Y.W;
       p.npad = w[14];
       p.cout = w[16];
-      p.cwrite = std::min(Y.C, p.npad);
+      p.cwrite = std::min(Y.split ? Y.C / 2 : Y.C, p.npad);
+      p.ysplit = Y.split ? Y.C / 2 : 0;
       p.y = tensor_ptr(n, w[1]);
       p.ycs = Y.cs;
       p.out_f32 = Y.is_f32 && !n->f32 ? 1 : (n->f32 ? 1 : 0);
@@ -1129,6 +1186,7 @@ static int run_ops(pc_net* n, int N) {
       if (w[21] >= 0) {
         const NetTensor& R = n->tens[w[21]];
         p.rcs = R.cs; p.rH = R.H; p.rW = R.W;
+        p.rsplit = R.split ? R.C / 2 : 0;
       }
       p.act_after_res = w[23];
       p.kt_total = kt;
@@ -1165,13 +1223,15 @@ static int run_ops(pc_net* n, int N) {
       p.cpad = w[12];
       p.y = tensor_ptr(n, w[1]);
       const StemPlan& st = n->stems[i];
-      const int st_cwrite = std::min(Y.C, st.npad);
+      const int st_cwrite = std::min(Y.split ? Y.C / 2 : Y.C, st.npad);
+      p.ysplit = Y.split ? Y.C / 2 : 0;
       // fused gather + MFMA stem (pc_stem.hip) unless PC_STEM_UNFUSED is set
       // (stem_fused stores f16: an f32 output tensor inside an f16 net takes the unfused path)
       const bool fused = st.use_mfma && !getenv("PC_STEM_UNFUSED") && !Y.is_f32 &&
                          stem_fused_ok(n->f32, X.C, st.cin_true, p.KH, p.KW, st.npad, st_cwrite, Y.cs, Y.coff) &&
                          X.cs % 4 == 0 && (reinterpret_cast<uintptr_t>(p.x) & 7) == 0 &&
                          (reinterpret_cast<uintptr_t>(p.y) & 15) == 0;
+      if (st.split && !fused) return fail(c, PC_ERR_FORMAT, "split stem: the fused kernel cannot run this op");
       if (fused) {
         rec.kind = OP_CONV;
         rec.flops = n->plans[i].flops_per_image * N;
@@ -1216,6 +1276,8 @@ static int run_ops(pc_net* n, int N) {
       p.x = tensor_ptr(n, w[2]); p.N = N; p.H = X.H; p.W = X.W; p.C = X.C; p.xcs = X.cs;
       p.y = tensor_ptr(n, w[1]); p.OH = Y.H; p.OW = Y.W; p.ycs = Y.cs;
       p.k = w[3]; p.stride = w[4]; p.pad = w[5];
+      p.split = X.split;
+      if (X.split) p.C = X.C / 2;   // the hi half; lo at +C (create checked Y.split == X.split)
       HIPCHK(c, maxpool_launch(n->f32, p, s));
     } else if (w[0] == OP_UPSAMPLE) {
       UpsampleParams p;

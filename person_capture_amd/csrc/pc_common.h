@@ -26,6 +26,11 @@ struct ConvSeg {
   int kt;              // K tiles in this segment = KH*KW*(C/BKE)
   int cblk;            // C / BKE
   unsigned zero_off;   // bytes from x to >= 256 zero bytes (padding taps read there)
+  // f16x3 split tensors (x = hi + lo, stored [hi | lo] per pixel): the K loop walks the
+  // virtual channel blocks [hi, lo, hi] against weights [W_hi, W_hi, W_lo] of each tap, so
+  // x_hi*W_hi + x_lo*W_hi + x_hi*W_lo accumulate in f32. cblk counts the
+  // virtual blocks; a virtual block >= vwrap reads physical block (block - vwrap). 0: plain.
+  int vwrap;
 };
 
 struct ConvParams {
@@ -52,6 +57,10 @@ struct ConvParams {
   int kt_total;
   const void* zero;    // >= 256 zero bytes (padding taps read from here)
   int dbg;             // tuning experiments only (PC_CONV_DBG): 1 no staging, 2 no MFMA, 4 one-image footprint
+  // f16x3 split output / residual: the lo half sits this many elements after the hi half
+  // of each pixel (0: plain tensor). Output: hi = f16(v), lo = f16(v - hi); residual: hi + lo.
+  int ysplit;
+  int rsplit;
 };
 
 // Direct convolution for tiny input channel counts (network stems, Cin <= 4).
@@ -66,12 +75,14 @@ struct StemParams {
   int cout, ycs;       // valid output channels, output pixel stride
   void* y;
   int cpad;            // channels written (>= cout, the tail is zero-filled)
+  int ysplit;          // f16x3 split output: lo half at +ysplit elements (0: plain)
 };
 
 struct PoolParams {
   const void* x; int N, H, W, C, xcs;
   void* y; int OH, OW, ycs;
   int k, stride, pad;
+  int split;           // f16x3 split tensors: C is the hi half, the lo half follows at +C
 };
 
 }  // namespace pc

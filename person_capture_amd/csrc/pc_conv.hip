@@ -85,14 +85,14 @@ __global__ __launch_bounds__(64 * WC * WP, 1) void conv_igemm(ConvParams p) {
   __amdgpu_buffer_rsrc_t xrs;
   const __amdgpu_buffer_rsrc_t wrs =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.w), (short)0, (int)0xffffffff, 0x00020000);
-  int sH, sW, scs, sKH, sKW, sstr, spad, scblk;
+  int sH, sW, scs, sKH, sKW, sstr, spad, scblk, svwrap;
   unsigned szero;
   auto load_seg = [&](const ConvSeg& S) __attribute__((always_inline)) {
     sx = reinterpret_cast<const char*>(S.x);
     xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(S.x), (short)0, (int)0xffffffff, 0x00020000);
     sH = S.H; sW = S.W; scs = S.cs;
     sKH = S.KH; sKW = S.KW; sstr = S.stride; spad = S.pad;
-    scblk = S.cblk; szero = S.zero_off;
+    scblk = S.cblk; szero = S.zero_off; svwrap = S.vwrap;
   };
   if (seg) load_seg(p.seg[1]);
   else load_seg(p.seg[0]);
@@ -161,7 +161,8 @@ __global__ __launch_bounds__(64 * WC * WP, 1) void conv_igemm(ConvParams p) {
 
   auto stage = [&](auto bufc, int ktl) __attribute__((always_inline)) {
     constexpr int buf = decltype(bufc)::value;
-    const int xso = cb * (BKE * ESZ), wso = ktl * (BKE * ESZ);
+    // f16x3 split input: virtual channel blocks [hi, lo, hi] read physical [hi, lo]
+    const int xso = (svwrap && cb >= svwrap ? cb - svwrap : cb) * (BKE * ESZ), wso = ktl * (BKE * ESZ);
     static_for<NI>([&](auto ic) __attribute__((always_inline)) {
       constexpr int i = decltype(ic)::value;
       const int g = i * NW + wave;
@@ -531,6 +532,45 @@ __global__ void maxpool_nhwc_f16x8(PoolParams p) {
   *reinterpret_cast<f16x8*>(reinterpret_cast<f16*>(p.y) + (size_t)pix * p.ycs + g * 8) = h;
 }
 
+// f16x3 split NHWC max pool: channels [0, C) hold hi, [C, 2C) lo of the same values. The max
+// runs over the exact f32 values hi + lo (PyTorch's f32 max pool of the f32 activations),
+// and the maximum is written back split (hi = f16(m), lo = f16(m - hi): m again exactly).
+__global__ void maxpool_split_f16x8(PoolParams p) {
+  const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned cg = (unsigned)p.C >> 3;
+  const unsigned hw = (unsigned)(p.OH * p.OW);
+  if (i >= (unsigned)p.N * hw * cg) return;
+  const unsigned pix = i / cg, g = i - pix * cg;
+  const unsigned n = pix / hw, rem = pix - n * hw;
+  const int oh = (int)(rem / (unsigned)p.OW), ow = (int)(rem - (unsigned)oh * (unsigned)p.OW);
+  float m[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) m[j] = -INFINITY;
+  const f16* xb = reinterpret_cast<const f16*>(p.x) + g * 8;
+  for (int kh = 0; kh < p.k; ++kh) {
+    const int ih = oh * p.stride - p.pad + kh;
+    if ((unsigned)ih >= (unsigned)p.H) continue;
+    for (int kw = 0; kw < p.k; ++kw) {
+      const int iw = ow * p.stride - p.pad + kw;
+      if ((unsigned)iw >= (unsigned)p.W) continue;
+      const f16* px = xb + ((size_t)(n * p.H + ih) * p.W + iw) * p.xcs;
+      const f16x8 h = *reinterpret_cast<const f16x8*>(px);
+      const f16x8 l = *reinterpret_cast<const f16x8*>(px + p.C);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], (float)h[j] + (float)l[j]);
+    }
+  }
+  f16x8 h, l;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    h[j] = (f16)m[j];
+    l[j] = (f16)(m[j] - (float)h[j]);
+  }
+  f16* yp = reinterpret_cast<f16*>(p.y) + (size_t)pix * p.ycs + g * 8;
+  *reinterpret_cast<f16x8*>(yp) = h;
+  *reinterpret_cast<f16x8*>(yp + p.C) = l;
+}
+
 // ---------------------------------------------------------------------------
 // host-side launchers
 // ---------------------------------------------------------------------------
@@ -616,6 +656,13 @@ hipError_t maxpool_launch(int f32, const PoolParams& p, hipStream_t s) {
   const long long total = (long long)p.N * p.OH * p.OW * (p.C / 4);
   dim3 grid((unsigned)((total + 255) / 256));
   const bool al16 = (((uintptr_t)p.x | (uintptr_t)p.y) & 15) == 0;
+  if (p.split) {
+    if (f32 || !al16 || p.C % 8 || p.xcs % 8 || p.ycs % 8 || total / 2 >= 2147483647LL ||
+        (long long)p.N * p.H * p.W >= 2147483647LL)
+      return hipErrorInvalidValue;
+    hipLaunchKernelGGL(maxpool_split_f16x8, dim3((unsigned)((total / 2 + 255) / 256)), dim3(256), 0, s, p);
+    return hipGetLastError();
+  }
   if (!f32 && al16 && p.C % 8 == 0 && p.xcs % 8 == 0 && p.ycs % 8 == 0 && total / 2 < 2147483647LL &&
       (long long)p.N * p.H * p.W < 2147483647LL) {
     hipLaunchKernelGGL(maxpool_nhwc_f16x8, dim3((unsigned)((total / 2 + 255) / 256)), dim3(256), 0, s, p);

@@ -170,6 +170,12 @@ __device__ __forceinline__ void conv_epilogue_map(const ConvParams& p, f32x4 (&a
       if (p.res_mode != RES_NONE) {
         float r[4] = {0.f, 0.f, 0.f, 0.f};
         load4<T>(reinterpret_cast<const T*>(p.res) + rpix * p.rcs + ch, r, nv);
+        if (p.rsplit) {   // f16x3 residual: hi + lo (exact in f32)
+          float r2[4] = {0.f, 0.f, 0.f, 0.f};
+          load4<T>(reinterpret_cast<const T*>(p.res) + rpix * p.rcs + p.rsplit + ch, r2, nv);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) r[j] += r2[j];
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] += r[j];
       }
@@ -180,10 +186,18 @@ __device__ __forceinline__ void conv_epilogue_map(const ConvParams& p, f32x4 (&a
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         if (ch + j >= p.cout) v[j] = 0.f;  // keep channel padding exactly zero
-      if (p.out_f32)
+      if (p.out_f32) {
         store4<float>(reinterpret_cast<float*>(p.y) + (long long)pix * p.ycs + ch, v, nv);
-      else
-        store4<T>(reinterpret_cast<T*>(p.y) + (long long)pix * p.ycs + ch, v, nv);
+      } else {
+        T* yp = reinterpret_cast<T*>(p.y) + (long long)pix * p.ycs + ch;
+        store4<T>(yp, v, nv);
+        if (p.ysplit) {   // f16x3 output: lo = f16(v - f16(v))
+          float lo[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) lo[j] = v[j] - (float)(T)v[j];
+          store4<T>(yp + p.ysplit, lo, nv);
+        }
+      }
     });
   });
 }
@@ -204,7 +218,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, f32x4 (&acc)[
 // - bias (per channel or border class), activation, residual, zeroed channel
 // padding - and stores them with one 16-byte (f16) or two (f32) stores, so each
 // pixel row of the tile leaves as contiguous bytes and no load waits behind a store.
-template <typename T, int BC, int BP, int WC, int WP, int EPI_MAX = 131072, int RGMAX = 8>
+template <typename T, int BC, int BP, int WC, int WP, int EPI_MAX = 131072, int RGMAX = 8, bool SPLIT = false>
 __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, f32x4 (&acc)[BC / WC / 16][BP / WP / 16],
                                                   int c0, int p0, int wr, int wc, int lane, char* smem) {
   constexpr int NW = WC * WP, NT = 64 * NW;
@@ -222,6 +236,7 @@ __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, f32x4 (&a
   constexpr int ESZ = sizeof(T);
   const int oesz = p.out_f32 ? 4 : ESZ;
   const bool vec_ok = ((reinterpret_cast<uintptr_t>(p.y) | (uintptr_t)(p.ycs * oesz)) & 15) == 0 &&
+                      ((p.ysplit | p.rsplit) & 7) == 0 &&
                       (p.res_mode == RES_NONE ||
                        ((reinterpret_cast<uintptr_t>(p.res) | (uintptr_t)(p.rcs * ESZ)) & 15) == 0);
   const int hw = p.OH * p.OW;
@@ -305,12 +320,13 @@ __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, f32x4 (&a
       // (most of its ~11 us epilogue)
       constexpr int RG0 = (NPASS == 2 ? 2 : 4) < IT ? (NPASS == 2 ? 2 : 4) : IT;
       // (f16 tiles below 256x256 only: the f32 and the largest f16 instantiations spill with it)
-      constexpr int RGM = (ESZ == 2 && BC * BP < 65536) ? RGMAX : 0;
+      constexpr int RGM = (ESZ == 2 && BC * BP < 65536) ? (SPLIT ? RGMAX / 2 : RGMAX) : 0;
       constexpr int RG = IT <= RGM ? IT : (IT % RG0 == 0 ? RG0 : (IT % 2 == 0 ? 2 : 1));
       static_assert(IT % RG == 0, "residual groups");
 #pragma unroll 1
       for (int kg = 0; kg < IT; kg += RG) {
       RV rv[RG][RN];
+      RV rv2[SPLIT ? RG : 1][RN];   // f16x3: the residual's lo half
       if (p.res_mode != RES_NONE) {
 #pragma unroll
         for (int kk = 0; kk < RG; ++kk) {
@@ -318,6 +334,10 @@ __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, f32x4 (&a
           const int pix = p0 + pbase + pl0 + (kg + kk) * PSTEP;
 #pragma unroll
           for (int j = 0; j < RN; ++j) rv[k][j] = RV{};
+          if constexpr (SPLIT) {
+#pragma unroll
+            for (int j = 0; j < RN; ++j) rv2[k][j] = RV{};
+          }
           if (pix < p.M && full) {
             long long rpix = pix;
             if (p.res_mode == RES_UP2) {
@@ -328,6 +348,12 @@ __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, f32x4 (&a
             const T* rp = reinterpret_cast<const T*>(p.res) + rpix * p.rcs + ch;
 #pragma unroll
             for (int j = 0; j < RN; ++j) rv[k][j] = *reinterpret_cast<const RV*>(rp + j * (8 / RN));
+            if constexpr (SPLIT) {
+              if (p.rsplit) {
+#pragma unroll
+                for (int j = 0; j < RN; ++j) rv2[k][j] = *reinterpret_cast<const RV*>(rp + p.rsplit + j * (8 / RN));
+              }
+            }
           }
         }
       }
@@ -364,8 +390,13 @@ __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, f32x4 (&a
         if (has_res && !pre_act) {   // act(acc + bias + residual): residual first
           if (full) {
             if constexpr (ESZ == 2) {
+              if constexpr (SPLIT) {   // hi + lo first: the f32 value of the split residual
 #pragma unroll
-              for (int j = 0; j < 8; ++j) v[j] += (float)rv[k][0][j];
+                for (int j = 0; j < 8; ++j) v[j] += (float)rv[k][0][j] + (float)rv2[k][0][j];
+              } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] += (float)rv[k][0][j];
+              }
             } else {
 #pragma unroll
               for (int j = 0; j < 4; ++j) { v[j] += rv[k][0][j]; v[4 + j] += rv[k][1][j]; }
@@ -374,15 +405,20 @@ __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, f32x4 (&a
             long long rpix = pix;
             if (p.res_mode == RES_UP2) rpix = ((long long)n * p.rH + (oh >> 1)) * p.rW + (ow >> 1);
             const T* rp = reinterpret_cast<const T*>(p.res) + rpix * p.rcs + ch;
-            for (int j = 0; j < nv; ++j) v[j] += (float)rp[j];
+            for (int j = 0; j < nv; ++j) v[j] += SPLIT && p.rsplit ? (float)rp[j] + (float)rp[p.rsplit + j] : (float)rp[j];
           }
         }
         act8(v);   // the one activation point
         if (has_res && pre_act) {
           if (full) {
             if constexpr (ESZ == 2) {
+              if constexpr (SPLIT) {   // hi + lo first: the f32 value of the split residual
 #pragma unroll
-              for (int j = 0; j < 8; ++j) v[j] += (float)rv[k][0][j];
+                for (int j = 0; j < 8; ++j) v[j] += (float)rv[k][0][j] + (float)rv2[k][0][j];
+              } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] += (float)rv[k][0][j];
+              }
             } else {
 #pragma unroll
               for (int j = 0; j < 4; ++j) { v[j] += rv[k][0][j]; v[4 + j] += rv[k][1][j]; }
@@ -391,7 +427,7 @@ __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, f32x4 (&a
             long long rpix = pix;
             if (p.res_mode == RES_UP2) rpix = ((long long)n * p.rH + (oh >> 1)) * p.rW + (ow >> 1);
             const T* rp = reinterpret_cast<const T*>(p.res) + rpix * p.rcs + ch;
-            for (int j = 0; j < nv; ++j) v[j] += (float)rp[j];
+            for (int j = 0; j < nv; ++j) v[j] += SPLIT && p.rsplit ? (float)rp[j] + (float)rp[p.rsplit + j] : (float)rp[j];
           }
         }
 #pragma unroll
@@ -408,11 +444,23 @@ __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, f32x4 (&a
         } else {
           T* yp = reinterpret_cast<T*>(p.y) + (long long)pix * p.ycs + ch;
           if constexpr (ESZ == 2) {
+            const f16x8 h = f16x8{(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3], (f16)v[4], (f16)v[5], (f16)v[6], (f16)v[7]};
             if (full) {
-              *reinterpret_cast<f16x8*>(yp) = f16x8{(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3],
-                                                    (f16)v[4], (f16)v[5], (f16)v[6], (f16)v[7]};
+              *reinterpret_cast<f16x8*>(yp) = h;
             } else {
-              for (int j = 0; j < nv; ++j) yp[j] = (T)v[j];
+              for (int j = 0; j < nv; ++j) yp[j] = h[j];
+            }
+            if constexpr (SPLIT) {
+              if (p.ysplit) {   // f16x3 output: lo = f16(v - f16(v))
+                f16x8 l;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) l[j] = (f16)(v[j] - (float)h[j]);
+                if (full) {
+                  *reinterpret_cast<f16x8*>(yp + p.ysplit) = l;
+                } else {
+                  for (int j = 0; j < nv; ++j) yp[p.ysplit + j] = l[j];
+                }
+              }
             }
           } else {
             if (full) {

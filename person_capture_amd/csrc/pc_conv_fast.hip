@@ -35,7 +35,8 @@ __host__ __device__ constexpr int fast_epi_bytes() {
 
 // OCC: workgroups per CU the tile is sized for (LDS <= 160 KiB / OCC); with OCC = 2 one
 // workgroup's epilogue and DMA waits overlap the other's MFMAs.
-template <typename T, int BC, int BP, int ROWB, int WC, int WP, int NSTAGE, int OCC = 1>
+// SPLIT: the f16x3 epilogue (split output / residual)
+template <typename T, int BC, int BP, int ROWB, int WC, int WP, int NSTAGE, int OCC = 1, bool SPLIT = false>
 __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fast(ConvParams p) {
   constexpr int NW = WC * WP;
   constexpr int ESZ = sizeof(T);
@@ -87,7 +88,7 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
   unsigned b_zero;   // zero tail + a chunk offset (any 16 zero bytes do; the tail is wider than a row)
   // current issue segment (scalars)
   const char* sx;
-  int sH, sW, scs, sKW, scblk;
+  int sH, sW, scs, sKW, scblk, svwrap;
   // buffer resources over the whole 32-bit offset range (every offset is < 4 GiB by the
   // planner's 32-bit offset rule, so the range check never fires)
   auto rsrc = [&](const void* base) __attribute__((always_inline)) {
@@ -97,7 +98,7 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
   auto load_seg = [&](const ConvSeg& S) __attribute__((always_inline)) {
     sx = reinterpret_cast<const char*>(S.x);
     xrs = rsrc(sx);
-    sH = S.H; sW = S.W; scs = S.cs; sKW = S.KW; scblk = S.cblk;
+    sH = S.H; sW = S.W; scs = S.cs; sKW = S.KW; scblk = S.cblk; svwrap = S.vwrap;
     const int hw = p.OH * p.OW;
     static_for<NIB>([&](auto ic) __attribute__((always_inline)) {
       constexpr int i = decltype(ic)::value;
@@ -132,7 +133,8 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
       __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_ptr_t)(smem + slot * BUF + (i * NW + wave) * 1024), 16, off,
                                                wso, 0, 0);
     });
-    const int xso = icb * ROWB;
+    // f16x3 split input: virtual blocks [hi, lo, hi] -> physical [hi, lo] (a scalar select)
+    const int xso = (svwrap && icb >= svwrap ? icb - svwrap : icb) * ROWB;
     const unsigned tapoff = (unsigned)((ith * sW + itw) * scs * ESZ);
     static_for<NIB>([&](auto ic) __attribute__((always_inline)) {
       constexpr int i = decltype(ic)::value;
@@ -281,7 +283,7 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
   __syncthreads();
   if (p.dbg & 4) return;   // tuning only: skip the epilogue
   if constexpr (((BC / 8) & (BC / 8 - 1)) == 0 && ((BC / 16) & (BC / 16 - 1)) == 0)
-    conv_epilogue_lds<T, BC, BP, WC, WP, EPI_MAX>(p, acc, c0, p0, wr, wc, lane, smem);
+    conv_epilogue_lds<T, BC, BP, WC, WP, EPI_MAX, 8, SPLIT>(p, acc, c0, p0, wr, wc, lane, smem);
   else   // 96 / 224 channel tiles: per-fragment stores
     conv_epilogue<T, TC, TP, WTC, WTP>(p, acc, c0, p0, wr, wc, lane, 0);
 }
@@ -330,6 +332,16 @@ static hipError_t launch_fast_cfg(const ConvParams& p, hipStream_t s) {
     return hipErrorInvalidValue;
   } else {
     const int nwg = (p.M + BP - 1) / BP * (p.npad / BC);
+    // the split epilogue only where it can differ: f16 power-of-two channel tiles (the others
+    // take the per-fragment epilogue, which reads the split flags at run time)
+    constexpr bool LDS_EPI = ((BC / 8) & (BC / 8 - 1)) == 0 && ((BC / 16) & (BC / 16 - 1)) == 0;
+    if constexpr (sizeof(T) == 2 && LDS_EPI) {
+      if (p.ysplit || p.rsplit) {
+        hipLaunchKernelGGL((conv_fast<T, BC, BP, ROWB, WC, WP, NSTAGE, OCC, true>), dim3(nwg), dim3(64 * WC * WP), 0,
+                           s, p);
+        return hipGetLastError();
+      }
+    }
     hipLaunchKernelGGL((conv_fast<T, BC, BP, ROWB, WC, WP, NSTAGE, OCC>), dim3(nwg), dim3(64 * WC * WP), 0, s, p);
     return hipGetLastError();
   }

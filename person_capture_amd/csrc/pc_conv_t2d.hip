@@ -41,24 +41,32 @@ __device__ __forceinline__ void t2d_read_frags(const char* a0, f16x8* fb, std::i
 // NW waves, each owning TP output rows of 16 pixels x 32 output channels.
 // NBUF 3: three halo buffers, block i+2's halo is requested while block i is multiplied (the
 // DMA of one block of small TH does not hide behind one block's K loop).
-template <int NCH, int G, int NW, int TP, int NBUF = 2>
+// SPLIT (f16x3 detector): the input is a split tensor [hi | lo] (NCH physical
+// chunks = 2 x the logical ones), each tap walks the virtual chunks [hi, lo, hi] against the
+// weights [W_hi, W_hi, W_lo] held in registers (3/2 x the K steps of the physical halo), the
+// residual is read as hi + lo and the output is written split.
+template <int NCH, int G, int NW, int TP, int NBUF = 2, bool SPLIT = false>
 __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, int ntx, int ntiles) {
   constexpr int TW = 16, P = 24, TC = 2;
   constexpr int TH = TP * NW / G;             // output rows per block
   constexpr int NRP = (TH + 2) * P;           // halo rows per channel chunk
   constexpr int NINST = NRP / 16;             // DMA instructions per chunk
   constexpr int BUFB = NCH * NRP * 64;        // one halo buffer
-  constexpr int NKS = 9 * NCH;                // 32-element K steps
+  static_assert(!SPLIT || NCH % 2 == 0, "split halo: hi and lo chunks");
+  constexpr int NV = SPLIT ? NCH / 2 * 3 : NCH;   // virtual 32-channel chunks per tap
+  constexpr int NKS = 9 * NV;                 // 32-element K steps
   constexpr int NPAD_T = 32 * G;
   constexpr int TB = 10 * NPAD_T;             // bias classes [9][npad] + slopes [npad] (f32)
   static_assert(NRP % 16 == 0 && P % 8 == 0 && P >= TW + 2 && (TP == 4 || TP == 8), "halo geometry");
   // output staging: its own LDS area, or (when the two halo buffers leave no room) the block's
   // own halo buffer, free once every wave is past the K loop's closing barrier
   static_assert(NBUF == 2 || NBUF == 3, "halo buffers");
-  constexpr bool ALIAS = NBUF * BUFB + TB * 4 + TH * 16 * (64 * G + 16) > 163840;
+  constexpr int NS = SPLIT ? 2 : 1;           // halves per staged output pixel (hi, lo)
+  constexpr int STGB = TH * 16 * (NS * 64 * G + 16);
+  constexpr bool ALIAS = NBUF * BUFB + TB * 4 + STGB > 163840;
   static_assert(NBUF == 2 || !ALIAS, "three halo buffers need their own staging area");
-  static_assert(NBUF * BUFB + TB * 4 + (ALIAS ? 0 : TH * 16 * (64 * G + 16)) <= 163840, "LDS");
-  static_assert(!ALIAS || TH * 16 * (64 * G + 16) <= BUFB, "staging in a halo buffer");
+  static_assert(NBUF * BUFB + TB * 4 + (ALIAS ? 0 : STGB) <= 163840, "LDS");
+  static_assert(!ALIAS || STGB <= BUFB, "staging in a halo buffer");
   static_assert(NW % G == 0, "wave roles");
 
   // two halo buffers as two objects: the compiler then sees that a ds_read of one
@@ -69,9 +77,9 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, in
   __shared__ __attribute__((aligned(16))) float tab[TB];
   // output staging: [pixel][npad] f16 rows, pitch padded by 16 B (conflict-free 8-byte
   // fragment writes, 16-byte aligned row reads)
-  constexpr int NPAD = 32 * G, PITCH = NPAD * 2 + 16, BPIX = TH * TW, CH8 = NPAD / 8;
-  constexpr int SIT = BPIX * CH8 / (64 * NW);   // 16-byte chunks per thread per block
-  static_assert(SIT * 64 * NW == BPIX * CH8, "staging split");
+  constexpr int NPAD = 32 * G, PITCH = NS * NPAD * 2 + 16, BPIX = TH * TW, CH8 = NPAD / 8;
+  constexpr int SIT = BPIX * NS * CH8 / (64 * NW);   // 16-byte chunks per thread per block
+  static_assert(SIT * 64 * NW == BPIX * NS * CH8, "staging split");
   __shared__ __attribute__((aligned(16))) char stg_own[ALIAS ? 16 : BPIX * PITCH];
 
   const int lane = threadIdx.x & 63;
@@ -206,6 +214,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, in
     // (not zero-filled when unused: writing registers that a load of the previous block
     // targeted would make the compiler drain vmcnt - the next halo - right here)
     f16x4 rv[TP][TC];
+    f16x4 rl[SPLIT ? TP : 1][TC];   // the residual's lo half (split)
     // (addresses of pixels outside the image are clamped, not branched around: a load
     // under a divergent branch merges into a phi that waits for it right there)
     // Row part of the address is wave-uniform (scalar math, 64-bit), the lane part a 24-bit
@@ -226,7 +235,10 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, in
 #pragma unroll
         for (int a = 0; a < TC; ++a) {
           const int ch = g * 32 + a * 16 + chq;
-          if ((p.cwrite & 3) == 0) {   // uniform: whole 4-channel groups
+          if constexpr (SPLIT) {   // planner: whole 8-channel groups
+            rv[t][a] = *reinterpret_cast<const f16x4*>(rp + min(ch, p.cwrite - 4));
+            rl[t][a] = *reinterpret_cast<const f16x4*>(rp + p.rsplit + min(ch, p.cwrite - 4));
+          } else if ((p.cwrite & 3) == 0) {   // uniform: whole 4-channel groups
             rv[t][a] = *reinterpret_cast<const f16x4*>(rp + min(ch, p.cwrite - 4));
           } else {
             rv[t][a] = f16x4{};
@@ -262,14 +274,15 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, in
       f16x8(&cur_f)[TP] = (ks & 1) ? fb1 : fb0;
       f16x8(&nxt_f)[TP] = (ks & 1) ? fb0 : fb1;
       constexpr int H1 = TP > 4 ? 4 : TP;   // reads issued before the wait
+      // virtual chunk jv of the tap -> physical halo chunk j (split: [hi, lo, hi] over [hi, lo])
       if constexpr (ks + 1 < NKS) {
-        constexpr int tap = (ks + 1) / NCH, j = (ks + 1) - tap * NCH;
+        constexpr int tap = (ks + 1) / NV, jv = (ks + 1) - tap * NV, j = jv < NCH ? jv : jv - NCH;
         constexpr int th = tap / 3, tw = tap - th * 3;
         t2d_read_frags<P * 64, j * NRP * 64 + th * P * 64>(cur + ad[tw], nxt_f,
                                                           std::make_integer_sequence<int, H1>{});
       }
       if constexpr (ks + 1 < NKS && TP > H1) {
-        constexpr int tap = (ks + 1) / NCH, j = (ks + 1) - tap * NCH;
+        constexpr int tap = (ks + 1) / NV, jv = (ks + 1) - tap * NV, j = jv < NCH ? jv : jv - NCH;
         constexpr int th = tap / 3, tw = tap - th * 3;
         t2d_read_frags<P * 64, j * NRP * 64 + th * P * 64 + H1 * P * 64>(cur + ad[tw], nxt_f + H1,
                                                                        std::make_integer_sequence<int, TP - H1>{});
@@ -311,7 +324,10 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, in
 #pragma unroll
       for (int t = 0; t < TP; ++t)
 #pragma unroll
-        for (int a = 0; a < TC; ++a) rv[t][a] = f16x4{};
+        for (int a = 0; a < TC; ++a) {
+          rv[t][a] = f16x4{};
+          if constexpr (SPLIT) rl[t][a] = f16x4{};
+        }
     }
     const bool after = p.act_after_res != 0;
     // f16 rows through LDS: each pixel's channels leave as whole 16-byte chunks of
@@ -329,14 +345,18 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, in
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const float x = acc[a][t][j] + bt[j];
-          const float r = (float)rv[t][a][j];
+          const float r = SPLIT ? (float)rv[t][a][j] + (float)rl[t][a][j] : (float)rv[t][a][j];
           const float xr = x + r;                                    // act(acc + b + res)
           const float y1 = xr > 0.f ? xr : xr * sl[a][j];
           const float y0 = (x > 0.f ? x : x * sl[a][j]) + r;         // act(acc + b) + res
           v[j] = ch + j < p.cout ? (after ? y1 : y0) : 0.f;          // channel padding stays 0
         }
-        *reinterpret_cast<f16x4*>(stg + ((pg * TP + t) * TW + fr) * PITCH + ch * 2) =
-            f16x4{(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
+        const f16x4 h = f16x4{(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
+        *reinterpret_cast<f16x4*>(stg + ((pg * TP + t) * TW + fr) * PITCH + ch * 2) = h;
+        if constexpr (SPLIT)
+          *reinterpret_cast<f16x4*>(stg + ((pg * TP + t) * TW + fr) * PITCH + (NPAD + ch) * 2) =
+              f16x4{(f16)(v[0] - (float)h[0]), (f16)(v[1] - (float)h[1]), (f16)(v[2] - (float)h[2]),
+                    (f16)(v[3] - (float)h[3])};
       }
     }
     __syncthreads();
@@ -348,12 +368,13 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, in
 #pragma unroll
       for (int k = 0; k < SIT; ++k) {
         const int idx = threadIdx.x + k * 64 * NW;
-        const int pl = idx / CH8, cq = idx - (idx / CH8) * CH8;
+        const int pl = idx / (NS * CH8), cqs = idx - (idx / (NS * CH8)) * (NS * CH8);
+        const int half = SPLIT && cqs >= CH8 ? 1 : 0, cq = cqs - half * CH8;
         const int ry = pl / TW, rx = pl & (TW - 1);
         const int oy = ty * TH + ry, oxx = tx * TW + rx;
         if (oy >= H || oxx >= W || cq >= cw8) continue;
-        const f16x8 val = *reinterpret_cast<const f16x8*>(stg + pl * PITCH + cq * 16);
-        f16* yp = yblk + (__umul24((unsigned)(ry * W + rx), ycs) + (unsigned)(cq * 8));
+        const f16x8 val = *reinterpret_cast<const f16x8*>(stg + pl * PITCH + cqs * 16);
+        f16* yp = yblk + (__umul24((unsigned)(ry * W + rx), ycs) + (unsigned)(cq * 8 + half * p.ysplit));
         if (cq * 8 + 8 <= p.cwrite) {
           *reinterpret_cast<f16x8*>(yp) = val;
         } else {
@@ -396,6 +417,16 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, in
 // (one SIMD idle), 4 for 128. SCRFD-10G 80x80x96 (N 64): 200 -> 134 us per conv, the net
 // 6.24 -> 5.62 ms (r03o).
 struct T2dShape { int nch, g, nw, tp, nbuf = 2; };
+// split (f16x3) shapes: cin is the logical channel count (the halo holds 2x); the weights of
+// the 3/2 x longer virtual K (216 registers for 32 channels) leave one wave per SIMD, and the
+// block height keeps the two halo buffers and the split staging image within the LDS
+static bool t2d_shape_split(int cin, int npad, T2dShape* sh) {
+  if (getenv("PC_T2D_SPLIT") && atoi(getenv("PC_T2D_SPLIT")) == 0) return false;   // tuning: off
+  if (cin == 32 && npad == 32) *sh = {2, 1, 4, 4};
+  else if (cin == 32 && npad == 64) *sh = {2, 2, 4, 4};
+  else return false;
+  return true;
+}
 static bool t2d_shape(int cin, int npad, T2dShape* sh) {
   const bool wide = !getenv("PC_T2D_NARROW");   // tuning: the round-2 shapes only
   const bool la = getenv("PC_T2D_NBUF3") != nullptr;   // tuning: two-block halo lookahead
@@ -413,23 +444,25 @@ static bool t2d_shape(int cin, int npad, T2dShape* sh) {
 
 // piecewise-linear activations, f16 output in whole 16-byte pixel chunks; 0 if the conv
 // cannot run on it
+// split: input / output / residual are f16x3 split tensors (cin logical); only split-in ->
+// split-out convs (the detector trunk) run here
 int conv_t2d_supported(int cin, int npad, int KH, int KW, int stride, int pad, int act, int out_f32, int ycs,
-                       int ycoff) {
+                       int ycoff, int split) {
   if (KH != 3 || KW != 3 || stride != 1 || pad != 1) return 0;
   if (act != ACT_NONE && act != ACT_RELU && act != ACT_PRELU) return 0;
   if (out_f32 || (ycs & 7) || (ycoff & 7)) return 0;
   T2dShape sh;
-  return t2d_shape(cin, npad, &sh) ? 1 : 0;
+  return (split ? t2d_shape_split(cin, npad, &sh) : t2d_shape(cin, npad, &sh)) ? 1 : 0;
 }
 
 // output rows per block (the block is TH x 16 pixels)
-int conv_t2d_rows(int cin, int npad) {
+int conv_t2d_rows(int cin, int npad, int split) {
   T2dShape sh;
-  if (!t2d_shape(cin, npad, &sh)) return 16;
+  if (!(split ? t2d_shape_split(cin, npad, &sh) : t2d_shape(cin, npad, &sh))) return 16;
   return sh.tp * sh.nw / sh.g;
 }
 
-template <int NCH, int G, int NW, int TP, int NBUF = 2>
+template <int NCH, int G, int NW, int TP, int NBUF = 2, bool SPLIT = false>
 static hipError_t launch_t2d(const ConvParams& p, hipStream_t s) {
   static int ncu = 0;
   if (!ncu) {
@@ -443,14 +476,29 @@ static hipError_t launch_t2d(const ConvParams& p, hipStream_t s) {
   const long long nt = (long long)p.N * nty * ntx;
   if (nt <= 0 || nt >= (1LL << 31)) return hipErrorInvalidValue;
   const int grid = (int)std::min<long long>(nt, ncu);
-  hipLaunchKernelGGL((conv_t2d<NCH, G, NW, TP, NBUF>), dim3(grid), dim3(64 * NW), 0, s, p, nty, ntx, (int)nt);
+  hipLaunchKernelGGL((conv_t2d<NCH, G, NW, TP, NBUF, SPLIT>), dim3(grid), dim3(64 * NW), 0, s, p, nty, ntx, (int)nt);
   return hipGetLastError();
 }
 
 hipError_t conv_t2d_launch(const ConvParams& p, hipStream_t s) {
   const ConvSeg& S = p.seg[0];
-  if (p.nseg != 1 || p.splitk != 1 || S.H != p.OH || S.W != p.OW || p.cwrite > p.npad ||
-      !conv_t2d_supported(S.C, p.npad, S.KH, S.KW, S.stride, S.pad, p.act, p.out_f32, p.ycs, 0) ||
+  const int split = S.vwrap ? 1 : 0;
+  if (split) {
+    // split-in -> split-out only: [hi | lo] halo of 2 x cin channels, virtual K 3 x cin per tap
+    const int cin = S.C / 2;
+    if (p.nseg != 1 || p.splitk != 1 || S.H != p.OH || S.W != p.OW || p.cwrite > p.npad || p.cwrite % 8 ||
+        S.cs != S.C || S.vwrap * 3 != S.cblk * 2 || !p.ysplit || (p.ysplit & 7) ||
+        (p.res_mode != RES_NONE && (!p.rsplit || (p.rsplit & 3))) ||
+        !conv_t2d_supported(cin, p.npad, S.KH, S.KW, S.stride, S.pad, p.act, p.out_f32, p.ycs, 0, 1) ||
+        (reinterpret_cast<uintptr_t>(p.y) & 15) || p.ktot < 27LL * cin)
+      return hipErrorInvalidValue;
+    T2dShape sh;
+    t2d_shape_split(cin, p.npad, &sh);
+    if (sh.g == 1) return launch_t2d<2, 1, 4, 4, 2, true>(p, s);
+    return launch_t2d<2, 2, 4, 4, 2, true>(p, s);
+  }
+  if (p.nseg != 1 || p.splitk != 1 || S.H != p.OH || S.W != p.OW || p.cwrite > p.npad || p.ysplit || p.rsplit ||
+      !conv_t2d_supported(S.C, p.npad, S.KH, S.KW, S.stride, S.pad, p.act, p.out_f32, p.ycs, 0, 0) ||
       (reinterpret_cast<uintptr_t>(p.y) & 15) || p.ktot < 9LL * S.C)
     return hipErrorInvalidValue;
   // Cin 64: the 144 weight registers leave no room for a second wave per SIMD, so 4

@@ -20,13 +20,18 @@ namespace pc {
 // 16-pixel groups per wave: weights, bias and slopes are loaded once for all of them
 constexpr int kStemGroupsPerWave = 4;
 
-template <int NPAD>
+// SPLIT (f16x3 detector): the weights are W_hi | W_lo ([npad][64]: K 0-31 hi, 32-63 lo) and the
+// input (u8-derived, exact in f16) is multiplied by both, so the f32 accumulator holds x*W to
+// ~2^-22; the output is written split (hi = f16(v), lo = f16(v - hi), lo half at +ysplit).
+template <int NPAD, bool SPLIT = false>
 __global__ __launch_bounds__(256) void stem_fused(StemParams p, const f16* __restrict__ wpk,
                                                    const float* __restrict__ bias, const float* __restrict__ slope,
                                                    int cwrite) {
   constexpr int TC = NPAD / 16;
-  constexpr int PITCH = NPAD * 2 + 16;        // padded f16 row of the staging image
-  constexpr int CH8 = NPAD / 8;               // 16-byte chunks per pixel
+  constexpr int NS = SPLIT ? 2 : 1;           // halves in the staging image
+  constexpr int PITCH = NS * NPAD * 2 + 16;   // padded f16 row of the staging image
+  constexpr int CH8 = NPAD / 8;               // 16-byte chunks per pixel and half
+  constexpr int KROW = SPLIT ? 64 : 32;       // weight row length
   __shared__ __attribute__((aligned(16))) char stg[4][16 * PITCH];
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -37,11 +42,12 @@ __global__ __launch_bounds__(256) void stem_fused(StemParams p, const f16* __res
 
   // weights: A fragment a = rows a*16 + fr, K fq*8 .. fq*8+7; bias / slope of this lane's
   // output channels, all held for the wave's kStemGroupsPerWave pixel groups
-  f16x8 wa[TC];
+  f16x8 wa[TC], wl[SPLIT ? TC : 1];
   float bi[TC][4], sl[TC][4];
 #pragma unroll
   for (int a = 0; a < TC; ++a) {
-    wa[a] = *reinterpret_cast<const f16x8*>(wpk + (a * 16 + fr) * 32 + fq * 8);
+    wa[a] = *reinterpret_cast<const f16x8*>(wpk + (a * 16 + fr) * KROW + fq * 8);
+    if constexpr (SPLIT) wl[a] = *reinterpret_cast<const f16x8*>(wpk + (a * 16 + fr) * KROW + 32 + fq * 8);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       bi[a][j] = bias[a * 16 + fq * 4 + j];
@@ -88,6 +94,7 @@ __global__ __launch_bounds__(256) void stem_fused(StemParams p, const f16* __res
 #pragma unroll
     for (int a = 0; a < TC; ++a) {
       f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[a], b, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      if constexpr (SPLIT) acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[a], b, acc, 0, 0, 0);
       const int ch = a * 16 + fq * 4;   // output rows of this lane: pixel fr, channels ch .. ch+3
       float o[4];
 #pragma unroll
@@ -96,18 +103,25 @@ __global__ __launch_bounds__(256) void stem_fused(StemParams p, const f16* __res
         x = act_apply(x, p.act, sl[a][j]);
         o[j] = ch + j < p.cout ? x : 0.f;   // channel padding stays exactly zero
       }
-      *reinterpret_cast<f16x4*>(my + fr * PITCH + ch * 2) = f16x4{(f16)o[0], (f16)o[1], (f16)o[2], (f16)o[3]};
+      const f16x4 h = f16x4{(f16)o[0], (f16)o[1], (f16)o[2], (f16)o[3]};
+      *reinterpret_cast<f16x4*>(my + fr * PITCH + ch * 2) = h;
+      if constexpr (SPLIT)
+        *reinterpret_cast<f16x4*>(my + fr * PITCH + (NPAD + ch) * 2) =
+            f16x4{(f16)(o[0] - (float)h[0]), (f16)(o[1] - (float)h[1]), (f16)(o[2] - (float)h[2]),
+                  (f16)(o[3] - (float)h[3])};
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-    for (int k = 0; k < (16 * CH8 + 63) / 64; ++k) {
+    for (int k = 0; k < (16 * NS * CH8 + 63) / 64; ++k) {
       const int idx = lane + k * 64;
-      const int pl = idx / CH8, cq = idx - (idx / CH8) * CH8;
+      const int pl = idx / (NS * CH8), cqs = idx - pl * (NS * CH8);
+      const int half = cqs >= CH8 ? 1 : 0, cq = cqs - half * CH8;
       if (pl >= 16 || cq >= cw8 || q0 + pl >= M) continue;
-      const f16x8 val = *reinterpret_cast<const f16x8*>(my + pl * PITCH + cq * 16);
-      *reinterpret_cast<f16x8*>(reinterpret_cast<f16*>(p.y) + (size_t)(q0 + pl) * p.ycs + cq * 8) = val;
+      const f16x8 val = *reinterpret_cast<const f16x8*>(my + pl * PITCH + cqs * 16);
+      *reinterpret_cast<f16x8*>(reinterpret_cast<f16*>(p.y) + (size_t)(q0 + pl) * p.ycs + half * p.ysplit + cq * 8) =
+          val;
     }
   }
 }
@@ -129,6 +143,15 @@ hipError_t stem_fused_launch(const StemParams& p, const void* wpk, const float* 
       (reinterpret_cast<uintptr_t>(p.x) & 7))
     return hipErrorInvalidValue;
   const f16* w = reinterpret_cast<const f16*>(wpk);
+  if (p.ysplit) {
+    if (p.ysplit % 8) return hipErrorInvalidValue;
+    switch (npad) {
+      case 32: hipLaunchKernelGGL((stem_fused<32, true>), dim3((unsigned)nwg), dim3(256), 0, s, p, w, bias, slope, cwrite); break;
+      case 64: hipLaunchKernelGGL((stem_fused<64, true>), dim3((unsigned)nwg), dim3(256), 0, s, p, w, bias, slope, cwrite); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   switch (npad) {
     case 32: hipLaunchKernelGGL(stem_fused<32>, dim3((unsigned)nwg), dim3(256), 0, s, p, w, bias, slope, cwrite); break;
     case 64: hipLaunchKernelGGL(stem_fused<64>, dim3((unsigned)nwg), dim3(256), 0, s, p, w, bias, slope, cwrite); break;

@@ -8,7 +8,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import models
-from ._lib import PC_PREC_F16, PC_PREC_F32, LetterboxDesc, check
+from ._lib import PC_PREC_F16, PC_PREC_F16X3, PC_PREC_F32, LetterboxDesc, check, net_precision
 from .runtime import DeviceBuffer, GpuContext, Net
 
 
@@ -135,8 +135,9 @@ class ScrfdEngine:
         self.D = D
         self.variant = variant
         self.precision = precision
-        self.program = models.compile_scrfd(params, variant, D)
-        self.net = Net(ctx, self.program.serialize(), precision=precision, max_batch=max_batch)
+        # PC_PREC_F16X3: the split program on an f16 net (f32-class boxes and landmarks)
+        self.program = models.compile_scrfd(params, variant, D, split=precision == PC_PREC_F16X3)
+        self.net = Net(ctx, self.program.serialize(), precision=net_precision(precision), max_batch=max_batch)
         self.max_batch = max_batch
         self.max_det = max_det
 

@@ -44,7 +44,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import imageops, models, onnx_models
-from ._lib import PC_PREC_F16, PC_PREC_F32, ResizeDesc, WarpDesc, check
+from ._lib import PC_PREC_F16, PC_PREC_F16X3, PC_PREC_F32, ResizeDesc, WarpDesc, check
 from .engines import ArcFaceEngine, ScrfdEngine, opencv_vresize_simd_end
 from .face_yolo import YoloFaceBranch
 from .runtime import GpuContext
@@ -90,6 +90,22 @@ def get_context(device_index: int, role: str = "") -> GpuContext:
 def _precision(var: str = "PERSON_CAPTURE_AMD_PRECISION") -> int:
     v = os.getenv(var, os.getenv("PERSON_CAPTURE_AMD_PRECISION", "f16")).strip().lower()
     return PC_PREC_F32 if v in ("f32", "fp32", "float32") else PC_PREC_F16
+
+
+def _det_precision() -> int:
+    """SCRFD precision. Default f16x3 (split hi/lo activations and weights on the f16 MFMA
+    path): its boxes, landmarks and therefore chips and accept decisions are
+    the f32 path's, where plain f16 moved sub-pixel landmarks enough to flip decisions on
+    noise frames (bench.py parity). PERSON_CAPTURE_AMD_DET_PRECISION=f16 / f32 select the
+    others; with PERSON_CAPTURE_AMD_PRECISION=f32 (the parity mode) the detector is f32 too."""
+    v = os.getenv("PERSON_CAPTURE_AMD_DET_PRECISION", "").strip().lower()
+    if not v:
+        return PC_PREC_F32 if _precision() == PC_PREC_F32 else PC_PREC_F16X3
+    if v in ("f32", "fp32", "float32"):
+        return PC_PREC_F32
+    if v in ("f16x3", "x3", "split"):
+        return PC_PREC_F16X3
+    return PC_PREC_F16
 
 
 def synthetic_weights(kind: str, seed: int = 0) -> models.Params:
@@ -182,7 +198,7 @@ class FaceEmbedder(YoloFaceBranch):
         self.precision = _precision()
         # detector precision (default: the embedder's): SCRFD f32 + ArcFace f16 gives the f32
         # chips (the f16 landmarks move noise-frame chips, bench.py f16_parity attribution)
-        self.det_precision = _precision("PERSON_CAPTURE_AMD_DET_PRECISION")
+        self.det_precision = _det_precision()
         self._ctx = get_context(self._device_index)
         self._scrfd_ctx_id = self._device_index
         seed = int(os.getenv("PERSON_CAPTURE_AMD_SEED", "0"))
@@ -763,6 +779,46 @@ class FaceEmbedder(YoloFaceBranch):
 
     def set_policy_state(self, st: tuple) -> None:
         self._frame_idx, self._no_face_streak, self._last_face_idx, self._rot_cycle, self._prescan_rr = st
+
+    def prescan_policy_key(self, state: tuple, active: bool, H: int, W: int) -> tuple:
+        """What a fast pre-scan sample's extraction reads of the policy state, for the sharded
+        pre-scan merge (prescan_shard.py): a speculative result is reused only when this key is
+        the true stream's. With the pre-scan configuration (rot_adaptive off, gui_app.py:1164)
+        the regime picks escalation / full rotation mode (_scrfd_policy, face_embedder.py:
+        2330-2360: every empty sample probes rotations; "rr" mode probes (90, 270)[rr % 2]); the
+        no-face streak enters only through `streak >= 3` in _dyn_for, and only where that
+        changes the det size of this H x W sample. Adaptive rotation gates read the frame and
+        last-face indices: then the whole state is the key."""
+        if self.rot_adaptive or not self._fast_prescan:
+            return (bool(active), tuple(state))
+        im = _DevImage(0, int(H), int(W), int(W) * 3)
+        saved = self._no_face_streak
+        try:
+            self._no_face_streak = 0
+            d0 = self._dyn_for(im, None)
+            self._no_face_streak = 3
+            d3 = self._dyn_for(im, None)
+        finally:
+            self._no_face_streak = saved
+        fi, streak, last, rc, rr = state
+        return (bool(active), (streak >= 3) if d0 != d3 else None, None if active else rr % 2)
+
+    @staticmethod
+    def policy_transfer(spec_in: tuple, spec_out: tuple, true_in: tuple) -> tuple:
+        """The true policy state after a sample whose extraction ran speculatively from
+        spec_in to spec_out (same prescan_policy_key as true_in): the per-sample updates of
+        _scrfd_policy replayed on the true state - the frame index advances by one, a found
+        face resets the streak / rotation cycle and stamps the last-face index, an empty sample
+        grows them, an "rr" probe advances the round-robin counter."""
+        fi0, st0, lf0, rc0, rr0 = spec_in
+        fi1, st1, lf1, rc1, rr1 = spec_out
+        tfi, tst, tlf, trc, trr = true_in
+        found = lf1 != lf0   # a 0-degree face stamps the last-face index (always < the frame index)
+        return (tfi + (fi1 - fi0),
+                0 if found else tst + (st1 - st0),
+                tfi + (lf1 - fi0) if found else tlf,
+                0 if found else trc + (rc1 - rc0),
+                trr + (rr1 - rr0))
 
     def _dyn_for(self, im: _DevImage, imgsz: Optional[int]) -> int:
         """face_embedder.py:2190-2204."""

@@ -25,7 +25,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import imageops, models_yolo
-from ._lib import PC_PREC_F16, WarpDesc, YoloLetterboxDesc, YoloScale, check
+from ._lib import PC_PREC_F16, WarpDesc, YoloLetterboxDesc, YoloScale, check, net_precision
 from .engines import opencv_vresize_simd_end
 from .runtime import GpuContext, Net
 
@@ -120,7 +120,8 @@ class YoloFaceBranch:
             # batch capacity for the speculative 0-degree pass of extract_batch; big fallback
             # canvases keep the activation footprint of a det_batch x 640 x 640 engine
             mb = max(1, min(self._det_batch, self._det_batch * 640 * 640 // (Hp * Wp)))
-            eng = YoloFaceEngine(self._ctx, self._yf_params, self.yolo_scale, Hp, Wp, self.det_precision, max_batch=mb)
+            eng = YoloFaceEngine(self._ctx, self._yf_params, self.yolo_scale, Hp, Wp, net_precision(self.det_precision),
+                                 max_batch=mb)
             self._yf_engines[(Hp, Wp)] = eng
         return eng
 

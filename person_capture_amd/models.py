@@ -280,12 +280,14 @@ def _conv_bias(P: Program, p: Params, x: int, name: str, cin: int, cout: int, k:
     return out
 
 
-def compile_scrfd(p: Params, variant: str = "10g", D: int = 640) -> Program:
+def compile_scrfd(p: Params, variant: str = "10g", D: int = 640, split: bool = False) -> Program:
     """SCRFD -> program for a DxD letterboxed input (NHWC4, (x-127.5)/128, RGB).
-    Outputs (per stride 8/16/32): f32 [H][W][32] = cls logits(2) | bbox(8) | kps(20)."""
+    Outputs (per stride 8/16/32): f32 [H][W][32] = cls logits(2) | bbox(8) | kps(20).
+    split: the f16x3 form (program.Program): f32-class activations and weights on the f16
+    MFMA path - the detector precision whose boxes and landmarks match the f32 path."""
     assert D % 32 == 0
     cfg = SCRFD_CFG[variant]
-    P = Program()
+    P = Program(split=split)
     x = P.input_tensor(D, D, 4)
     base = cfg["base"]
     # deep stem: conv3x3/s2 (direct stem kernel) + 2 convs, then maxpool 3x3/s2

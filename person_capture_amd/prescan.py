@@ -108,6 +108,18 @@ class _LoopState:
         return c
 
 
+@dataclass
+class SpecRecord:
+    """One speculatively extracted sample of a pre-scan shard (prescan_shard.py): the regime
+    it ran under (span open: escalation + full rotation mode), the FaceEmbedder policy state
+    before and after it, and its faces (host dicts: bbox, kps5, feat, quality)."""
+    pos: int
+    active: bool
+    state_in: tuple
+    state_out: tuple
+    faces: list
+
+
 class PrescanRunner:
     """Processor._prescan's sampling loop for one FaceEmbedder (SCRFD backend)."""
 
@@ -118,6 +130,63 @@ class PrescanRunner:
         self.records: List[SampleRecord] = []
         self.chunks = 0
         self.cuts = 0
+        self.spec: Optional[List[SpecRecord]] = None   # run(..., speculate=True) fills it
+        self.initial_state: Optional[tuple] = None
+
+    def samples(self) -> List[int]:
+        """Frame index of every sample position (gui_app.py:1468: range(0, total, stride))."""
+        return list(range(0, self.total, max(1, int(self.cfg.prescan_stride))))
+
+    def setup_face(self) -> None:
+        """The FaceEmbedder configuration of a pre-scan (gui_app.py:1162-1196)."""
+        f = self.face
+        self._apply_face_cfg()
+        f.configure_rotation_strategy(adaptive=False)
+        f.set_prescan_fast(True, mode="rr")
+        f.set_prescan_hint(escalate=False)
+        self._apply_face_cfg()
+
+    def extract_one(self, frame_at, pos: int, active: bool, state: tuple):
+        """Sample `pos` extracted under the given regime and policy state (the sharded
+        merge's re-extraction). Returns (faces, policy state after)."""
+        f = self.face
+        f.set_policy_state(state)
+        f._prescan_rr_mode = "full" if active else "rr"
+        f.set_prescan_hint(escalate=active)
+        im = frame_at(self.samples()[pos])
+        if not hasattr(im, "ptr"):
+            im = f._upload(np.ascontiguousarray(im), key="prescan_src0")
+        im = self._downscale(im, 0)
+        res = f.extract_batch([None], dev_frames=[im])
+        return res[0], f.policy_state()
+
+    def close(self, st: "_LoopState") -> List[Tuple[int, int]]:
+        """End of the loop: close an open span at the last frame, then bridge short gaps
+        (gui_app.py:1648-1668)."""
+        c = self.cfg
+        if st.active:
+            pad = int(round(c.prescan_pad_sec * self.fps))
+            min_len = int(round(c.prescan_min_segment_sec * self.fps))
+            s, e = max(0, st.start - pad), self.total - 1
+            if e - s + 1 >= min_len:
+                if st.spans and s <= st.spans[-1][1] + 1:
+                    st.spans[-1] = (st.spans[-1][0], max(st.spans[-1][1], e))
+                else:
+                    st.spans.append((s, e))
+        spans = st.spans
+        if spans and c.prescan_bridge_gap_sec > 0:
+            gap = int(round(c.prescan_bridge_gap_sec * self.fps))
+            bridged = []
+            cs, ce = spans[0]
+            for s, e in spans[1:]:
+                if s - ce <= gap:
+                    ce = max(ce, e)
+                else:
+                    bridged.append((cs, ce))
+                    cs, ce = s, e
+            bridged.append((cs, ce))
+            spans = bridged
+        return spans
 
     # ---- FaceEmbedder runtime configuration (gui_app.py:1162-1196) ----
     def _apply_face_cfg(self) -> None:
@@ -198,24 +267,27 @@ class PrescanRunner:
         n = len(faces) if extracted else 0
         return SampleRecord(idx, extracted, float(best), n, action, st.active)
 
-    def run(self, frame_at: Callable[[int], object]) -> Tuple[List[Tuple[int, int]], Optional[np.ndarray]]:
+    def run(self, frame_at: Callable[[int], object], positions: Optional[range] = None,
+            speculate: bool = False) -> Tuple[List[Tuple[int, int]], Optional[np.ndarray]]:
         """frame_at(frame_index) -> the frame as a device image (face_embedder._DevImage) or a host
-        BGR array. Returns (spans, updated bank) like Processor._prescan."""
+        BGR array. Returns (spans, updated bank) like Processor._prescan.
+        positions: run only these sample positions (a contiguous shard of the sample list, as
+        if the clip started there); speculate: record every extracted sample as a SpecRecord
+        in self.spec (regime, policy state in / out, faces) for the sharded merge."""
         f, c = self.face, self.cfg
-        self._apply_face_cfg()
-        f.configure_rotation_strategy(adaptive=False)
-        f.set_prescan_fast(True, mode="rr")
-        f.set_prescan_hint(escalate=False)
-        self._apply_face_cfg()
-        stride = max(1, int(c.prescan_stride))
-        samples = list(range(0, self.total, stride))
+        self.setup_face()
+        self.initial_state = f.policy_state()
+        samples = self.samples()
+        pos = range(len(samples)) if positions is None else positions
+        if speculate:
+            self.spec = []
         st = _LoopState(self.ref_feat)
-        k = 0
-        while k < len(samples):
+        k = pos.start
+        while k < pos.stop:
             # ---- predict the next chunk under the current regime ----
             sim = st.copy()
             plan = []   # (sample position, skip)
-            for j in range(k, min(len(samples), k + self.batch)):
+            for j in range(k, min(pos.stop, k + self.batch)):
                 skip, _ = self._gate(sim)
                 plan.append((j, skip))
                 # regime assumption: the last extracted sample's outcome repeats (faces with a finite
@@ -253,6 +325,8 @@ class PrescanRunner:
                 st.processed += 1
                 self.records.append(rec)
                 if not skip:
+                    if speculate:
+                        self.spec.append(SpecRecord(j, active0, last_state, state_after[j], _host_faces(by_pos[j])))
                     last_state = state_after[j]
             if cut is not None:
                 self.cuts += 1
@@ -260,32 +334,18 @@ class PrescanRunner:
             else:
                 k = plan[-1][0] + 1
             f.set_policy_state(last_state)
-        if st.active:
-            pad = int(round(c.prescan_pad_sec * self.fps))
-            min_len = int(round(c.prescan_min_segment_sec * self.fps))
-            s, e = max(0, st.start - pad), self.total - 1
-            if e - s + 1 >= min_len:
-                if st.spans and s <= st.spans[-1][1] + 1:
-                    st.spans[-1] = (st.spans[-1][0], max(st.spans[-1][1], e))
-                else:
-                    st.spans.append((s, e))
-        spans = st.spans
-        if spans and c.prescan_bridge_gap_sec > 0:
-            gap = int(round(c.prescan_bridge_gap_sec * self.fps))
-            bridged = []
-            cs, ce = spans[0]
-            for s, e in spans[1:]:
-                if s - ce <= gap:
-                    ce = max(ce, e)
-                else:
-                    bridged.append((cs, ce))
-                    cs, ce = s, e
-            bridged.append((cs, ce))
-            spans = bridged
+        spans = self.close(st)
         f.set_prescan_fast(False)
         f.set_prescan_hint(escalate=False)
         self.final_state = st
         return spans, st.bank
+
+
+def _host_faces(faces) -> list:
+    """The parts of extract()'s face dicts the pre-scan loop and its merge read (picklable
+    host values: no chips or device handles)."""
+    keep = ("bbox", "kps5", "feat", "quality", "score")
+    return [{k: f[k] for k in keep if k in f} for f in faces]
 
 
 def run_cached(runner: "PrescanRunner", frame_at, video, refs="", cache_dir: str = "prescan_cache",

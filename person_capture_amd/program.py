@@ -10,7 +10,8 @@ residual epilogues or second K-segments). The device executor
 Binary format (little-endian int32 words, then float32 data):
   magic 'PCNT', version 1, n_buf, n_tensor, n_array, n_op, n_out, input_tensor
   buffers : n_buf   x [elems_per_image lo, hi, is_f32, 0]
-  tensors : n_tensor x [buf, H, W, C, cs, coff, is_f32, 0]
+  tensors : n_tensor x [buf, H, W, C, cs, coff, is_f32, split]
+            (split: f16x3 tensor, C physical channels = [hi | lo] halves of C/2)
   arrays  : n_array x [offset lo, hi, count lo, hi]   (in floats, into data)
   outputs : n_out tensor ids
   ops     : n_op x 32 words (layouts below, mirrored in pc_api.cpp)
@@ -34,11 +35,20 @@ def cpad(c: int, m: int = 32) -> int:
 
 
 class Program:
-    """Builder for a pcgpu network program."""
+    """Builder for a pcgpu network program.
 
-    def __init__(self) -> None:
+    split=True builds the f16x3 form: every f16 activation is stored as
+    two f16 halves [hi | lo] (x = hi + lo, f32-class precision), and every conv that reads
+    one walks K as [hi, lo, hi] per tap against weights [W_hi, W_hi, W_lo], so the device
+    accumulates x_hi*W_hi + x_lo*W_hi + x_hi*W_lo in f32 (the dropped x_lo*W_lo is ~2^-22
+    relative). The models compile unchanged: act() allocates the halves and conv()
+    expands the weight columns."""
+
+    def __init__(self, split: bool = False) -> None:
+        self.split = bool(split)
         self.vbufs: List[List[int]] = []          # [elems_per_image, is_f32]
-        self.tensors: List[List[int]] = []        # [vbuf, H, W, C, cs, coff, is_f32]
+        self.tensors: List[List[int]] = []        # [vbuf, H, W, C, cs, coff, is_f32]  (C, cs physical)
+        self.tsplit: List[int] = []               # per tensor: 1 = f16x3 split
         self.arrays: List[np.ndarray] = []
         self.ops: List[List[int]] = []
         self.outputs: List[int] = []
@@ -49,27 +59,35 @@ class Program:
     def input_tensor(self, H: int, W: int, C: int) -> int:
         t = len(self.tensors)
         self.tensors.append([-1, H, W, C, C, 0, 0])
+        self.tsplit.append(0)
         self.input = t
         return t
 
     def act(self, H: int, W: int, C: int, is_f32: int = 0) -> int:
+        """Activation of C (padded) channels; in a split program an f16 one holds 2C."""
+        sp = 1 if (self.split and not is_f32) else 0
+        Cp = C * (2 if sp else 1)
         vb = len(self.vbufs)
-        self.vbufs.append([H * W * C, is_f32])
+        self.vbufs.append([H * W * Cp, is_f32])
         t = len(self.tensors)
-        self.tensors.append([vb, H, W, C, C, 0, is_f32])
+        self.tensors.append([vb, H, W, Cp, Cp, 0, is_f32])
+        self.tsplit.append(sp)
         return t
 
     def view(self, t: int, coff: int, C: int) -> int:
         """Channel slice [coff, coff+C) of tensor t (same buffer and pixel stride):
         concatenations are written and read in place."""
         vb, H, W, C0, cs, off, f32 = self.tensors[t]
+        assert not self.tsplit[t], "channel views of split tensors are not supported"
         assert coff + C <= C0
         self.tensors.append([vb, H, W, C, cs, off + coff, f32])
+        self.tsplit.append(0)
         return len(self.tensors) - 1
 
     def dims(self, t: int) -> Tuple[int, int, int]:
+        """(H, W, logical channels): a split tensor's C counts one half."""
         T = self.tensors[t]
-        return T[1], T[2], T[3]
+        return T[1], T[2], T[3] // 2 if self.tsplit[t] else T[3]
 
     def arr(self, a: np.ndarray) -> int:
         self.arrays.append(np.ascontiguousarray(a, dtype=np.float32).reshape(-1))
@@ -85,6 +103,8 @@ class Program:
         flops_cout: true output channels for the FLOP count when the packed weight rows
         interleave padding (outputs split into padded channel slices)."""
         assert 1 <= len(segs) <= 2
+        if any(self.tsplit[s[0]] for s in segs):
+            w_packed = self._split_columns(w_packed, segs)
         npad, ktot = w_packed.shape
         w = [0] * 32
         w[0] = OP_CONV
@@ -111,6 +131,26 @@ class Program:
         fc = flops_cout or cout
         for (t, kh, kw, s, p, cin) in segs:
             self.flops_per_image += 2.0 * oh * ow * fc * kh * kw * cin
+
+    def _split_columns(self, w_packed: np.ndarray, segs) -> np.ndarray:
+        """[npad][sum KH*KW*C] -> split segments' columns as [W_hi | W_hi | W_lo] per tap
+        (f32 values exactly representable in f16: the device's f16 upload is exact)."""
+        w32 = np.asarray(w_packed, dtype=np.float32)
+        npad = w32.shape[0]
+        cols, k0 = [], 0
+        for (t, kh, kw, _s, _p, _cin) in segs:
+            cp = self.dims(t)[2]
+            n = kh * kw * cp
+            blk = w32[:, k0:k0 + n]
+            k0 += n
+            if self.tsplit[t]:
+                taps = blk.reshape(npad, kh * kw, cp)
+                hi = taps.astype(np.float16).astype(np.float32)
+                lo = (taps - hi).astype(np.float16).astype(np.float32)
+                blk = np.concatenate([hi, hi, lo], axis=2).reshape(npad, kh * kw * 3 * cp)
+            cols.append(blk)
+        assert k0 == w32.shape[1], "packed weight columns do not match the segments"
+        return np.concatenate(cols, axis=1)
 
     def stem(self, out: int, x: int, w: np.ndarray, bias: np.ndarray, stride: int, pad: int,
              slope: Optional[np.ndarray] = None, act: int = ACT_NONE, cin_true: int = 3) -> None:
@@ -213,8 +253,8 @@ class Program:
                             len(self.outputs), self.input]
         for elems, f32, _ in phys:
             words += [elems & 0xFFFFFFFF, elems >> 32, f32, 0]
-        for vb, H, W, C, cs, coff, f32 in self.tensors:
-            words += [mapping[vb] if vb >= 0 else -1, H, W, C, cs, coff, f32, 0]
+        for (vb, H, W, C, cs, coff, f32), sp in zip(self.tensors, self.tsplit):
+            words += [mapping[vb] if vb >= 0 else -1, H, W, C, cs, coff, f32, sp]
         off = 0
         for a in self.arrays:
             n = a.size

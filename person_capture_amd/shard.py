@@ -12,8 +12,12 @@ single stream does; only the first frames of each run start from a fresh state.
 Launch with `python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ...`
 (or `bench.py --gpus N`, which spawns the ranks itself); each rank binds
 `cuda:LOCAL_RANK` and builds its own FaceEmbedder (context, stream, weights).
-Sequential caller policy (pre-scan bank growth, lock-ROI) is replayed on rank 0 over
-the gathered, frame-ordered results (match.stream_ref_bank_update is host code).
+The pre-scan loop of one clip is sequential (fd9 gate, bank growth, span hysteresis):
+prescan_shard.run_sharded shards its sample positions the same way, gathers each rank's
+speculative per-sample results (with the regime and policy state they ran under) on rank 0,
+and replays the loop there in sample order, extracting again the samples whose speculative
+state was wrong - the single-stream spans and bank (tests/test_prescan_shard_cpu.py,
+tests/test_gpu_prescan_shard.py).
 """
 from __future__ import annotations
 

@@ -35,17 +35,42 @@ def run_program(P: pg.Program, x_nhwc: np.ndarray):
     bufs = {}
     A = [torch.from_numpy(a.astype(np.float32)) for a in P.arrays]
 
+    tsplit = getattr(P, "tsplit", [0] * len(P.tensors))
+
     def read(t):
+        """The tensor's values (a split tensor: hi + lo, exact in f32)."""
         vb, H, W, C, cs, off, _ = P.tensors[t]
         if vb < 0:
             return inp[:, off:off + C]
-        return bufs[vb][:, off:off + C]
+        x = bufs[vb][:, off:off + C]
+        if tsplit[t]:
+            return x[:, :C // 2] + x[:, C // 2:]
+        return x
+
+    def read_k(t):
+        """The channels a conv's K walks: a split tensor's virtual [hi, lo, hi]."""
+        vb, H, W, C, cs, off, _ = P.tensors[t]
+        if tsplit[t]:
+            x = bufs[vb][:, off:off + C]
+            return torch.cat([x[:, :C // 2], x[:, C // 2:], x[:, :C // 2]], 1)
+        return read(t)
 
     def write(t, y):
         vb, H, W, C, cs, off, _ = P.tensors[t]
         if vb not in bufs:
             bufs[vb] = torch.zeros(N, cs, H, W)
+        if tsplit[t]:   # device epilogue: hi = f16(v), lo = f16(v - hi)
+            h = C // 2
+            v = y[:, :h].float()
+            hi = v.half().float()
+            bufs[vb][:, off:off + h] = hi
+            bufs[vb][:, off + h:off + C] = (v - hi).half().float()
+            return
         bufs[vb][:, off:off + C] = y[:, :C]
+
+    def logical_c(t):
+        C = P.tensors[t][3]
+        return C // 2 if tsplit[t] else C
 
     for w in P.ops:
         if w[0] == pg.OP_CONV:
@@ -55,7 +80,7 @@ def run_program(P: pg.Program, x_nhwc: np.ndarray):
             k0 = 0
             for s in range(w[2]):
                 t, kh, kw, st, pd = w[3 + 5 * s: 8 + 5 * s]
-                X = read(t)
+                X = read_k(t)
                 cp = X.shape[1]
                 n = kh * kw * cp
                 ws = Wm[:, k0:k0 + n].reshape(npad, kh, kw, cp).permute(0, 3, 1, 2).contiguous()
@@ -90,7 +115,7 @@ def run_program(P: pg.Program, x_nhwc: np.ndarray):
                 acc[:, :k] = acc[:, :k] + res[:, :k]
             if w[23]:
                 acc = _act(acc, act, slope)
-            C = P.tensors[w[1]][3]
+            C = logical_c(w[1])
             out = torch.zeros(N, C, Ho, Wo)
             k = min(C, npad)
             out[:, :k] = acc[:, :k]
@@ -100,9 +125,15 @@ def run_program(P: pg.Program, x_nhwc: np.ndarray):
             X = read(w[2])
             cout = w[8]
             wt = A[w[7]].view(cout, 3, 3, 4).permute(0, 3, 1, 2).contiguous()
-            y = F.conv2d(X, wt, stride=w[5], padding=w[6]) + A[w[9]].view(1, -1, 1, 1)
+            if tsplit[w[1]]:   # split stem: x * W_hi + x * W_lo (the input is exact in f16)
+                whi = wt.half().float()
+                y = F.conv2d(X, whi, stride=w[5], padding=w[6]) + \
+                    F.conv2d(X, (wt - whi).half().float(), stride=w[5], padding=w[6])
+                y = y + A[w[9]].view(1, -1, 1, 1)
+            else:
+                y = F.conv2d(X, wt, stride=w[5], padding=w[6]) + A[w[9]].view(1, -1, 1, 1)
             y = _act(y, w[11], A[w[10]] if w[10] >= 0 else None)
-            cp = P.tensors[w[1]][3]
+            cp = logical_c(w[1])
             out = torch.zeros(y.shape[0], cp, y.shape[2], y.shape[3])
             out[:, :cout] = y
             write(w[1], out)

@@ -59,3 +59,31 @@ def test_program_serialization_and_buffer_reuse(r18):
             if P.tensors[t][0] >= 0:
                 assert mapping[P.tensors[t][0]] != ob
     assert 4e9 < P.flops_per_image < 8e9           # IResNet-18 at 112x112
+
+
+@pytest.mark.parametrize("variant", ["2.5g", "10g"])
+def test_scrfd_split_program_is_f32_class(variant):
+    """f16x3 detector: with every activation stored as f16 hi + lo and the
+    weights expanded to [W_hi, W_hi, W_lo] per tap, the emulated device semantics (f16
+    rounding of both halves and of the weight halves) stay at f32-class error against the
+    fp32 oracle - what the f16 form (1e-2-class) cannot."""
+    p = models.synth_scrfd(variant, seed=2)
+    D = 160 if variant == "10g" else 192
+    rng = np.random.default_rng(1)
+    x = np.zeros((1, D, D, 4), np.float32)
+    x[..., :3] = (rng.integers(0, 256, (1, D, D, 3)).astype(np.float32) - 127.5) / 128.0
+    ref = nt.scrfd_forward(p, variant, torch.from_numpy(np.ascontiguousarray(x[..., :3].transpose(0, 3, 1, 2))))
+    P = models.compile_scrfd(p, variant, D, split=True)
+    assert sum(P.tsplit) > 0 and all(P.tensors[t][6] == 0 for t in range(len(P.tensors)) if P.tsplit[t])
+    words = np.frombuffer(P.serialize(), dtype="<i4")
+    nbuf, nten = words[2], words[3]
+    trec = words[8 + 4 * nbuf: 8 + 4 * nbuf + 8 * nten].reshape(nten, 8)
+    assert list(trec[:, 7]) == P.tsplit
+    outs = run_program(P, x)
+    worst = 0.0
+    for o, r in zip(outs, ref):
+        got = o.permute(0, 2, 3, 1)[..., :30].numpy()
+        r = r.numpy()
+        worst = max(worst, np.abs(got - r).max() / max(1.0, np.abs(r).max()))
+    # (the plain program in fp32 emulation, i.e. only the folding algebra, is at ~3e-6 here)
+    assert worst < 1e-5, worst

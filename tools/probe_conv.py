@@ -1,6 +1,8 @@
 """Single-conv microbenchmark of the implicit-GEMM engine (HIP-event timed).
 usage: python tools/probe_conv.py [cfg[:rowb] ...]   (cfg "auto" = planner's choice)
-env PROBE_SHAPES=name1,name2 restricts the shapes."""
+env PROBE_SHAPES=name1,name2 restricts the shapes; PROBE_SPLIT=1 probes the f16x3 split form
+(split input and output, DESIGN.md §3.6: a 1x1 conv writes the split input first; only the
+probed conv is timed)."""
 import os
 import sys
 
@@ -30,8 +32,13 @@ SHAPES = [
 
 
 def build(N, H, cin, cout, k, s):
-    P = pg.Program()
+    split = bool(os.environ.get("PROBE_SPLIT"))
+    P = pg.Program(split=split)
     x = P.input_tensor(H, H, cin)
+    if split:   # split copy of the input (identity 1x1 conv), then the probed conv reads it
+        t = P.act(H, H, cin)
+        P.conv(t, [(x, 1, 1, 1, 0, cin)], pg.pack_conv_weights([np.eye(cin)[:, :, None, None]], [cin], cin), cin)
+        x = t
     Ho = (H + 2 * (k // 2) - k) // s + 1
     y = P.act(Ho, Ho, cout)
     rng = np.random.default_rng(0)
@@ -87,11 +94,16 @@ def main():
             net.profile(True)
             for _ in range(10):
                 net.run(d.ptr, N)
-            r = net.profile_read()
+            last = len(P.ops) - 1   # the probed conv (the split form has the input copy first)
+            recs = [r for r in net.profile_ops() if int(r[0]) == last]
             net.profile(False)
-            us = r["conv_ms"] * 1e3 / r["conv_launches"]
-            tf = r["conv_flops"] / (r["conv_ms"] * 1e-3) / 1e12
-            print(f"{name:16s} cfg {spec:6s} {us:9.1f} us/launch  {tf:7.1f} TFLOP/s", flush=True)
+            ms = sum(r[2] for r in recs)
+            us = ms * 1e3 / len(recs)
+            tf = sum(r[3] for r in recs) / (ms * 1e-3) / 1e12
+            code = int(recs[0][4])
+            ran = f"t{code - 200}" if code >= 200 else (f"f{code - 100}" if code >= 100 else
+                                                         (f"h{code}" if code >= 0 else f"g{int(recs[0][5])}"))
+            print(f"{name:16s} cfg {spec:6s} ran {ran:4s} {us:9.1f} us/launch  {tf:7.1f} TFLOP/s", flush=True)
             net.close()
 
 

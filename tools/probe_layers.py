@@ -1,5 +1,6 @@
 """Per-layer profile of the two trunks (HIP events around every launch, pc_net_profile_ops).
-usage: python tools/probe_layers.py [arc|scrfd] [batch]   -> table grouped by conv shape."""
+usage: python tools/probe_layers.py [arc|scrfd|scrfdx3] [batch]   -> table grouped by conv shape.
+scrfdx3: the f16x3 split SCRFD program."""
 import sys
 from collections import defaultdict
 
@@ -33,7 +34,8 @@ def main():
     if which == "arc":
         P = models.compile_iresnet(models.synth_iresnet(100, seed=0, calibrate=False), 100)
     else:
-        P = models.compile_scrfd(models.synth_scrfd("10g", seed=0, calibrate=False), "10g", 640)
+        P = models.compile_scrfd(models.synth_scrfd("10g", seed=0, calibrate=False), "10g", 640,
+                                 split=which == "scrfdx3")
     prec = PC_PREC_F32 if os.environ.get('PROBE_F32') else PC_PREC_F16
     net = Net(ctx, P.serialize(), prec, max_batch=B)
     H, W, Cc = P.dims(P.input)
