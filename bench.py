@@ -31,6 +31,7 @@ sys.path.insert(0, ROOT)
 
 PEAK_F16_TFLOPS = 2500.0   # MI355X dense fp16 MFMA (MI355X_MICROARCH.md, chip table)
 PEAK_F32_TFLOPS = 157.3
+PEAK_HBM_GBPS = 8000.0     # MI355X HBM3E spec peak (MI355X_MICROARCH.md; ~6.3 TB/s achievable)
 
 
 def _dist_init():
@@ -108,7 +109,9 @@ def cpu_baseline(frames: np.ndarray, fe, bank: np.ndarray, n_sample: int, n_samp
     import torch
     from oracle import pipeline as op
 
-    def run(threads, n):
+    oracle_res = []
+
+    def run(threads, n, keep=False):
         torch.set_num_threads(threads)
         t0 = time.perf_counter()
         faces = 0
@@ -116,10 +119,12 @@ def cpu_baseline(frames: np.ndarray, fe, bank: np.ndarray, n_sample: int, n_samp
             r = op.extract_frame(frames[i], fe._scrfd_params, fe.scrfd_variant, fe._arc_params, fe._arc_depth,
                                  conf=fe.conf, D=640, bank=bank)
             faces += 0 if r == op.NEEDS_FALLBACK else len(r)
+            if keep:
+                oracle_res.append(None if r == op.NEEDS_FALLBACK else r)
         return n / (time.perf_counter() - t0), faces, time.perf_counter() - t0
 
     threads = min(16, os.cpu_count() or 1)
-    v, faces, dt = run(threads, n_sample)
+    v, faces, dt = run(threads, n_sample, keep=True)
     out = {"value": round(v, 4), "unit": "frames/s", "cores": threads, "kind": "port",
            "host_cpu_count": os.cpu_count(),
            "sample": f"{n_sample} of the bench's 1080p frames through oracle/pipeline.extract_frame "
@@ -130,6 +135,139 @@ def cpu_baseline(frames: np.ndarray, fe, bank: np.ndarray, n_sample: int, n_samp
         out["value_1_thread"] = round(v1, 4)
         out["sample_1_thread"] = f"first {n_sample_1t} frames, {faces1} faces, {dt1:.1f} s at 1 thread"
     torch.set_num_threads(threads)
+    out["_oracle_results"] = oracle_res   # checker results for the parity block (not part of the line)
+    return out
+
+
+def compare_faces(res_a, res_b, band: float = 1e-3) -> dict:
+    """Face-by-face comparison of two runs over the same frames (res_b the reference; nearest
+    box pairing): face-count / box / accept mismatches at the CLI threshold 0.32 and the GUI's
+    0.45, the largest fd difference, and the accept flips whose reference fd lies farther than
+    `band` from the threshold (a flip inside the band is the f32-class noise of any
+    non-bitwise-identical path: the device f32 mode flips there against the CPU oracle too).
+    Frames with res_b None (the oracle's fallback frames) are skipped."""
+    n = count_mis = box_mis = acc32 = acc45 = out32 = out45 = 0
+    worst = 0.0
+    near = []
+    for a_f, b_f in zip(res_a, res_b):
+        if b_f is None:
+            continue
+        count_mis += abs(len(a_f) - len(b_f))
+        for b in b_f:
+            n += 1
+            a = min(a_f, key=lambda f: int(np.abs(f["bbox"].astype(np.int64) - b["bbox"]).sum())) if a_f else None
+            if a is None:
+                box_mis += 1
+                continue
+            box_mis += int(not np.array_equal(a["bbox"], b["bbox"]))
+            fa, fb = float(a["fd"]), float(b["fd"])
+            worst = max(worst, abs(fa - fb))
+            for thr, key in ((0.32, 0), (0.45, 1)):
+                if (fa <= thr) != (fb <= thr):
+                    far = abs(fb - thr) > band
+                    if key == 0:
+                        acc32 += 1
+                        out32 += far
+                        near.append(round(abs(fb - thr), 5))
+                    else:
+                        acc45 += 1
+                        out45 += far
+    return {"faces": n, "face_count_mismatch": count_mis, "box_mismatch": box_mis, "accept_mismatch_0.32": acc32,
+            "accept_mismatch_0.45": acc45, f"accept_mismatch_outside_{band:g}_band": out32 + out45,
+            "max_fd_diff": round(worst, 6), "flipped_ref_distance_to_0.32": sorted(near)}
+
+
+def hbm_kernels(fe, devs, H: int, W: int, reps: int = 20, kinds=("letterbox", "warp", "maxpool")) -> dict:
+    """Achieved HBM rate of the bandwidth-bound kernels of the path, outside the
+    timed region, each on the workload's own data: algorithmic bytes per launch (bytes the op
+    must read + write) / average launch time (wall clock over `reps` back-to-back
+    launches on the context stream, synchronised; launch overhead included), and the fraction
+    of the 8 TB/s HBM3E peak. `pmc_bytes_per_dispatch`: the same kernel's FETCH_SIZE x2 +
+    WRITE_SIZE per dispatch in the round's rocprofv3 pass over the bench (bench_traffic.json),
+    where it ran on the bench's own launch sizes."""
+    import ctypes as C
+    from person_capture_amd import imageops
+    from person_capture_amd._lib import PC_PREC_F16, LetterboxDesc, WarpDesc, check
+    from person_capture_amd.engines import make_letterbox_desc
+    from person_capture_amd.face_embedder import dev_resize
+    ctx = fe._ctx
+    lib, h = ctx.lib, ctx.handle
+    traffic = {}
+    try:
+        traffic = json.load(open(os.path.join(ROOT, "bench_traffic.json"))).get("per_kernel", {})
+    except Exception:
+        pass
+
+    def pmc(substr):
+        for name, c in traffic.items():
+            if substr in name and "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+                return round(2048.0 * c["FETCH_SIZE"]["mean_kib"] + 1024.0 * c["WRITE_SIZE"]["mean_kib"])
+        return None
+
+    def timed(fn):
+        fn()
+        ctx.sync()
+        t = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        ctx.sync()
+        return (time.perf_counter() - t) / reps
+
+    def entry(kernel, per_launch, nbytes, sec, what, pmc_key):
+        gbps = nbytes / sec / 1e9
+        return {"kernel": kernel, "launch": per_launch, "algorithmic_bytes_per_launch": int(nbytes),
+                "bytes": what, "avg_launch_us": round(sec * 1e6, 2), "achieved_gbps": round(gbps, 1),
+                "peak_gbps": PEAK_HBM_GBPS, "frac": round(gbps / PEAK_HBM_GBPS, 4),
+                "pmc_bytes_per_dispatch": pmc(pmc_key)}
+
+    out = {}
+    n, D = min(32, len(devs)), 640
+    if "resize_area" in kinds:   # the pre-scan downscale (gui_app.py:1505-1507): 4K -> 416 wide
+        k = devs[0]
+        nh = int(round(k.H * (416 / float(k.W))))
+        sec = timed(lambda: dev_resize(ctx, k, "hbm_area", (416, nh), 0.0, 0.0, True))
+        out["resize_area_u8"] = entry("resize_area_u8 (pc_image.hip)", f"1 frame {k.H}x{k.W} -> {nh}x416 INTER_AREA",
+                                      k.H * k.W * 3 + nh * 416 * 3, sec, "4K frame + 416-wide output", "resize_area")
+    if "letterbox" not in kinds:
+        return out
+    # letterbox_blob: a 32-frame detection chunk, 1080p -> 640 f16 NHWC4 blob
+    descs = (LetterboxDesc * n)(*[make_letterbox_desc(d.ptr, d.H, d.W, d.stride, D)[0] for d in devs[:n]])
+    blob = ctx.scratch("hbm_letterbox", n * D * D * 4 * 2)
+    sec = timed(lambda: check(lib.pc_letterbox(h, PC_PREC_F16, descs, n, D, C.c_void_p(blob.ptr)), h, "letterbox"))
+    out["letterbox_blob"] = entry("letterbox_blob (pc_image.hip)", f"{n} frames {H}x{W} -> {D}x{D}x4 f16",
+                                  n * (H * W * 3 + D * D * 4 * 2), sec, "source frame + blob", "letterbox")
+    # warp_affine_u8: one ArcFace quantum of chips (146 faces) from the 1080p frames, ~100 px faces -> 112x112
+    m = 146
+    chips = ctx.scratch("hbm_chips", m * 112 * 112 * 3)
+    ws = []
+    for i in range(m):
+        d = devs[i % len(devs)]
+        x0, y0 = 40 + (i * 97) % (W - 200), 40 + (i * 61) % (H - 200)
+        M = np.array([[1.12, 0.05, -1.12 * x0], [-0.05, 1.12, -1.12 * y0]], np.float64)
+        ws.append(imageops.warp_desc(d.ptr, d.stride, W, H, M.reshape(-1), chips.ptr + i * 112 * 112 * 3))
+    warr = (WarpDesc * m)(*ws)
+    sec = timed(lambda: check(lib.pc_warp_affine(h, warr, m), h, "warp_affine"))
+    out["warp_affine_u8"] = entry("warp_affine_u8 (pc_image.hip)", f"{m} chips 112x112 from 1080p frames",
+                                  m * 2 * 112 * 112 * 3, sec, "chip written + ~the same source pixels read",
+                                  "warp_affine")
+    # the SCRFD stem max pool (3x3/s2 over the split stem output) inside a 32-frame detection chunk:
+    # its HIP-event time from the net profile, bytes from the program's tensors
+    eng = fe._engine(640)
+    P = eng.program
+    mp = [w for w in P.ops if w[0] == 3][0]
+    ti, to = P.tensors[mp[2]], P.tensors[mp[1]]
+    nbytes = n * 2 * (ti[1] * ti[2] * ti[4] + to[1] * to[2] * to[4])
+    eng.net.profile(True)
+    for _ in range(3):
+        eng.detect_frames([(d.ptr, d.H, d.W, d.stride) for d in devs[:n]], thresh=fe.conf)
+    recs = [r for r in eng.net.profile_ops() if int(r[1]) == 3]
+    eng.net.profile(False)
+    if recs:
+        sec = sum(r[2] for r in recs) * 1e-3 / len(recs)
+        out["maxpool"] = entry("maxpool_split_f16x8 / maxpool_nhwc_f16x8 (pc_conv.hip)",
+                               f"{n} frames {ti[1]}x{ti[2]}x{ti[3]} -> {to[1]}x{to[2]}x{to[3]} f16"
+                               + (" (split hi|lo)" if P.tsplit[mp[2]] else ""), nbytes, sec,
+                               "input + output activations (HIP events)", "maxpool")
     return out
 
 
@@ -200,7 +338,9 @@ def f16_parity(fe16, devs, bank_h, conf: float = 0.5) -> dict:
                 near.append(round(abs(float(b["fd"]) - 0.32), 5))
             acc_mis_45 += (a["fd"] <= 0.45) != (b["fd"] <= 0.45)
     kps_d = np.array(kps_d) if kps_d else np.zeros(1)
-    return {"reference": "same frames, f32 parity mode on the device", "faces_f32": n,
+    far = sum(1 for d in near if d > 1e-3)
+    return {"reference": "same frames, f32 parity mode on the device", "faces_f32": n, "_res32": res32,
+            "_res16": res16, "accept_mismatch_0.32_outside_0.001_band": far,
             "face_count_mismatch": count_mis, "box_mismatch": box_mis, "accept_mismatch_0.32": acc_mis,
             "accept_mismatch_0.45": acc_mis_45, "accept_mismatch_frac_0.32": round(acc_mis / max(1, n), 4),
             "max_fd_diff": round(worst_fd, 6), "flipped_faces_f32_distance_to_0.32": sorted(near),
@@ -241,6 +381,8 @@ def smooth_parity(fe16, frames: np.ndarray, bank_rows: int) -> dict:
     finally:
         fe16.conf = conf0
     r.pop("flipped_faces_f32_distance_to_0.32", None)
+    r.pop("_res32", None)
+    r.pop("_res16", None)
     r["frames"] = "bench frames, Gaussian sigma 1.5 px, contrast x2.5 about 127.5; SCRFD conf 0.8"
     ctx.sync()
     d.free()
@@ -310,6 +452,8 @@ def main():
     ap.add_argument("--bank", type=int, default=32)
     ap.add_argument("--cpu-sample", type=int, default=48)
     ap.add_argument("--cpu-sample-1t", type=int, default=4)
+    ap.add_argument("--c5-samples", type=int, default=256,
+                    help="C5: samples of the one clip whose positions are sharded over the ranks (strong scaling)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-parity", action="store_true", help="skip the f16-vs-f32 decision parity pass")
     ap.add_argument("--precision", default="f16", choices=["f16", "f32"])
@@ -351,7 +495,7 @@ def main():
     os.environ.setdefault("PERSON_CAPTURE_AMD_PRECISION", args.precision)
     os.environ.setdefault("PERSON_CAPTURE_AMD_DET_BATCH", str(args.batch))
     os.environ.setdefault("PERSON_CAPTURE_AMD_ARC_BATCH", "512")
-    from person_capture_amd._lib import PC_PREC_F32
+    from person_capture_amd._lib import PC_PREC_F16X3, PC_PREC_F32
     from person_capture_amd.face_embedder import FaceEmbedder, _DevImage
     from person_capture_amd.match import DeviceBank, fd_min
 
@@ -457,7 +601,7 @@ def main():
                                            "host fd"}[args.frames],
                    "faces_per_frame": round(nfaces / args.batch, 3), "accepted_faces_per_step": accept,
                    "accepted_faces_per_step_cli_0.32": accept_cli, "bank_planted_rows": n_plant,
-                   "detector_dtype": "f32" if fe.det_precision == PC_PREC_F32 else "f16",
+                   "detector_dtype": {PC_PREC_F32: "f32", PC_PREC_F16X3: "f16x3"}.get(fe.det_precision, "f16"),
                    "parallelism": f"frame-shard x{world} (no collective)"},
         "roofline": {"bound": "mfma", "achieved": dom["achieved_tflops"], "peak": peak, "unit": "TFLOP/s",
                      "frac": round(dom["achieved_tflops"] / peak, 4),
@@ -484,40 +628,64 @@ def main():
                      "dominant_kernel_rocprof": dominant},
         "cpu_baseline": None,
     }
+    res32 = res16 = None
     if rank == 0 and args.precision == "f16" and not args.no_parity and args.frames == "resident" and \
             fe.detector_backend == "scrfd":
         out["parity"] = f16_parity(fe, devs, bank_h)
-        # the same pipeline with the detector in f32 (PERSON_CAPTURE_AMD_DET_PRECISION=f32): f32
-        # landmarks give the f32 chips; its throughput and decisions, measured here too
-        old_dp = os.environ.get("PERSON_CAPTURE_AMD_DET_PRECISION")
-        os.environ["PERSON_CAPTURE_AMD_DET_PRECISION"] = "f32"
-        try:
-            fe_d = FaceEmbedder(ctx=f"cuda:{local}", yolo_model="scrfd_10g_bnkps", conf=0.5)
-        finally:
-            if old_dp is None:
-                os.environ.pop("PERSON_CAPTURE_AMD_DET_PRECISION", None)
-            else:
-                os.environ["PERSON_CAPTURE_AMD_DET_PRECISION"] = old_dp
-        run_d = lambda: fe_d.extract_batch([None] * args.batch, dev_frames=devs, bank=bank)
-        run_d()
-        fe_d._ctx.sync()
-        t0 = time.perf_counter()
-        for _ in range(3):
+        res32, res16 = out["parity"].pop("_res32"), out["parity"].pop("_res16")
+        out["parity"]["timed_mode"] = "SCRFD " + out["config"]["detector_dtype"] + " + ArcFace f16"
+
+        # the same pipeline with the detector in another precision: its throughput and decisions
+        # (f32: the f32 SCRFD kernels, chips identical to the f32 mode's; f16: plain f16 SCRFD,
+        # the round-3 headline, whose sub-pixel landmark shifts flip decisions on noise frames)
+        def alt_mode(dp):
+            old_dp = os.environ.get("PERSON_CAPTURE_AMD_DET_PRECISION")
+            os.environ["PERSON_CAPTURE_AMD_DET_PRECISION"] = dp
+            try:
+                fe_d = FaceEmbedder(ctx=f"cuda:{local}", yolo_model="scrfd_10g_bnkps", conf=0.5)
+            finally:
+                if old_dp is None:
+                    os.environ.pop("PERSON_CAPTURE_AMD_DET_PRECISION", None)
+                else:
+                    os.environ["PERSON_CAPTURE_AMD_DET_PRECISION"] = old_dp
+            run_d = lambda: fe_d.extract_batch([None] * args.batch, dev_frames=devs, bank=bank)
             run_d()
-        fe_d._ctx.sync()
-        fe_d._ectx.sync()
-        fps_d = 3 * args.batch / (time.perf_counter() - t0)
-        pd = f16_parity(fe_d, devs, bank_h)
-        out["parity"]["detector_f32_mode"] = {
-            "frames_per_s": round(fps_d, 2), "steps": 3,
-            **{k: pd[k] for k in ("face_count_mismatch", "box_mismatch", "accept_mismatch_0.32",
-                                  "accept_mismatch_0.45", "accept_mismatch_frac_0.32", "max_fd_diff")},
-            "chips_identical": pd["attribution"]["chips_identical"],
-            "note": "SCRFD f32 + ArcFace f16 (env PERSON_CAPTURE_AMD_DET_PRECISION=f32): identical chips, the "
-                    "remaining flips are the f16 ArcFace's"}
+            fe_d._ctx.sync()
+            t0 = time.perf_counter()
+            for _ in range(3):
+                run_d()
+            fe_d._ctx.sync()
+            fe_d._ectx.sync()
+            fps_d = 3 * args.batch / (time.perf_counter() - t0)
+            pd = f16_parity(fe_d, devs, bank_h)
+            return {"frames_per_s": round(fps_d, 2), "steps": 3,
+                    **{k: pd[k] for k in ("face_count_mismatch", "box_mismatch", "accept_mismatch_0.32",
+                                          "accept_mismatch_0.45", "accept_mismatch_frac_0.32", "max_fd_diff",
+                                          "accept_mismatch_0.32_outside_0.001_band")},
+                    "chips_identical": pd["attribution"]["chips_identical"]}
+
+        out["parity"]["detector_f32_mode"] = dict(alt_mode("f32"), note=(
+            "SCRFD f32 + ArcFace f16 (PERSON_CAPTURE_AMD_DET_PRECISION=f32): the f32 mode's SCRFD kernels, identical "
+            "chips; the remaining differences are the f16 ArcFace's"))
+        out["parity"]["detector_f16_mode"] = dict(alt_mode("f16"), note=(
+            "plain f16 SCRFD + ArcFace f16 (PERSON_CAPTURE_AMD_DET_PRECISION=f16, the round-3 headline)"))
+        out["parity"]["timed_mode_speedup_vs_detector_f32_mode"] = round(
+            value / out["parity"]["detector_f32_mode"]["frames_per_s"], 3)
         out["parity"]["smooth_frames"] = smooth_parity(fe, frames, args.bank)
+    if rank == 0 and args.frames == "resident" and not args.no_parity:
+        out["hbm"] = hbm_kernels(fe, devs, 1080, 1920)
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(frames, fe, bank_h, args.cpu_sample, args.cpu_sample_1t)
+        oracle_res = out["cpu_baseline"].pop("_oracle_results")
+        if res16 is not None:
+            # the north star's reference: the CPU path itself (oracle port, fp32 torch SCRFD + ArcFace,
+            # 0-degree frames) on the sample frames, against the timed mode and the device f32 mode
+            out["parity"]["cpu_oracle"] = {
+                "frames": len(oracle_res), "frames_needing_fallback_skipped": sum(r is None for r in oracle_res),
+                "timed_mode": compare_faces(res16[:len(oracle_res)], oracle_res),
+                "device_f32_mode": compare_faces(res32[:len(oracle_res)], oracle_res),
+                "note": "the oracle (oracle/pipeline.extract_frame) is the checker here; both device modes are "
+                        "compared with it face by face (nearest box)"}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -554,7 +722,8 @@ def main_c2(args):
     B = 256
     ctx = GpuContext(local)
     prec = PC_PREC_F16 if args.precision == "f16" else PC_PREC_F32
-    eng = ArcFaceEngine(ctx, models.synth_iresnet(100, seed=0), 100, precision=prec, max_batch=2 * B)
+    arc_params = models.synth_iresnet(100, seed=0)
+    eng = ArcFaceEngine(ctx, arc_params, 100, precision=prec, max_batch=2 * B)
     chips = np.random.default_rng(20260505 + rank).integers(0, 256, (B, 112, 112, 3), dtype=np.uint8)
     d_chips = ctx.upload(chips)
     d_out = ctx.alloc(B * eng.dim * 4)
@@ -602,6 +771,8 @@ def main_c2(args):
                      "tflops": round(2 * fl / (t_flip / args.steps) / 1e12, 2)},
         "cpu_baseline": None,
     }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline_c2(arc_params, chips, 16)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -637,70 +808,105 @@ def main_dry(args):
 
 
 def main_other(args):
-    """C4 (full path) and C5 (4K pre-scan): secondary workloads, same JSON contract."""
+    """C4 (full path) and C5 (4K pre-scan of one clip, sharded over the ranks): secondary
+    workloads, same JSON contract."""
     world, rank, local = _dist_init()
     local = _device(local)
     os.environ.setdefault("PERSON_CAPTURE_AMD_PRECISION", args.precision)
     os.environ.setdefault("PERSON_CAPTURE_AMD_DET_BATCH", str(args.batch))
     os.environ.setdefault("PERSON_CAPTURE_AMD_ARC_BATCH", "512")
-    from person_capture_amd._lib import PC_PREC_F32
     from person_capture_amd.face_embedder import FaceEmbedder, _DevImage
     from person_capture_amd.match import DeviceBank
 
     fe = FaceEmbedder(ctx=f"cuda:{local}", yolo_model="scrfd_10g_bnkps", conf=0.5)
     ctx = fe._ctx
-    H, W = (1080, 1920) if args.workload == "c4" else (2160, 3840)
-    frames = synth_frames(rank, args.batch, H, W)
+    c4 = args.workload == "c4"
+    H, W = (1080, 1920) if c4 else (2160, 3840)
+    # C5: every rank holds the same clip (one clip sharded over the ranks); C4: per-rank frames
+    frames = synth_frames(rank if c4 else 0, args.batch, H, W)
     dframes = ctx.alloc(frames.nbytes)
     ctx.upload(frames, dframes)
     fsz = frames[0].nbytes
     devs = [_DevImage(dframes.ptr + i * fsz, H, W, W * 3) for i in range(args.batch)]
-    bank_n = args.bank if args.workload == "c4" else 1024
-    bank = DeviceBank(ctx, synth_bank(bank_n))
+    bank_n = args.bank if c4 else 1024
+    bank_h = synth_bank(bank_n)
+    bank = DeviceBank(ctx, bank_h)
     stats = {}
     nets = [fe._arc.net]
-    if args.workload == "c4":
+    units_per_step = args.batch
+    scaling = "weak"
+    if c4:
         from person_capture_amd.detectors import PersonDetector
         from person_capture_amd.reid_embedder import ReIDEmbedder
         det = PersonDetector("yolov8n.pt", device=f"cuda:{local}")
-        # the untrained synthetic SCRFD fires on ~150 anchors of a bilinearly upscaled person crop
-        # at 0.5 (it was calibrated on native-scale frames); 0.75 gives a few faces per crop as a
-        # trained detector would. Real weights need no such knob.
-        fe.conf = 0.75
         reid = ReIDEmbedder(device=f"cuda:{local}")
         stats["reid_dtype"] = "f32" if reid._engine.net.precision == 1 else "f16"
         dtuples = [(d.ptr, H, W, W * 3) for d in devs]
 
-        def step():
-            persons = det.detect_device(dtuples, conf=0.35)
+        def person_crops():
             crops = []
-            for d, dets in zip(devs, persons):
+            for d, dets in zip(devs, det.detect_device(dtuples, conf=0.35)):
                 for x1, y1, x2, y2, _ in dets:   # main.py:231-236
                     x1, y1 = max(0, int(x1)), max(0, int(y1))
                     x2, y2 = min(W - 1, int(x2)), min(H - 1, int(y2))
                     if x2 <= x1 + 2 or y2 <= y1 + 2:
                         continue
                     crops.append(_DevImage(d.ptr + y1 * d.stride + x1 * 3, y2 - y1, x2 - x1, d.stride))
+            return crops
+
+        # The untrained synthetic SCRFD fires on many anchors of a bilinearly upscaled person crop
+        # (calibrated on native-scale frames). A trained detector finds the 1-2 faces a person crop
+        # holds, so the per-crop face threshold is calibrated once, before timing, to the lowest of
+        # a fixed ladder that gives 1-4 faces per crop on these frames. Real weights need no knob.
+        crops0 = person_crops()
+        # kept detections at a higher threshold = the kept set at 0.75 filtered by score (greedy NMS:
+        # only higher-scoring boxes suppress), so one detection pass over the crops gives the ladder
+        eng = fe._engine(640)
+        scores = []
+        for i in range(0, len(crops0), eng.max_batch):
+            part = crops0[i:i + eng.max_batch]
+            for dets, _ in eng.detect_frames([(c.ptr, c.H, c.W, c.stride) for c in part], thresh=0.75):
+                scores.extend(float(v) for v in dets[:, 4])
+        scores = np.sort(np.asarray(scores))[::-1]
+        conf_used = 0.75
+        for c in (0.75, 0.85, 0.9, 0.95, 0.97, 0.98, 0.99, 0.995, 0.998, 0.999):
+            conf_used = c
+            if int((scores >= c).sum()) <= 4 * max(1, len(crops0)):
+                break
+        fe.conf = conf_used
+        print(f"[bench c4] {len(crops0)} person crops; face threshold calibrated to {conf_used} "
+              f"({int((scores >= conf_used).sum())} detections at it)", file=sys.stderr, flush=True)
+        stats["face_conf_calibrated"] = conf_used
+
+        def step():
+            crops = person_crops()
             faces = fe.extract_batch([None] * len(crops), dev_frames=crops, bank=bank) if crops else []
             feats = reid.extract_device([(c.ptr, c.H, c.W, c.stride) for c in crops])
             stats["persons"] = len(crops)
             stats["faces"] = sum(len(f) for f in faces)
+            stats["faces_per_crop"] = round(stats["faces"] / max(1, len(crops)), 3)
             return feats
         nets += [fe._engine(640).net, reid._engine.net]
         wl = (f"C4: YOLOv8n persons + SCRFD-10G@640 per person crop + ArcFace-R100 flip-TTA + CLIP ViT-L/14 ReID "
               f"per crop + match vs {bank_n}-embedding bank, 1080p, batch {args.batch} frames per GPU")
     else:
-        # the pre-scan driver (Processor._prescan's sampling loop, person_capture_amd/prescan.py):
-        # the resident 4K frames are the sampled frames of a clip at stride 24 (gui_app.py:555),
-        # downscaled to 416 wide on the device, fast pre-scan SCRFD + ArcFace, fd against the
-        # 1024-row bank, bank growth and span hysteresis replayed in sample order
+        # the pre-scan driver (Processor._prescan's sampling loop) over ONE clip of c5_samples samples at
+        # stride 24 (gui_app.py:555), the clip's sample positions sharded over the ranks
+        # (prescan_shard.run_sharded: speculation per rank, rank-0 replay with re-extraction of
+        # misses, the single-stream spans and bank): strong scaling. The resident 4K frames are the
+        # clip's sampled frames (cycled), downscaled to 416 wide on the device.
         from person_capture_amd.prescan import PrescanConfig, PrescanRunner
+        from person_capture_amd.prescan_shard import run_sharded
         pcfg = PrescanConfig()
         stride = pcfg.prescan_stride
-        bank_h = synth_bank(bank_n)
+        S = args.c5_samples
+        units_per_step = S
+        scaling = "strong"
+        total = S * stride
+        at = lambda idx: devs[(idx // stride) % len(devs)]
         # plant a quarter of the bank from faces of the first samples (downscaled as the driver
         # does) so spans open and the escalated two-forward path is timed too
-        r0 = PrescanRunner(fe, pcfg, 30.0, args.batch * stride, ref_feat=None, batch=args.batch)
+        r0 = PrescanRunner(fe, pcfg, 30.0, total, ref_feat=None, batch=args.batch)
         ims = [r0._downscale(devs[i], i) for i in range(min(16, len(devs)))]
         fe.set_prescan_fast(True, mode="rr")
         seed_res = fe.extract_batch([None] * len(ims), dev_frames=ims)
@@ -708,22 +914,26 @@ def main_other(args):
         stats["bank_planted_rows"] = plant_bank(seed_res, bank_h)
 
         def step():
-            r = PrescanRunner(fe, pcfg, 30.0, args.batch * stride, ref_feat=bank_h, batch=args.batch)
-            spans, _ = r.run(lambda idx: devs[idx // stride])
-            stats["faces"] = sum(x.n_faces for x in r.records)
-            stats["extracted_samples"] = sum(1 for x in r.records if x.extracted)
-            stats["driver_chunks"], stats["driver_cuts"], stats["spans"] = r.chunks, r.cuts, len(spans)
-            return spans
-        wl = (f"C5: pre-scan driver over 4K frames sampled at stride {stride} -> INTER_AREA 416 wide, fast pre-scan "
-              f"SCRFD-10G, ArcFace-R100 (1 forward, 2 while a span is active), fd vs {bank_n}-embedding bank, "
-              f"batch {args.batch} samples per GPU")
+            r = run_sharded(fe, pcfg, 30.0, total, at, ref_feat=bank_h, batch=args.batch, rank=rank, world=world)
+            if r is not None:
+                spans, _, recs, ms = r
+                stats["faces"] = sum(x.n_faces for x in recs)
+                stats["extracted_samples"] = sum(1 for x in recs if x.extracted)
+                stats["spans"] = len(spans)
+                stats["merge"] = {"reused": ms.reused, "reextracted_on_rank0": ms.reextracted,
+                                  "skipped": ms.skipped, "speculated_per_rank": ms.per_rank_spec}
+            return r
+        wl = (f"C5: pre-scan of one clip of {S} samples at stride {stride} (4K frames -> INTER_AREA 416 wide, "
+              f"fast pre-scan SCRFD-10G, ArcFace-R100 1 forward / 2 while a span is active, fd vs a {bank_n}-embedding "
+              f"bank, bank growth and span hysteresis), sample positions sharded over {world} rank(s) with the "
+              f"single-stream result (rank-0 replay)")
     for k in range(args.warmup):
         t = time.perf_counter()
         step()
         ctx.sync()
         print(f"[bench {args.workload}] warmup {k}: {time.perf_counter() - t:.3f} s {stats}", file=sys.stderr,
               flush=True)
-    if args.workload == "c5":
+    if not c4:
         nets += [e.net for e in fe._scrfd_engines.values()]
     for n in nets:
         n.profile(True)
@@ -735,29 +945,131 @@ def main_other(args):
     conv_flops = sum(p["conv_flops"] for p in prof)
     conv_launches = sum(p["conv_launches"] for p in prof)
     achieved = conv_flops / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
+    # per-net roofline at its own dtype's peak (the ReID tower runs f32 like the reference: 157 TF/s)
+    names = ["arcface"] + (["scrfd", "reid"] if c4 else [f"scrfd{i}" for i in range(len(nets) - 1)])
+    per_net = {}
+    for nm, n, p_ in zip(names, nets, prof):
+        if p_["conv_ms"] <= 0:
+            continue
+        f32 = n.precision == 1
+        tf = p_["conv_flops"] / (p_["conv_ms"] * 1e-3) / 1e12
+        pk = PEAK_F32_TFLOPS if f32 else PEAK_F16_TFLOPS
+        per_net[nm] = {"dtype": "f32" if f32 else "f16", "conv_ms_per_step": round(p_["conv_ms"] / args.steps, 3),
+                       "achieved_tflops": round(tf, 1), "peak": pk, "frac": round(tf / pk, 4)}
     peak = PEAK_F16_TFLOPS if args.precision == "f16" else PEAK_F32_TFLOPS
-    total_frames = _sum_over_ranks(world, args.batch * args.steps)
+    total_units = units_per_step * args.steps if scaling == "strong" else _sum_over_ranks(world, units_per_step *
+                                                                                           args.steps)
     out = {
-        "metric": "frames/sec detect+embed+match @1080p, 1/2/4/8 GPU; MFMA util %" if args.workload == "c4"
+        "metric": "frames/sec detect+embed+match @1080p, 1/2/4/8 GPU; MFMA util %" if c4
         else "frames/sec pre-scan detect+embed+match @4K, 1/2/4/8 GPU; MFMA util %",
-        "value": round(total_frames / elapsed, 3), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
+        "value": round(total_units / elapsed, 3), "unit": "frames/s" if c4 else "samples/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": args.precision,
         "data": "synthetic (seeded u8 frames, seeded synthetic weights of every net)",
-        "config": {"workload": wl, "frames_per_step_per_gpu": args.batch, "bank": bank_n,
-                   **{k: v for k, v in stats.items()}, "parallelism": f"frame-shard x{world} (no collective)"},
+        "config": {"workload": wl, ("frames_per_step_per_gpu" if c4 else "samples_per_clip"): units_per_step,
+                   "bank": bank_n, **{k: v for k, v in stats.items()},
+                   "parallelism": f"frame-shard x{world} (no collective)" if c4 else
+                   f"sample-position shard x{world}, host gather + rank-0 replay (no device collective)"},
         "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": None,
                      "kernel": "implicit-GEMM MFMA convs (all nets, ViT linears as 1x1)", "launches": conv_launches,
                      "avg_launch_us": round(conv_ms * 1e3 / max(1, conv_launches), 2),
-                     "conv_share_of_step": round(conv_ms * 1e-3 / local_dt, 4)},
+                     "conv_share_of_step": round(conv_ms * 1e-3 / local_dt, 4), "per_net": per_net},
         "cpu_baseline": None,
     }
+    if rank == 0 and not c4 and not args.no_parity:
+        out["hbm"] = hbm_kernels(fe, devs, H, W, kinds=("resize_area",))
+    if rank == 0 and world == 1 and not args.no_cpu:
+        print(f"[bench {args.workload}] CPU baseline (oracle port) ...", file=sys.stderr, flush=True)
+        out["cpu_baseline"] = cpu_baseline_c4(frames, fe, det, bank_h) if c4 else \
+            cpu_baseline_c5(frames, fe, bank_h, stride)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+
+
+def cpu_baseline_c2(params, chips: np.ndarray, n: int) -> dict:
+    """The oracle's fp32 torch-CPU IResNet-100 (+ L2) on a bounded sample of the C2 chips."""
+    import torch
+    from oracle import nets_torch as nt
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    x = nt.arcface_input_from_chips(chips[:n])
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        nt.iresnet_forward(params, 100, x)
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 3), "unit": "faces/s", "cores": threads, "kind": "port",
+            "host_cpu_count": os.cpu_count(),
+            "sample": f"{n} of the C2 chips through oracle/nets_torch.iresnet_forward (fp32 torch CPU, one batch), "
+                      f"{dt:.1f} s at {threads} threads"}
+
+
+def cpu_baseline_c4(frames: np.ndarray, fe, det, bank: np.ndarray, max_crops: int = 4) -> dict:
+    """The oracle chain of C4 on the host cores for one frame: YOLOv8n person heads + postprocess,
+    the person crops' SCRFD + ArcFace branch (OracleFaceEmbedder, same calibrated threshold),
+    ViT-L/14 ReID of each crop, fd against the bank. Bounded sample: the frame's first crops."""
+    import torch
+    from oracle import nets_torch as nt
+    from oracle import pipeline as op
+    from oracle import ref_algos as ra
+    from person_capture_amd.reid_embedder import clip_weights
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    frame = frames[0]
+    H, W = frame.shape[:2]
+    o = op.OracleFaceEmbedder(fe._scrfd_params, fe.scrfd_variant, fe._arc_params, fe._arc_depth, conf=fe.conf)
+    cw = clip_weights("ViT-L-14", 0)
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        canvas, (_, _, _, _, Hp, Wp) = ra.yolo_letterbox(frame)
+        x = torch.from_numpy(np.ascontiguousarray(canvas[None].transpose(0, 3, 1, 2)))
+        heads = [t[0].numpy() for t in nt.yolov8_forward(det._params, "n", x)]
+        persons = ra.yolo_postprocess(heads, 0.35, 0.45, 40, Hp, Wp, H, W)
+        crops = []
+        for p in persons:
+            x1, y1 = max(0, int(p[0])), max(0, int(p[1]))
+            x2, y2 = min(W - 1, int(p[2])), min(H - 1, int(p[3]))
+            if x2 > x1 + 2 and y2 > y1 + 2:
+                crops.append(frame[y1:y2, x1:x2])
+        crops = crops[:max_crops]
+        faces = 0
+        for c in crops:
+            for f in o.extract(c):
+                ra.fd_min(f["feat"], bank)
+                faces += 1
+        if crops:
+            nt.clip_vit_forward(cw, "ViT-L-14", torch.stack([nt.clip_preprocess_pil(c) for c in crops]))
+    dt = time.perf_counter() - t0
+    per_frame = dt / max(1, len(crops)) * max(1, len(persons))   # scaled to all of the frame's persons
+    return {"value": round(1.0 / per_frame, 4), "unit": "frames/s", "cores": threads, "kind": "port",
+            "host_cpu_count": os.cpu_count(),
+            "sample": f"frame 0: YOLOv8n oracle + {len(crops)} of its {len(persons)} person crops (SCRFD-10G + "
+                      f"ArcFace-R100 oracle branch, {faces} faces; ViT-L/14 fp32) in {dt:.1f} s at {threads} threads, "
+                      f"scaled to the frame's {len(persons)} crops"}
+
+
+def cpu_baseline_c5(frames: np.ndarray, fe, bank: np.ndarray, stride: int, n: int = 6) -> dict:
+    """The oracle pre-scan loop (oracle/prescan.prescan over OracleFaceEmbedder: INTER_AREA to 416,
+    fast pre-scan SCRFD + ArcFace, bank, hysteresis) on the host cores, a bounded clip of n samples."""
+    import torch
+    from oracle import pipeline as op
+    from oracle import prescan as oprescan
+    from person_capture_amd.prescan import PrescanConfig
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    o = op.OracleFaceEmbedder(fe._scrfd_params, fe.scrfd_variant, fe._arc_params, fe._arc_depth, conf=0.5)
+    t0 = time.perf_counter()
+    _, _, recs = oprescan.prescan(o, PrescanConfig(), 30.0, n * stride, lambda idx: frames[(idx // stride) % len(frames)],
+                                  ref_feat=bank)
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 4), "unit": "samples/s", "cores": threads, "kind": "port",
+            "host_cpu_count": os.cpu_count(),
+            "sample": f"a {n}-sample clip of the bench's 4K frames through oracle/prescan.prescan "
+                      f"({sum(1 for r in recs if r[1])} extracted, {sum(r[3] for r in recs)} faces), {dt:.1f} s at "
+                      f"{threads} threads"}
 
 
 if __name__ == "__main__":

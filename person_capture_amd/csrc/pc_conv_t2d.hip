@@ -42,9 +42,12 @@ __device__ __forceinline__ void t2d_read_frags(const char* a0, f16x8* fb, std::i
 // NBUF 3: three halo buffers, block i+2's halo is requested while block i is multiplied (the
 // DMA of one block of small TH does not hide behind one block's K loop).
 // SPLIT (f16x3 detector): the input is a split tensor [hi | lo] (NCH physical
-// chunks = 2 x the logical ones), each tap walks the virtual chunks [hi, lo, hi] against the
-// weights [W_hi, W_hi, W_lo] held in registers (3/2 x the K steps of the physical halo), the
-// residual is read as hi + lo and the output is written split.
+// chunks = 2 x the logical ones). Per tap and logical chunk j the wave reads the two B
+// fragments (hi: chunk j, lo: chunk NCC + j) once and issues W_hi*hi, W_lo*hi, W_hi*lo, with
+// W_hi and W_lo each held once in registers (the weight rows are packed [W_hi, W_hi, W_lo] per
+// tap for the implicit-GEMM kernels' virtual K; the duplicate is not loaded). The residual is
+// read as hi + lo and the output is written split. (Accumulation order: per chunk, not the
+// implicit-GEMM kernels' [hi, lo, hi] blocks: equal to them at f32 class, not bitwise.)
 template <int NCH, int G, int NW, int TP, int NBUF = 2, bool SPLIT = false>
 __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, int ntx, int ntiles) {
   constexpr int TW = 16, P = 24, TC = 2;
@@ -53,8 +56,8 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, in
   constexpr int NINST = NRP / 16;             // DMA instructions per chunk
   constexpr int BUFB = NCH * NRP * 64;        // one halo buffer
   static_assert(!SPLIT || NCH % 2 == 0, "split halo: hi and lo chunks");
-  constexpr int NV = SPLIT ? NCH / 2 * 3 : NCH;   // virtual 32-channel chunks per tap
-  constexpr int NKS = 9 * NV;                 // 32-element K steps
+  constexpr int NCC = SPLIT ? NCH / 2 : NCH;  // logical 32-channel chunks
+  constexpr int NKS = 9 * NCC;                // K steps (split: each is 3 MFMA products)
   constexpr int NPAD_T = 32 * G;
   constexpr int TB = 10 * NPAD_T;             // bias classes [9][npad] + slopes [npad] (f32)
   static_assert(NRP % 16 == 0 && P % 8 == 0 && P >= TW + 2 && (TP == 4 || TP == 8), "halo geometry");
@@ -162,14 +165,25 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, in
   }
 
   // weights -> registers: A fragment (ks, a) = rows g*32 + a*16 + fr, K ks*32 + fq*8 .. +7
+  // (split: step ks = tap*NCC + j holds W_hi of virtual chunk tap*3NCC + j in wa and W_lo of
+  // virtual chunk tap*3NCC + 2NCC + j in wl)
   f16x8 wa[NKS][TC];
+  f16x8 wl[SPLIT ? NKS : 1][TC];
   {
     const char* wb = reinterpret_cast<const char*>(p.w);
 #pragma unroll
     for (int a = 0; a < TC; ++a) {
       const char* row = wb + (long long)(g * 32 + a * 16 + fr) * p.ktot * 2 + fq * 16;
 #pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) wa[ks][a] = *reinterpret_cast<const f16x8*>(row + ks * 64);
+      for (int ks = 0; ks < NKS; ++ks) {
+        if constexpr (SPLIT) {
+          const int tap = ks / NCC, j = ks - tap * NCC;
+          wa[ks][a] = *reinterpret_cast<const f16x8*>(row + (tap * 3 * NCC + j) * 64);
+          wl[ks][a] = *reinterpret_cast<const f16x8*>(row + (tap * 3 * NCC + 2 * NCC + j) * 64);
+        } else {
+          wa[ks][a] = *reinterpret_cast<const f16x8*>(row + ks * 64);
+        }
+      }
     }
     // retire the weight loads here, visibly to the compiler: otherwise its wait for them
     // lands before the first MFMA inside the block loop as a vmcnt(0), which would also
@@ -177,7 +191,10 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, in
 #pragma unroll
     for (int a = 0; a < TC; ++a)
 #pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) asm volatile("" : "+v"(wa[ks][a]));
+      for (int ks = 0; ks < NKS; ++ks) {
+        asm volatile("" : "+v"(wa[ks][a]));
+        if constexpr (SPLIT) asm volatile("" : "+v"(wl[ks][a]));
+      }
   }
 
   auto bar = [&]() __attribute__((always_inline)) {
@@ -269,20 +286,25 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, in
     // MFMAs (two fragment sets live; the schedule is pinned so the compiler does not
     // hoist every read of the block and spill the weight registers).
     f16x8 fb0[TP], fb1[TP];
+    f16x8 fl0[SPLIT ? TP : 1], fl1[SPLIT ? TP : 1];   // split: the lo-chunk fragments
     if (!(p.dbg & 2)) static_for<NKS + 1>([&](auto ksc) __attribute__((always_inline)) {
       constexpr int ks = decltype(ksc)::value - 1;   // -1: prologue read of step 0
       f16x8(&cur_f)[TP] = (ks & 1) ? fb1 : fb0;
       f16x8(&nxt_f)[TP] = (ks & 1) ? fb0 : fb1;
       constexpr int H1 = TP > 4 ? 4 : TP;   // reads issued before the wait
-      // virtual chunk jv of the tap -> physical halo chunk j (split: [hi, lo, hi] over [hi, lo])
       if constexpr (ks + 1 < NKS) {
-        constexpr int tap = (ks + 1) / NV, jv = (ks + 1) - tap * NV, j = jv < NCH ? jv : jv - NCH;
+        constexpr int tap = (ks + 1) / NCC, j = (ks + 1) - tap * NCC;
         constexpr int th = tap / 3, tw = tap - th * 3;
         t2d_read_frags<P * 64, j * NRP * 64 + th * P * 64>(cur + ad[tw], nxt_f,
                                                           std::make_integer_sequence<int, H1>{});
+        if constexpr (SPLIT) {   // the lo half of the same pixels and channels: halo chunk NCC + j
+          f16x8(&nxt_l)[SPLIT ? TP : 1] = (ks & 1) ? fl0 : fl1;
+          t2d_read_frags<P * 64, (NCC + j) * NRP * 64 + th * P * 64>(cur + ad[tw], nxt_l,
+                                                                      std::make_integer_sequence<int, TP>{});
+        }
       }
       if constexpr (ks + 1 < NKS && TP > H1) {
-        constexpr int tap = (ks + 1) / NV, jv = (ks + 1) - tap * NV, j = jv < NCH ? jv : jv - NCH;
+        constexpr int tap = (ks + 1) / NCC, j = (ks + 1) - tap * NCC;
         constexpr int th = tap / 3, tw = tap - th * 3;
         t2d_read_frags<P * 64, j * NRP * 64 + th * P * 64 + H1 * P * 64>(cur + ad[tw], nxt_f + H1,
                                                                        std::make_integer_sequence<int, TP - H1>{});
@@ -293,6 +315,19 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, in
 #pragma unroll
           for (int t = 0; t < TP; ++t)
             acc[a][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[ks][a], cur_f[t], acc[a][t], 0, 0, 0);
+        if constexpr (SPLIT) {   // + W_lo * x_hi + W_hi * x_lo (f32 accumulation)
+          f16x8(&cur_l)[SPLIT ? TP : 1] = (ks & 1) ? fl1 : fl0;
+#pragma unroll
+          for (int a = 0; a < TC; ++a)
+#pragma unroll
+            for (int t = 0; t < TP; ++t)
+              acc[a][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[ks][a], cur_f[t], acc[a][t], 0, 0, 0);
+#pragma unroll
+          for (int a = 0; a < TC; ++a)
+#pragma unroll
+            for (int t = 0; t < TP; ++t)
+              acc[a][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[ks][a], cur_l[t], acc[a][t], 0, 0, 0);
+        }
       }
       __builtin_amdgcn_sched_barrier(0);
     });
@@ -424,6 +459,9 @@ static bool t2d_shape_split(int cin, int npad, T2dShape* sh) {
   if (getenv("PC_T2D_SPLIT") && atoi(getenv("PC_T2D_SPLIT")) == 0) return false;   // tuning: off
   if (cin == 32 && npad == 32) *sh = {2, 1, 4, 4};
   else if (cin == 32 && npad == 64) *sh = {2, 2, 4, 4};
+  // 64 channels (288 weight registers, one wave per SIMD, 8-row blocks) measured slower than
+  // conv_fast's 64x512 tile on SCRFD 160x160x64 (611 vs 557-572 us, r04d): opt-in only
+  else if (cin == 64 && npad == 64 && getenv("PC_T2D_SPLIT64")) *sh = {4, 2, 4, 4};
   else return false;
   return true;
 }
@@ -494,6 +532,7 @@ hipError_t conv_t2d_launch(const ConvParams& p, hipStream_t s) {
       return hipErrorInvalidValue;
     T2dShape sh;
     t2d_shape_split(cin, p.npad, &sh);
+    if (sh.nch == 4) return launch_t2d<4, 2, 4, 4, 2, true>(p, s);
     if (sh.g == 1) return launch_t2d<2, 1, 4, 4, 2, true>(p, s);
     return launch_t2d<2, 2, 4, 4, 2, true>(p, s);
   }

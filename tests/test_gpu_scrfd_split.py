@@ -59,6 +59,7 @@ def _heads_vs_oracle(ctx, p, variant, D, frames, env, monkeypatch):
 
 KERNEL_MODES = {
     "default": {},                                             # split t2d (32-ch trunk) + conv_fast
+    "t2d64": {"PC_T2D_SPLIT64": "1"},                          # + the opt-in 64-channel split t2d
     "fast": {"PC_CONV_T2D": "0"},                              # conv_fast everywhere it runs
     "igemm": {"PC_CONV_T2D": "0", "PC_CONV_FAST": "0"},        # the generic kernel
 }
@@ -79,18 +80,20 @@ def test_split_net_parity_2_5g(gpu_ctx, monkeypatch):
     assert worst < TOL_X3, worst
 
 
-def test_split_t2d_equals_conv_fast(gpu_ctx, s10g, monkeypatch):
-    """Same K order on both kernels: the whole split net is bit-identical with and without
-    the split t2d kernel."""
+def test_split_t2d_close_to_conv_fast(gpu_ctx, s10g, monkeypatch):
+    """The split t2d kernel sums the three products per 32-channel chunk (W_hi*hi, W_lo*hi,
+    W_hi*lo), the implicit-GEMM kernels per [hi, lo, hi] block: the same values to f32 class
+    (relative 1e-5 on the heads), not bitwise."""
     frames = [_frame(4), _frame(5)]
     _, a, _ = _heads_vs_oracle(gpu_ctx, s10g, "10g", 320, frames, {}, monkeypatch)
     _, b, _ = _heads_vs_oracle(gpu_ctx, s10g, "10g", 320, frames, {"PC_CONV_T2D": "0"}, monkeypatch)
     for x, y in zip(a, b):
-        assert np.array_equal(x, y)
+        assert np.abs(x - y).max() / max(1.0, np.abs(y).max()) < 1e-5
 
 
 def test_split_t2d_ran(gpu_ctx, s10g):
-    """The planner sends the 32-channel split trunk convs to the split t2d kernel."""
+    """The planner sends the 32-channel split trunk convs to the split t2d kernel (64 channels:
+    opt-in PC_T2D_SPLIT64, measured slower than conv_fast)."""
     eng = ScrfdEngine(gpu_ctx, s10g, "10g", D=320, precision=PC_PREC_F16X3, max_batch=1)
     f = _frame(6)
     d = gpu_ctx.upload(f)
@@ -98,7 +101,7 @@ def test_split_t2d_ran(gpu_ctx, s10g):
     eng.detect_frames([(d.ptr, f.shape[0], f.shape[1], f.strides[0])], thresh=0.5)
     codes = [int(r[4]) for r in eng.net.profile_ops()]
     eng.net.profile(False)
-    assert sum(1 for c in codes if 200 <= c < 300) == 2, codes   # stem.3 (32->32) and stem.6 (32->64)
+    assert sum(1 for c in codes if 200 <= c < 300) == 2, codes   # stem.3 (32->32), stem.6 (32->64)
 
 
 @pytest.mark.parametrize("seed", [20, 21])
