@@ -204,6 +204,10 @@ int pc_net_chain_info(pc_net* net, int32_t* h_min_batch, int32_t* h_images_per_r
 int pc_net_set_chain_min_batch(pc_net* net, int32_t min_batch);
 /* capture pc_net_run(batch) into a HIP graph and replay it on later runs of the same batch */
 int pc_net_set_graph(pc_net* net, int enable);
+/* with graphs enabled, capture / replay only runs of at most max_batch images (the per-frame
+ * extract() path: dozens of small launches per net run); larger runs launch eagerly (and can
+ * be profiled). Default: every batch. Replaces nothing in the reference (launch plumbing). */
+int pc_net_set_graph_max_batch(pc_net* net, int32_t max_batch);
 /* HIP-event timing of every op of every later (non-graph) run; enable resets the counters.
  * read: [0] conv ms, [1] conv launches, [2] conv FLOPs (algorithmic), [3] other ms, [4] other launches */
 int pc_net_profile(pc_net* net, int enable);

@@ -111,6 +111,7 @@ SIGNATURES = {
     "pc_net_chain_info": ([_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32)], _I),
     "pc_net_set_chain_min_batch": ([_P, C.c_int32], _I),
     "pc_net_set_graph": ([_P, _I], _I),
+    "pc_net_set_graph_max_batch": ([_P, C.c_int32], _I),
     "pc_net_profile": ([_P, _I], _I),
     "pc_net_profile_read": ([_P, C.POINTER(C.c_double)], _I),
     "pc_net_profile_ops": ([_P, C.POINTER(C.c_double), _I], _I),

@@ -492,8 +492,9 @@ struct pc_net {
   // implicit-GEMM loader finds a zero tail behind it (ConvSeg::zero_off)
   void* in_copy = nullptr;
   size_t in_img_bytes = 0;
-  // graph replay
+  // graph replay (runs of at most graph_max_batch images)
   int use_graph = 0;
+  int graph_max_batch = 1 << 30;
   // per-op HIP-event profiling (pc_net_profile)
   int prof = 0;
   std::vector<hipEvent_t> ev_pool;
@@ -1369,7 +1370,7 @@ extern "C" int pc_net_run(pc_net* n, const void* d_in, int N) {
   pc_ctx* c = n->ctx;
   if (N <= 0 || N > n->max_batch) return fail(c, PC_ERR_ARG, "batch out of range");
   n->cur_input = d_in;
-  if (!n->use_graph) return run_ops(n, N);
+  if (!n->use_graph || N > n->graph_max_batch) return run_ops(n, N);
   auto key = std::make_pair(N, d_in);
   auto it = n->graphs.find(key);
   if (it == n->graphs.end()) {
@@ -1392,6 +1393,11 @@ extern "C" int pc_net_run(pc_net* n, const void* d_in, int N) {
 extern "C" int pc_net_set_graph(pc_net* n, int enable) {
   if (!n) return PC_ERR_ARG;
   n->use_graph = enable ? 1 : 0;
+  return PC_OK;
+}
+extern "C" int pc_net_set_graph_max_batch(pc_net* n, int32_t max_batch) {
+  if (!n || max_batch < 1) return PC_ERR_ARG;
+  n->graph_max_batch = max_batch;
   return PC_OK;
 }
 

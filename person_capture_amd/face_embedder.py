@@ -272,6 +272,13 @@ class FaceEmbedder(YoloFaceBranch):
         self._stage_threads = int(os.getenv("PERSON_CAPTURE_AMD_STAGE_THREADS", "4"))
         self._arc = ArcFaceEngine(self._ectx, self._arc_params, self._arc_depth, precision=self.precision,
                                   max_batch=self._arc_batch)
+        # HIP graphs for small net runs (unchanged callers' per-frame extract(): a SCRFD pass of one
+        # frame and an ArcFace pass of its faces are ~60 and ~100 small launches each): runs of at
+        # most this many images replay a captured graph (bit-identical, the same launches);
+        # PERSON_CAPTURE_AMD_GRAPH_BATCH=0 launches eagerly
+        self._graph_batch = int(os.getenv("PERSON_CAPTURE_AMD_GRAPH_BATCH", "8"))
+        if self._graph_batch > 0:
+            self._arc.net.set_graph(True, max_batch=4 * self._graph_batch)
         self._arc_feat_dim = self._arc.dim
         self._arc_fixed_batch = False
         # resident block chains (one image per CU through the 14x14x256 stage) need whole CUs:
@@ -371,6 +378,8 @@ class FaceEmbedder(YoloFaceBranch):
             mb = max(1, min(self._det_batch, self._det_batch * 640 * 640 // (D * D)))
             e = ScrfdEngine(self._ctx, self._scrfd_params, self.scrfd_variant, D=D, precision=self.det_precision,
                             max_batch=mb, max_det=1024)
+            if self._graph_batch > 0:   # per-frame / fallback runs: one graph launch per net run
+                e.net.set_graph(True, max_batch=self._graph_batch)
             self._scrfd_engines[D] = e
         return e
 

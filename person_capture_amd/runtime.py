@@ -256,8 +256,12 @@ class Net:
         if k < 0:
             check(-k, self.ctx.handle, "set_chain_min_batch")
 
-    def set_graph(self, enable: bool) -> None:
+    def set_graph(self, enable: bool, max_batch: Optional[int] = None) -> None:
+        """HIP-graph capture / replay of net runs (of at most max_batch images when given)."""
         check(self.ctx.lib.pc_net_set_graph(self.handle, 1 if enable else 0), self.ctx.handle, "set_graph")
+        if max_batch is not None:
+            check(self.ctx.lib.pc_net_set_graph_max_batch(self.handle, int(max_batch)), self.ctx.handle,
+                  "set_graph_max_batch")
 
     def profile(self, enable: bool) -> None:
         check(self.ctx.lib.pc_net_profile(self.handle, 1 if enable else 0), self.ctx.handle, "profile")

@@ -63,19 +63,32 @@ def test_chained_align_quality_embed(gpu_ctx, monkeypatch, prec, tol_f):
     assert n >= 4
 
 
-# f32 is the parity mode; f16 is the throughput mode (the reference's TensorRT fp16
-# engines): there the detector's landmarks move by a fraction of a pixel, the chip
-# resamples slightly differently and the synthetic (untrained, not
-# warp-invariant) embedder turns that into a small rotation of the feature, so the
-# f16 bar is on the cosine between features (bit-exact chaining from the same
-# landmarks is test_chained_align_quality_embed's job).
+# f32 is the parity mode; "f16" the throughput mode with its default f16x3 detector (f32-class
+# landmarks: identical boxes, the chip differs from the oracle's only where an f32-level landmark
+# difference moves a warp coordinate across a rounding step); "f16det" the plain f16 detector
+# (PERSON_CAPTURE_AMD_DET_PRECISION=f16, the reference's TRT fp16 precision): there the landmarks
+# move by a fraction of a pixel, the chip resamples and the synthetic (untrained, not
+# warp-invariant) embedder turns that into a small rotation of the feature, so its bar is on the
+# cosine between features (bit-exact chaining from the same landmarks is
+# test_chained_align_quality_embed's job).
 @pytest.mark.parametrize("prec,tol_box,tol_count,tol_q,min_cos,tol_fd",
-                         [("f32", 0, 0, 1e-3, 0.9999, 1e-3), ("f16", 1, 1, 5e-2, 0.98, 1e-2)])
+                         [("f32", 0, 0, 1e-9, 1.0 - 1e-6, 1e-4), ("f16", 0, 0, 2e-2, 0.999, 2e-3),
+                          ("f16det", 1, 1, 5e-2, 0.98, 1e-2)])
 def test_face_embedder_end_to_end(gpu_ctx, monkeypatch, prec, tol_box, tol_count, tol_q, min_cos, tol_fd):
-    """f32 is the parity mode: the same faces, identical int boxes. f16 (the reference's
-    TRT fp16 mode) may flip a detection whose synthetic score sits at the threshold, and
-    the int() truncation of a box edge may land one pixel over: at most `tol_count`
-    unmatched faces per frame, boxes within `tol_box`."""
+    """f32 is the parity mode: the same faces, identical int boxes; a face whose chip is
+    byte-identical to the oracle's has its feature within 1e-4 and fd within 1e-4 (north
+    star), and one whose landmarks differ in the last f32 bits (a few warped pixels move) is
+    checked through the chain and end to end within the measured 1e-3. The f16x3 detector
+    keeps counts and boxes exact. The plain f16 detector may flip a detection whose synthetic
+    score sits at the threshold, and the int() truncation of a box edge may land one pixel over:
+    at most `tol_count` unmatched faces per frame, boxes within `tol_box`."""
+    if prec == "f16det":
+        monkeypatch.setenv("PERSON_CAPTURE_AMD_DET_PRECISION", "f16")
+        prec = "f16"
+        plain16 = True
+    else:
+        monkeypatch.delenv("PERSON_CAPTURE_AMD_DET_PRECISION", raising=False)
+        plain16 = False
     monkeypatch.setenv("PERSON_CAPTURE_AMD_PRECISION", prec)
     fe = fe_mod.FaceEmbedder(ctx="cuda:0", yolo_model="scrfd_10g_bnkps", conf=0.5)
     fe.debug_chips = True   # f16: a chip that differs from the oracle's was re-aligned, not mis-embedded
@@ -101,15 +114,18 @@ def test_face_embedder_end_to_end(gpu_ctx, monkeypatch, prec, tol_box, tol_count
                 # edges): the chip, and so the feature, legitimately differ
                 nshifted += 1
                 continue
-            if prec == "f16" and not np.array_equal(a["chip"], b["chip"]):
-                # f16 landmarks moved by a fraction of a pixel and the warp resampled:
-                # the landmarks must agree closely, and the device embedding must be the
-                # oracle embedding of the device's own chip (the chained check)
-                assert np.abs(a["kps5"] - b["kps5"]).max() < 1.0
+            if not np.array_equal(a["chip"], b["chip"]):
+                # the landmarks differ (f32 / f16x3: in the last f32 bits; plain f16: by a fraction
+                # of a pixel) and the warp resampled: the landmarks must agree closely, and the device
+                # embedding must be the oracle embedding of the device's own chip (the chained check)
+                assert np.abs(a["kps5"] - b["kps5"]).max() < (1.0 if plain16 else 1e-3)
                 e = nt.iresnet_forward(fe._arc_params, 100, nt.arcface_input_from_chips(a["chip"][None])).numpy()
                 ef = nt.iresnet_forward(fe._arc_params, 100,
                                         nt.arcface_input_from_chips(a["chip"][None, :, ::-1])).numpy()
-                assert np.abs(ra.arcface_postprocess(e, ef)[0] - a["feat"]).max() < 1e-2
+                assert np.abs(ra.arcface_postprocess(e, ef)[0] - a["feat"]).max() < (1e-4 if prec == "f32" else 1e-2)
+                # end to end against the oracle's own chip: measured <= 7e-4 in f32 (C3, 332 faces)
+                if not plain16:
+                    assert abs(a["fd"] - b["fd"]) < (1e-3 if prec == "f32" else 2e-3)
                 nrealigned += 1
                 continue
             assert abs(a["quality"] - b["quality"]) <= tol_q * max(1.0, b["quality"])
@@ -120,10 +136,11 @@ def test_face_embedder_end_to_end(gpu_ctx, monkeypatch, prec, tol_box, tol_count
                     assert (a["fd"] <= thr) == (b["fd"] <= thr)
             nchecked += 1
         assert unmatched <= tol_count
+    # f32: most chips differ from the oracle's in a few warped pixels (f32-level landmark
+    # differences), so they are checked through the chain; some are byte-identical
+    assert nchecked + nrealigned >= 4 and nshifted <= (nchecked + nrealigned) // 2
     if prec == "f32":
-        assert nchecked >= 4 and nshifted + nrealigned <= nchecked
-    else:
-        assert nchecked + nrealigned >= 4 and nshifted <= (nchecked + nrealigned) // 2
+        assert nchecked >= 1 and nshifted == 0
 
 
 def test_extract_single_matches_batch(gpu_ctx):
