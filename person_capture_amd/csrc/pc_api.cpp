@@ -30,10 +30,10 @@ int conv_fast_valid(int cfg, int rowb);
 int conv_halo_num_cfgs();
 int conv_halo_tile(int cfg, int* bc, int* bp);
 int conv_halo_fits(int cfg, int KH, int KW, int W);
-hipError_t conv_t2d_launch(const ConvParams& p, hipStream_t s);
-int conv_t2d_supported(int cin, int npad, int KH, int KW, int stride, int pad, int act, int out_f32, int ycs,
-                       int ycoff, int split);
-int conv_t2d_rows(int cin, int npad, int split);
+hipError_t conv_t2d_launch(const ConvParams& p, int variant, hipStream_t s);
+int conv_t2d_select(int cin, int npad, int KH, int KW, int stride, int pad, int act, int out_f32, int ycs,
+                    int ycoff, int split);
+int conv_t2d_rows(int variant);
 int conv_chain_fits(int H, int W, int C, int npad, long long ktot);
 hipError_t conv_chain_launch(const void* x, int xcs, void* y, int ycs, const void* blk_dev, int nblk, int N, int H,
                              int W, long long ktot, int dbg, hipStream_t s);
@@ -667,15 +667,16 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
     const bool split_ok = !sp ? !any_split
                               : (Y.split && (w[21] < 0 || n->tens[w[21]].split) && Y.C / 2 >= 8 && (Y.C / 2) % 8 == 0);
     const int cin_l = sp ? X.C / 2 : X.C;
-    if (mode > 0 && !n->f32 && nseg == 1 && pl.splitk == 1 && X.H == Y.H && X.W == Y.W && split_ok &&
-        conv_t2d_supported(cin_l, npad, w[4], w[5], w[6], w[7], w[20], Y.is_f32, Y.cs, Y.coff, sp) &&
-        w[15] >= (sp ? 27LL : 9LL) * cin_l &&
+    const int var = (mode > 0 && !n->f32 && nseg == 1 && pl.splitk == 1 && X.H == Y.H && X.W == Y.W && split_ok)
+                        ? conv_t2d_select(cin_l, npad, w[4], w[5], w[6], w[7], w[20], Y.is_f32, Y.cs, Y.coff, sp)
+                        : -1;
+    if (var >= 0 && w[15] >= (sp ? 27LL : 9LL) * cin_l &&
         (double)X.H * X.W * n->max_batch * X.cs * esz + kZeroTail < 4294967296.0 &&
         (double)M < 2147483647.0) {
-      const int th = conv_t2d_rows(cin_l, npad, sp);
+      const int th = conv_t2d_rows(var);
       const double cover = (double)Y.H * Y.W / ((double)((Y.H + th - 1) / th * th) * ((Y.W + 15) / 16 * 16));
       if (mode == 2 || cover >= 0.75) {
-        pl.t2d = 0;
+        pl.t2d = var;   // the variant, fixed at plan time (conv_t2d_launch runs exactly it)
         pl.fast = -1;
         pl.halo = -1;
       }
@@ -1196,7 +1197,7 @@ static int run_ops(pc_net* n, int N) {
       p.zero = c->zero;
       if (const char* e = getenv("PC_CONV_DBG")) p.dbg = atoi(e);
       if (pl.t2d >= 0) {
-        HIPCHK(c, conv_t2d_launch(p, s));
+        HIPCHK(c, conv_t2d_launch(p, pl.t2d, s));
       } else if (pl.fast >= 0) {
         HIPCHK(c, conv_fast_launch(n->f32, pl.rowb, pl.fast, p, s));
       } else if (pl.halo >= 0) {

@@ -445,61 +445,13 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_t2d(ConvParams p, int nty, in
 // host side
 // ---------------------------------------------------------------------------
 
-// (Cin, npad) -> instantiation: NCH 32-channel input chunks, G 32-channel output groups,
-// NW waves, TP output rows per wave (a block is TP*NW/G rows x 16 pixels). The wide shapes
-// (Cin/npad 96 and 128: SCRFD's 80x80x96 trunk, IResNet's 28x28x128 stage) hold 216 / 288
-// weight registers per wave, so they run one wave per SIMD: 3 waves for 96 output channels
-// (one SIMD idle), 4 for 128. SCRFD-10G 80x80x96 (N 64): 200 -> 134 us per conv, the net
-// 6.24 -> 5.62 ms (r03o).
-struct T2dShape { int nch, g, nw, tp, nbuf = 2; };
-// split (f16x3) shapes: cin is the logical channel count (the halo holds 2x); the weights of
-// the 3/2 x longer virtual K (216 registers for 32 channels) leave one wave per SIMD, and the
-// block height keeps the two halo buffers and the split staging image within the LDS
-static bool t2d_shape_split(int cin, int npad, T2dShape* sh) {
-  if (getenv("PC_T2D_SPLIT") && atoi(getenv("PC_T2D_SPLIT")) == 0) return false;   // tuning: off
-  if (cin == 32 && npad == 32) *sh = {2, 1, 4, 4};
-  else if (cin == 32 && npad == 64) *sh = {2, 2, 4, 4};
-  // 64 channels (288 weight registers, one wave per SIMD, 8-row blocks) measured slower than
-  // conv_fast's 64x512 tile on SCRFD 160x160x64 (611 vs 557-572 us, r04d): opt-in only
-  else if (cin == 64 && npad == 64 && getenv("PC_T2D_SPLIT64")) *sh = {4, 2, 4, 4};
-  else return false;
-  return true;
-}
-static bool t2d_shape(int cin, int npad, T2dShape* sh) {
-  const bool wide = !getenv("PC_T2D_NARROW");   // tuning: the round-2 shapes only
-  const bool la = getenv("PC_T2D_NBUF3") != nullptr;   // tuning: two-block halo lookahead
-  if (cin == 32 && npad == 32) *sh = {1, 1, 8, 4};
-  else if (cin == 32 && npad == 64) *sh = {1, 2, 8, 4, la ? 3 : 2};
-  else if (cin == 64 && npad == 64) *sh = la ? T2dShape{2, 2, 4, 4, 3} : T2dShape{2, 2, 4, 8};
-  else if (wide && cin == 96 && npad == 96) *sh = {3, 3, 3, 4, la ? 3 : 2};
-  else if (wide && cin == 64 && npad == 96) *sh = {2, 3, 3, 8, la ? 3 : 2};
-  // 128 channels measured slower than conv_fast's 128x256 tile (IResNet 28x28x128 b256: 101.8
-  // vs 96.0 us per conv, r03o): opt-in only
-  else if (wide && cin == 128 && npad == 128 && getenv("PC_T2D_128")) *sh = {4, 4, 4, atoi(getenv("PC_T2D_128")) == 8 ? 8 : 4};
-  else return false;
-  return true;
-}
-
-// piecewise-linear activations, f16 output in whole 16-byte pixel chunks; 0 if the conv
-// cannot run on it
-// split: input / output / residual are f16x3 split tensors (cin logical); only split-in ->
-// split-out convs (the detector trunk) run here
-int conv_t2d_supported(int cin, int npad, int KH, int KW, int stride, int pad, int act, int out_f32, int ycs,
-                       int ycoff, int split) {
-  if (KH != 3 || KW != 3 || stride != 1 || pad != 1) return 0;
-  if (act != ACT_NONE && act != ACT_RELU && act != ACT_PRELU) return 0;
-  if (out_f32 || (ycs & 7) || (ycoff & 7)) return 0;
-  T2dShape sh;
-  return (split ? t2d_shape_split(cin, npad, &sh) : t2d_shape(cin, npad, &sh)) ? 1 : 0;
-}
-
-// output rows per block (the block is TH x 16 pixels)
-int conv_t2d_rows(int cin, int npad, int split) {
-  T2dShape sh;
-  if (!(split ? t2d_shape_split(cin, npad, &sh) : t2d_shape(cin, npad, &sh))) return 16;
-  return sh.tp * sh.nw / sh.g;
-}
-
+// Instantiations (variants): NCH 32-channel input chunks (split: hi + lo chunks), G 32-channel
+// output groups, NW waves, TP output rows per wave (a block is TP*NW/G rows x 16 pixels), NBUF
+// halo buffers. The wide shapes (Cin/npad 96 and 128: SCRFD's 80x80x96 trunk, IResNet's 28x28x128
+// stage) hold 216 / 288 weight registers per wave, so they run one wave per SIMD: 3 waves for 96
+// output channels (one SIMD idle), 4 for 128. SCRFD-10G 80x80x96 (N 64): 200 -> 134 us per conv,
+// the net 6.24 -> 5.62 ms (r03o). The planner picks a variant once (conv_t2d_select, at
+// pc_net_create: the tuning switches are read there) and the launch runs exactly that one.
 template <int NCH, int G, int NW, int TP, int NBUF = 2, bool SPLIT = false>
 static hipError_t launch_t2d(const ConvParams& p, hipStream_t s) {
   static int ncu = 0;
@@ -518,39 +470,91 @@ static hipError_t launch_t2d(const ConvParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t conv_t2d_launch(const ConvParams& p, hipStream_t s) {
-  const ConvSeg& S = p.seg[0];
-  const int split = S.vwrap ? 1 : 0;
+struct T2dVariant {
+  int cin, npad;   // logical input channels, padded output channels
+  int nch, g, nw, tp, nbuf;
+  bool split;
+  hipError_t (*launch)(const ConvParams&, hipStream_t);
+};
+static const T2dVariant kT2d[] = {
+    {32, 32, 1, 1, 8, 4, 2, false, launch_t2d<1, 1, 8, 4>},            // 0
+    {32, 64, 1, 2, 8, 4, 2, false, launch_t2d<1, 2, 8, 4>},            // 1
+    {32, 64, 1, 2, 8, 4, 3, false, launch_t2d<1, 2, 8, 4, 3>},         // 2  PC_T2D_NBUF3
+    {64, 64, 2, 2, 4, 8, 2, false, launch_t2d<2, 2, 4, 8>},            // 3  (144 weight registers: 4 waves of 8 rows)
+    {64, 64, 2, 2, 4, 4, 3, false, launch_t2d<2, 2, 4, 4, 3>},         // 4  PC_T2D_NBUF3
+    {96, 96, 3, 3, 3, 4, 2, false, launch_t2d<3, 3, 3, 4>},            // 5
+    {96, 96, 3, 3, 3, 4, 3, false, launch_t2d<3, 3, 3, 4, 3>},         // 6  PC_T2D_NBUF3
+    {64, 96, 2, 3, 3, 8, 2, false, launch_t2d<2, 3, 3, 8>},            // 7
+    {64, 96, 2, 3, 3, 8, 3, false, launch_t2d<2, 3, 3, 8, 3>},         // 8  PC_T2D_NBUF3
+    {128, 128, 4, 4, 4, 4, 2, false, launch_t2d<4, 4, 4, 4>},          // 9  PC_T2D_128 (opt-in)
+    {128, 128, 4, 4, 4, 8, 2, false, launch_t2d<4, 4, 4, 8>},          // 10 PC_T2D_128=8
+    {32, 32, 2, 1, 4, 4, 2, true, launch_t2d<2, 1, 4, 4, 2, true>},    // 11 split
+    {32, 64, 2, 2, 4, 4, 2, true, launch_t2d<2, 2, 4, 4, 2, true>},    // 12 split
+    {64, 64, 4, 2, 4, 4, 2, true, launch_t2d<4, 2, 4, 4, 2, true>},    // 13 split, PC_T2D_SPLIT64 (opt-in)
+};
+static const int kNumT2d = sizeof(kT2d) / sizeof(kT2d[0]);
+
+// The variant for (cin, npad) and the planner's tuning switches, or -1.
+// split (f16x3): the split t2d reads each tap's hi and lo fragments once; 64 channels (288 weight
+// registers, one wave per SIMD, 8-row blocks) measured slower than conv_fast's 64x512 tile on
+// SCRFD 160x160x64 (611 vs 557-572 us, r04d): opt-in. 128 channels measured slower than
+// conv_fast's 128x256 tile (IResNet 28x28x128 b256: 101.8 vs 96.0 us per conv, r03o): opt-in.
+static int t2d_variant(int cin, int npad, int split) {
   if (split) {
-    // split-in -> split-out only: [hi | lo] halo of 2 x cin channels, virtual K 3 x cin per tap
-    const int cin = S.C / 2;
-    if (p.nseg != 1 || p.splitk != 1 || S.H != p.OH || S.W != p.OW || p.cwrite > p.npad || p.cwrite % 8 ||
-        S.cs != S.C || S.vwrap * 3 != S.cblk * 2 || !p.ysplit || (p.ysplit & 7) ||
-        (p.res_mode != RES_NONE && (!p.rsplit || (p.rsplit & 3))) ||
-        !conv_t2d_supported(cin, p.npad, S.KH, S.KW, S.stride, S.pad, p.act, p.out_f32, p.ycs, 0, 1) ||
-        (reinterpret_cast<uintptr_t>(p.y) & 15) || p.ktot < 27LL * cin)
-      return hipErrorInvalidValue;
-    T2dShape sh;
-    t2d_shape_split(cin, p.npad, &sh);
-    if (sh.nch == 4) return launch_t2d<4, 2, 4, 4, 2, true>(p, s);
-    if (sh.g == 1) return launch_t2d<2, 1, 4, 4, 2, true>(p, s);
-    return launch_t2d<2, 2, 4, 4, 2, true>(p, s);
+    if (getenv("PC_T2D_SPLIT") && atoi(getenv("PC_T2D_SPLIT")) == 0) return -1;   // tuning: off
+    if (cin == 32 && npad == 32) return 11;
+    if (cin == 32 && npad == 64) return 12;
+    if (cin == 64 && npad == 64 && getenv("PC_T2D_SPLIT64")) return 13;
+    return -1;
   }
-  if (p.nseg != 1 || p.splitk != 1 || S.H != p.OH || S.W != p.OW || p.cwrite > p.npad || p.ysplit || p.rsplit ||
-      !conv_t2d_supported(S.C, p.npad, S.KH, S.KW, S.stride, S.pad, p.act, p.out_f32, p.ycs, 0, 0) ||
-      (reinterpret_cast<uintptr_t>(p.y) & 15) || p.ktot < 9LL * S.C)
+  const bool wide = !getenv("PC_T2D_NARROW");          // tuning: the round-2 shapes only
+  const bool la = getenv("PC_T2D_NBUF3") != nullptr;   // tuning: two-block halo lookahead
+  if (cin == 32 && npad == 32) return 0;
+  if (cin == 32 && npad == 64) return la ? 2 : 1;
+  if (cin == 64 && npad == 64) return la ? 4 : 3;
+  if (wide && cin == 96 && npad == 96) return la ? 6 : 5;
+  if (wide && cin == 64 && npad == 96) return la ? 8 : 7;
+  if (wide && cin == 128 && npad == 128 && getenv("PC_T2D_128")) return atoi(getenv("PC_T2D_128")) == 8 ? 10 : 9;
+  return -1;
+}
+
+// piecewise-linear activations, f16 output in whole 16-byte pixel chunks: the variant id, or -1
+// if the conv cannot run here. split: input / output / residual are f16x3 split tensors (cin
+// logical); only split-in -> split-out convs (the detector trunk) run here.
+int conv_t2d_select(int cin, int npad, int KH, int KW, int stride, int pad, int act, int out_f32, int ycs,
+                    int ycoff, int split) {
+  if (KH != 3 || KW != 3 || stride != 1 || pad != 1) return -1;
+  if (act != ACT_NONE && act != ACT_RELU && act != ACT_PRELU) return -1;
+  if (out_f32 || (ycs & 7) || (ycoff & 7)) return -1;
+  return t2d_variant(cin, npad, split);
+}
+
+// output rows per block of a variant (the block is TH x 16 pixels)
+int conv_t2d_rows(int variant) {
+  if (variant < 0 || variant >= kNumT2d) return 16;
+  const T2dVariant& v = kT2d[variant];
+  return v.tp * v.nw / v.g;
+}
+
+hipError_t conv_t2d_launch(const ConvParams& p, int variant, hipStream_t s) {
+  if (variant < 0 || variant >= kNumT2d) return hipErrorInvalidValue;
+  const T2dVariant& v = kT2d[variant];
+  const ConvSeg& S = p.seg[0];
+  const int cin = v.split ? S.C / 2 : S.C;
+  // the conv must be the one the variant was planned for (checked, not re-derived)
+  if (p.nseg != 1 || p.splitk != 1 || S.H != p.OH || S.W != p.OW || p.cwrite > p.npad || cin != v.cin ||
+      p.npad != v.npad || S.KH != 3 || S.KW != 3 || S.stride != 1 || S.pad != 1 || p.out_f32 || (p.ycs & 7) ||
+      (p.act != ACT_NONE && p.act != ACT_RELU && p.act != ACT_PRELU) || (reinterpret_cast<uintptr_t>(p.y) & 15))
     return hipErrorInvalidValue;
-  // Cin 64: the 144 weight registers leave no room for a second wave per SIMD, so 4
-  // waves of 8 rows each (a block is 16 x 16 pixels either way)
-  T2dShape sh;
-  t2d_shape(S.C, p.npad, &sh);
-  const bool b3 = sh.nbuf == 3;
-  if (sh.nch == 1)
-    return p.npad == 32 ? launch_t2d<1, 1, 8, 4>(p, s) : (b3 ? launch_t2d<1, 2, 8, 4, 3>(p, s) : launch_t2d<1, 2, 8, 4>(p, s));
-  if (sh.nch == 2 && sh.g == 2) return b3 ? launch_t2d<2, 2, 4, 4, 3>(p, s) : launch_t2d<2, 2, 4, 8>(p, s);
-  if (sh.nch == 2) return b3 ? launch_t2d<2, 3, 3, 8, 3>(p, s) : launch_t2d<2, 3, 3, 8>(p, s);
-  if (sh.nch == 3) return b3 ? launch_t2d<3, 3, 3, 4, 3>(p, s) : launch_t2d<3, 3, 3, 4>(p, s);
-  return sh.tp == 8 ? launch_t2d<4, 4, 4, 8>(p, s) : launch_t2d<4, 4, 4, 4>(p, s);
+  if (v.split) {
+    // split-in -> split-out: [hi | lo] halo of 2 x cin channels, virtual K 3 x cin per tap
+    if (p.cwrite % 8 || S.cs != S.C || S.vwrap * 3 != S.cblk * 2 || !p.ysplit || (p.ysplit & 7) ||
+        (p.res_mode != RES_NONE && (!p.rsplit || (p.rsplit & 3))) || p.ktot < 27LL * cin)
+      return hipErrorInvalidValue;
+  } else if (S.vwrap || p.ysplit || p.rsplit || p.ktot < 9LL * S.C) {
+    return hipErrorInvalidValue;
+  }
+  return v.launch(p, s);
 }
 
 }  // namespace pc

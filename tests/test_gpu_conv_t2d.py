@@ -60,7 +60,8 @@ def _run(gpu_ctx, monkeypatch, P, xin, N, mode):
     d = gpu_ctx.upload(xin.astype(np.float16))
     net.run(d.ptr, N)
     out = net.read_output(0, N)
-    kinds = {int(r[4]) for r in _profile_kinds(net, d, N)}
+    # profile code 200 + v: the 2-D block kernel, variant v (pc_conv_t2d.hip kT2d); folded to 200
+    kinds = {200 if 200 <= int(r[4]) < 300 else int(r[4]) for r in _profile_kinds(net, d, N)}
     return out, kinds
 
 
@@ -151,7 +152,7 @@ def test_t2d_auto_plan_covers_trunks(gpu_ctx):
         H, W, C = P.dims(P.input)
         d = gpu_ctx.upload(np.zeros((B, H, W, C), np.float16))
         recs = _profile_kinds(net, d, B)
-        n_t2d = sum(1 for r in recs if int(r[4]) == 200)
+        n_t2d = sum(1 for r in recs if 200 <= int(r[4]) < 300)
         del net, d
         assert n_t2d >= want, n_t2d
 

@@ -23,13 +23,24 @@ done
 python3 - "$OUT" "$MATCH" <<'PY'
 import csv, glob, sys, collections
 out, match = sys.argv[1], sys.argv[2]
-agg = collections.defaultdict(float); cnt = collections.Counter()
+agg = collections.defaultdict(lambda: collections.defaultdict(float))
+cnt = collections.defaultdict(collections.Counter)
+tot = collections.defaultdict(float); cntall = collections.Counter()
 for f in glob.glob(out + "/p*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if match not in r.get("Kernel_Name", ""): continue
-        agg[r["Counter_Name"]] += float(r["Counter_Value"]); cnt[r["Counter_Name"]] += 1
+        name = r.get("Kernel_Name", "")
+        if match not in name: continue
+        c, v = r["Counter_Name"], float(r["Counter_Value"])
+        agg[name][c] += v; cnt[name][c] += 1
+        tot[c] += v; cntall[c] += 1
 with open(out + "/summary.txt", "w") as fo:
-    for k in sorted(agg):
-        line = f"{k:32s} {agg[k] / max(cnt[k],1):18.1f}  (per dispatch, {cnt[k]} rows)"
+    def emit(line):
         print(line); fo.write(line + "\n")
+    emit(f"== all kernels matching '{match}' (per dispatch)")
+    for k in sorted(tot):
+        emit(f"{k:32s} {tot[k] / max(cntall[k], 1):18.1f}  ({cntall[k]} rows)")
+    for name in sorted(agg, key=lambda n: -max(cnt[n].values())):
+        emit(f"== {name} (per dispatch)")
+        for k in sorted(agg[name]):
+            emit(f"{k:32s} {agg[name][k] / max(cnt[name][k], 1):18.1f}  ({cnt[name][k]} rows)")
 PY
