@@ -27,6 +27,7 @@ hipError_t conv_fast_launch(int f32, int rowb, int cfg, const ConvParams& p, hip
 int conv_fast_num_cfgs();
 int conv_fast_tile(int cfg, int* bc, int* bp);
 int conv_fast_valid(int cfg, int rowb);
+int conv_fast_valid_sx(int cfg, int rowb);
 int conv_halo_num_cfgs();
 int conv_halo_tile(int cfg, int* bc, int* bp);
 int conv_halo_fits(int cfg, int KH, int KW, int W);
@@ -442,7 +443,8 @@ struct NetBuf { long long elems; int is_f32; void* d = nullptr; };
 // C / 2 each; the lo half of a pixel is C / 2 elements after its hi half
 struct NetTensor { int buf, H, W, C, cs, coff, is_f32, split; };
 struct NetOp { int w[32]; };
-struct ConvPlan { int rowb, cfg, splitk, halo = -1, fast = -1, t2d = -1; long long M_per_image; double flops_per_image; };
+// sx: fused f16x3 split tiles on conv_fast (pc_conv_fast.hip SX)
+struct ConvPlan { int rowb, cfg, splitk, halo = -1, fast = -1, t2d = -1, sx = 0; long long M_per_image; double flops_per_image; };
 // A stem (tiny Cin) runs as im2col + a 1x1 MFMA conv over 32-element K rows.
 struct StemPlan {
   int use_mfma = 0, npad = 0, cfg = 0, rowb = 0, cin_true = 0;
@@ -622,13 +624,20 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
   // MI355X (bigger wave tiles stage fewer LDS bytes per MFMA).
   // PC_CONV_FAST=0 disables, =k+1 forces tile k.
   pl.fast = -1;
+  pl.sx = 0;
+  // f16x3 split inputs on conv_fast: fused tiles (a (tap, hi block) with its lo block and both
+  // weight halves, pc_conv_fast.hip SX) where two stages of the doubled tile fit the LDS.
+  // PC_SPLIT_FUSED=0: walk the virtual [hi, lo, hi] blocks as plain tiles instead.
+  bool all_split = nseg > 0 && !n->f32;
+  for (int sg = 0; sg < nseg; ++sg) all_split = all_split && n->tens[w[3 + 5 * sg]].split;
+  const bool try_sx = all_split && pl.splitk == 1 && !(getenv("PC_SPLIT_FUSED") && atoi(getenv("PC_SPLIT_FUSED")) == 0);
   {
     const char* e = getenv("PC_CONV_FAST");
     const int force = e ? atoi(e) : ((getenv("PC_CONV_CFG") || getenv("PC_CONV_HALO")) ? 0 : -1);
     bool ok = pl.splitk == 1 && force != 0;
     // odd multiples of 32 channels (96, 160, 224: SCRFD trunks) run faster on the generic
     // kernel's 96x256 / 32x512 tiles (measured per layer, tools/probe_layers.py scrfd)
-    if (force < 0 && npad > 32 && npad % 64 == 32) ok = false;
+    if (force < 0 && npad > 32 && npad % 64 == 32 && !try_sx) ok = false;
     for (int sg = 0; sg < nseg && ok; ++sg) {
       const NetTensor& X = n->tens[w[3 + 5 * sg]];
       if ((double)X.H * X.W * n->max_batch * X.cs * esz + kZeroTail >= 4294967296.0) ok = false;
@@ -649,6 +658,23 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
         const double rounds = (double)((t + 256 * occ[k] - 1) / (256 * occ[k]));
         const double est = rounds * bc * bp * occ[k] * cost[k];
         if (best < 0 || est < best_t) { best = k; best_t = est; best_rowb = rb; }
+      }
+      if (try_sx) {   // the same choice among the tiles that can stage fused split tiles
+        int bsx = -1, bsx_rowb = rowb;
+        double bsx_t = 0;
+        for (int k = 0; k < conv_fast_num_cfgs(); ++k) {
+          int bc = 0, bp = 0;
+          conv_fast_tile(k, &bc, &bp);
+          if (npad % bc || (force > 0 && k != force - 1)) continue;
+          for (int rb : {rowb, 64}) {
+            if (!conv_fast_valid_sx(k, rb)) continue;
+            const long long t = (M + bp - 1) / bp * (npad / bc);
+            const double est = (double)((t + 255) / 256) * bc * bp * cost[k];
+            if (bsx < 0 || est < bsx_t) { bsx = k; bsx_t = est; bsx_rowb = rb; }
+            break;
+          }
+        }
+        if (bsx >= 0) { best = bsx; best_rowb = bsx_rowb; pl.sx = 1; }
       }
       pl.fast = best;
       if (best >= 0) { pl.halo = -1; pl.rowb = best_rowb; }
@@ -678,6 +704,7 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
       if (mode == 2 || cover >= 0.75) {
         pl.t2d = var;   // the variant, fixed at plan time (conv_t2d_launch runs exactly it)
         pl.fast = -1;
+        pl.sx = 0;
         pl.halo = -1;
       }
     }
@@ -697,6 +724,7 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
       if (sk >= 2) {
         pl.splitk = sk;
         pl.fast = pl.halo = pl.t2d = -1;
+        pl.sx = 0;
         pl.cfg = cfg;
         pl.rowb = rowb;
       }
@@ -1162,7 +1190,10 @@ static int run_ops(pc_net* n, int N) {
         S.H = X.H; S.W = X.W; S.C = X.C; S.cs = X.cs;
         S.KH = w[4 + 5 * sg]; S.KW = w[5 + 5 * sg]; S.stride = w[6 + 5 * sg]; S.pad = w[7 + 5 * sg];
         S.cblk = X.C / bke;
-        if (X.split) {   // virtual channel blocks [hi, lo, hi] (pc_common.h ConvSeg::vwrap)
+        if (X.split && pl.sx) {   // fused split tiles: the hi blocks; lo block = hi block + vwrap
+          S.cblk = S.cblk / 2;
+          S.vwrap = S.cblk;
+        } else if (X.split) {     // virtual channel blocks [hi, lo, hi] (pc_common.h ConvSeg::vwrap)
           S.vwrap = S.cblk;
           S.cblk = S.cblk / 2 * 3;
         }
@@ -1192,6 +1223,7 @@ static int run_ops(pc_net* n, int N) {
       }
       p.act_after_res = w[23];
       p.kt_total = kt;
+      p.sx = pl.sx;
       p.splitk = pl.splitk;
       p.partial = n->partial;
       p.zero = c->zero;

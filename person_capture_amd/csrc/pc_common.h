@@ -61,6 +61,9 @@ struct ConvParams {
   // of each pixel (0: plain tensor). Output: hi = f16(v), lo = f16(v - hi); residual: hi + lo.
   int ysplit;
   int rsplit;
+  // f16x3 fused split tiles (conv_fast SX): a K tile is one (tap, hi channel block) staged with
+  // its lo block and both weight halves; seg cblk counts hi blocks, vwrap is the lo block offset
+  int sx;
 };
 
 // Direct convolution for tiny input channel counts (network stems, Cin <= 4).

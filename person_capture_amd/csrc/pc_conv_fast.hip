@@ -35,10 +35,17 @@ __host__ __device__ constexpr int fast_epi_bytes() {
 
 // OCC: workgroups per CU the tile is sized for (LDS <= 160 KiB / OCC); with OCC = 2 one
 // workgroup's epilogue and DMA waits overlap the other's MFMAs.
-// SPLIT: the f16x3 epilogue (split output / residual)
-template <typename T, int BC, int BP, int ROWB, int WC, int WP, int NSTAGE, int OCC = 1, bool SPLIT = false>
+// SPLIT: the f16x3 epilogue (split output / residual).
+// SX: fused f16x3 tiles over split inputs - a K tile is one (tap, hi channel block): the hi and
+// lo pixel rows and the W_hi and W_lo weight rows are staged together and every k-substep issues
+// W_hi*x_hi, W_lo*x_hi, W_hi*x_lo (2/3 of the staging and fragment reads of walking the virtual
+// [hi, lo, hi] blocks as plain tiles). The weight rows keep the [W_hi, W_hi, W_lo] per-tap layout
+// of the virtual K (the duplicate is skipped).
+template <typename T, int BC, int BP, int ROWB, int WC, int WP, int NSTAGE, int OCC = 1, bool SPLIT = false,
+          bool SX = false>
 __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fast(ConvParams p) {
   constexpr int NW = WC * WP;
+  constexpr int NH = SX ? 2 : 1;              // staged halves per tile
   constexpr int ESZ = sizeof(T);
   constexpr int CHUNKS = ROWB / 16;
   constexpr int BKE = ROWB / ESZ;             // K elements per tile
@@ -47,10 +54,11 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
   static_assert(NA % NW == 0, "every wave must issue the same weight DMA count");
   // im2col rows: when NB is not a multiple of the wave count, the last round of DMAs of
   // the waves past NB goes to a trash area, so every wave still issues NIB (static vmcnt)
-  constexpr int NIA = NA / NW, NIB = (NB + NW - 1) / NW, NI = NIA + NIB;
+  constexpr int NIA = NA / NW, NIB = (NB + NW - 1) / NW, NI = NH * (NIA + NIB);
+  static_assert(!SX || sizeof(T) == 2, "fused split tiles: f16 only");
   constexpr int WTC = BC / WC, WTP = BP / WP;
   constexpr int TC = WTC / 16, TP = WTP / 16;
-  constexpr int BUF = (BC + BP) * ROWB;
+  constexpr int BUF = NH * (BC + BP) * ROWB;
   constexpr int RING = NSTAGE * BUF;
   constexpr int EPI_MAX = OCC == 1 ? 131072 : 65536;
   constexpr int EPI = fast_epi_bytes<BC, BP, WC, WP, EPI_MAX>();
@@ -117,6 +125,10 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
   load_seg(p.seg[0]);
   int iseg = 0, ith = 0, itw = 0, icb = 0;
   const int seg0_kh = p.seg[0].KH;
+  // SX: weight K byte base of the current segment (segment 1 starts after segment 0's
+  // KH*KW taps of 3 x cblk virtual blocks)
+  int swk = 0;
+  const int swk1 = SX ? p.seg[0].KH * p.seg[0].KW * 3 * p.seg[0].cblk * ROWB : 0;
   const __amdgpu_buffer_rsrc_t wrs = rsrc(p.w);
 
   // DMA of the current iterator position (K-tile index kt) into ring slot `slot`
@@ -125,25 +137,36 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
     // MUBUF LDS-DMA (buffer_load ... lds), not FLAT global_load_lds: a pending FLAT op
     // counts in lgkmcnt too, so the compiler waited lgkmcnt(0) before the first MFMA of
     // every K-tile instead of counting the fragment reads
-    const int wso = kt * ROWB;
-    static_for<NIA>([&](auto ic) __attribute__((always_inline)) {
-      constexpr int i = decltype(ic)::value;
-      unsigned off = woff[i];
-      asm volatile("" : "+v"(off));
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_ptr_t)(smem + slot * BUF + (i * NW + wave) * 1024), 16, off,
-                                               wso, 0, 0);
+    // SX: W_hi of (tap, hi block icb) in the virtual per-tap layout [W_hi, W_hi, W_lo], W_lo 2 x cblk
+    // blocks further
+    const int wso = SX ? swk + ((ith * sKW + itw) * 3 * scblk + icb) * ROWB : kt * ROWB;
+    static_for<NH>([&](auto hc) __attribute__((always_inline)) {
+      constexpr int h = decltype(hc)::value;
+      static_for<NIA>([&](auto ic) __attribute__((always_inline)) {
+        constexpr int i = decltype(ic)::value;
+        unsigned off = woff[i];
+        asm volatile("" : "+v"(off));
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs,
+                                                 (lds_ptr_t)(smem + slot * BUF + h * BC * ROWB + (i * NW + wave) * 1024),
+                                                 16, off, wso + h * 2 * scblk * ROWB, 0, 0);
+      });
     });
-    // f16x3 split input: virtual blocks [hi, lo, hi] -> physical [hi, lo] (a scalar select)
-    const int xso = (svwrap && icb >= svwrap ? icb - svwrap : icb) * ROWB;
+    // f16x3 split input: virtual blocks [hi, lo, hi] -> physical [hi, lo] (a scalar select);
+    // SX: hi block icb, then its lo block icb + vwrap
+    const int xso = SX ? icb * ROWB : (svwrap && icb >= svwrap ? icb - svwrap : icb) * ROWB;
     const unsigned tapoff = (unsigned)((ith * sW + itw) * scs * ESZ);
-    static_for<NIB>([&](auto ic) __attribute__((always_inline)) {
-      constexpr int i = decltype(ic)::value;
-      const bool ok = (unsigned)(b_ih[i] + ith) < (unsigned)sH && (unsigned)(b_iw[i] + itw) < (unsigned)sW;
-      unsigned off = ok ? b_base[i] + tapoff : b_zero;
-      asm volatile("" : "+v"(off));
-      const int dst = (NB % NW == 0 || i * NW + wave < NB) ? slot * BUF + BC * ROWB + (i * NW + wave) * 1024
-                                                           : RING + wave * 1024;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)(smem + dst), 16, off, xso, 0, 0);
+    static_for<NH>([&](auto hc) __attribute__((always_inline)) {
+      constexpr int h = decltype(hc)::value;
+      static_for<NIB>([&](auto ic) __attribute__((always_inline)) {
+        constexpr int i = decltype(ic)::value;
+        const bool ok = (unsigned)(b_ih[i] + ith) < (unsigned)sH && (unsigned)(b_iw[i] + itw) < (unsigned)sW;
+        unsigned off = ok ? b_base[i] + tapoff : b_zero;
+        asm volatile("" : "+v"(off));
+        const int dst = (NB % NW == 0 || i * NW + wave < NB)
+                            ? slot * BUF + (NH * BC + h * BP) * ROWB + (i * NW + wave) * 1024
+                            : RING + wave * 1024;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)(smem + dst), 16, off, xso + h * svwrap * ROWB, 0, 0);
+      });
     });
   };
   // advance the issue iterator by one K-tile (no-op once the last tile was issued)
@@ -159,6 +182,7 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
     if (iseg == 0 && ith == seg0_kh) {   // once per launch, 2-segment convs only
       iseg = 1;
       ith = 0;
+      swk = swk1;
       load_seg(p.seg[1]);
     }
   };
@@ -173,7 +197,7 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
   const int fr = lane & 15;
   const int sw = (fr >> 1) & (CHUNKS - 1);
   const unsigned a_row = (wr * WTC + fr) * ROWB;
-  const unsigned b_row = (BC + wc * WTP + fr) * ROWB;
+  const unsigned b_row = (NH * BC + wc * WTP + fr) * ROWB;
   // Pinned two-k-substep schedule (f16, 128-byte K rows, two register sets fit beside the
   // accumulators): the 11 fragment reads of k-substep 0 go out first, the reads of k-substep 1
   // are interleaved one per MFMA with k-substep 0's MFMAs, and every MFMA waits (counted
@@ -181,7 +205,7 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
   // The compiler's own schedule waited lgkmcnt(0) for all of a substep's reads at the tile
   // start and again halfway through it (A fragments re-read into the same registers), which
   // exposed the LDS latency twice per K-tile on top of the barrier.
-  constexpr bool PINNED = ESZ == 2 && KSTEPS <= 2 && NW % 4 == 0 && KSTEPS * (TC + TP) * 4 + TC * TP * 4 <= 200;
+  constexpr bool PINNED = !SX && ESZ == 2 && KSTEPS <= 2 && NW % 4 == 0 && KSTEPS * (TC + TP) * 4 + TC * TP * 4 <= 200;
   auto compute_pinned = [&](auto slotc) __attribute__((always_inline)) {
     constexpr int slot = decltype(slotc)::value;
     const char* base = smem + slot * BUF;
@@ -209,6 +233,41 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
     const char* base = smem + slot * BUF;
     if constexpr (PINNED) {
       compute_pinned(slotc);
+      return;
+    }
+    if constexpr (SX) {
+#pragma unroll
+      for (int ks = 0; ks < KSTEPS; ++ks) {
+        const unsigned ko = ((ks * 4 + (lane >> 4)) ^ sw) << 4;
+        f16x8 fah[TC], fal[TC], fbh[TP], fbl[TP];
+#pragma unroll
+        for (int t = 0; t < TC; ++t) {
+          fah[t] = *reinterpret_cast<const f16x8*>(base + a_row + ko + t * 16 * ROWB);
+          fal[t] = *reinterpret_cast<const f16x8*>(base + a_row + BC * ROWB + ko + t * 16 * ROWB);
+        }
+#pragma unroll
+        for (int t = 0; t < TP; ++t) {
+          fbh[t] = *reinterpret_cast<const f16x8*>(base + b_row + ko + t * 16 * ROWB);
+          fbl[t] = *reinterpret_cast<const f16x8*>(base + b_row + BP * ROWB + ko + t * 16 * ROWB);
+        }
+        // three passes over the fragment grid (a dependent MFMA is TC*TP issues away)
+#pragma unroll
+        for (int a = 0; a < TC; ++a)
+#pragma unroll
+          for (int b = 0; b < TP; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fah[a], fbh[b], acc[a][b], 0, 0, 0);
+#pragma unroll
+        for (int a = 0; a < TC; ++a)
+#pragma unroll
+          for (int b = 0; b < TP; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fal[a], fbh[b], acc[a][b], 0, 0, 0);
+#pragma unroll
+        for (int a = 0; a < TC; ++a)
+#pragma unroll
+          for (int b = 0; b < TP; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fah[a], fbl[b], acc[a][b], 0, 0, 0);
+        if constexpr (TC * TP >= 16) __builtin_amdgcn_sched_barrier(0);
+      }
       return;
     }
 #pragma unroll
@@ -326,12 +385,28 @@ int conv_fast_tile(int cfg, int* bc, int* bp) {
   return 1;
 }
 
+// fused split tiles: two stages of the doubled tile (+ trash rows) and the epilogue image fit the LDS
+template <int BC, int BP, int ROWB, int NW, int OCC = 1>
+constexpr bool fast_sx_fits() {
+  constexpr int RING = 2 * 2 * (BC + BP) * ROWB + ((BP / (1024 / ROWB)) % NW ? NW * 1024 : 0);
+  return OCC == 1 && RING <= 163840;
+}
+
 template <typename T, int BC, int BP, int ROWB, int WC, int WP, int NSTAGE, int OCC = 1>
 static hipError_t launch_fast_cfg(const ConvParams& p, hipStream_t s) {
   if constexpr (!fast_valid<BC, BP, ROWB, WC * WP>()) {
     return hipErrorInvalidValue;
   } else {
     const int nwg = (p.M + BP - 1) / BP * (p.npad / BC);
+    if (p.sx) {   // fused f16x3 tiles: always the split epilogue, two stages
+      if constexpr (sizeof(T) == 2 && fast_sx_fits<BC, BP, ROWB, WC * WP, OCC>()) {
+        hipLaunchKernelGGL((conv_fast<T, BC, BP, ROWB, WC, WP, 2, OCC, true, true>), dim3(nwg), dim3(64 * WC * WP), 0,
+                           s, p);
+        return hipGetLastError();
+      } else {
+        return hipErrorInvalidValue;
+      }
+    }
     // the split epilogue only where it can differ: f16 power-of-two channel tiles (the others
     // take the per-fragment epilogue, which reads the split flags at run time)
     constexpr bool LDS_EPI = ((BC / 8) & (BC / 8 - 1)) == 0 && ((BC / 16) & (BC / 16 - 1)) == 0;
@@ -372,6 +447,17 @@ static hipError_t launch_fast_t(const ConvParams& p, int cfg, hipStream_t s) {
       else return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }
+}
+
+// can cfg run fused f16x3 split tiles (SX) at K rows of rowb bytes?
+int conv_fast_valid_sx(int cfg, int rowb) {
+  if (cfg < 0 || cfg >= kNumFastCfgs || (rowb != 64 && rowb != 128)) return 0;
+  if (cfg == 10 || cfg == 14) return 0;   // sized for 2 workgroups per CU
+  const FastCfg& c = kFastCfgs[cfg];
+  const int rpi = 1024 / rowb;
+  if ((c.bc / rpi) % c.nw || c.bp % rpi) return 0;
+  const int ring = 2 * 2 * (c.bc + c.bp) * rowb + ((c.bp / rpi) % c.nw ? c.nw * 1024 : 0);
+  return ring <= 163840;
 }
 
 // can cfg run convs whose K rows are rowb bytes?

@@ -4,7 +4,8 @@ Every activation of the split program is an f16 pair [hi | lo] and every conv wa
 [hi, lo, hi] against [W_hi, W_hi, W_lo]: the net must be f32-class against the fp32 oracle
 (oracle/nets_torch.scrfd_forward) on every conv kernel family that can run it - the split
 2-D block kernel (conv_t2d SPLIT), the statically scheduled kernel (conv_fast SPLIT
-epilogue) and the generic implicit GEMM (conv_igemm, run-time split flags) - with the split
+epilogue; fused split tiles - hi and lo pixel rows with both weight halves per K tile - or the
+virtual [hi, lo, hi] K) and the generic implicit GEMM (conv_igemm, run-time split flags) - with the split
 stem (W_hi + W_lo K steps) and the split max pool. The t2d and conv_fast paths accumulate K
 in the same order, so the whole net is bit-identical between them. At the detection level
 the f16x3 boxes and landmarks are the f32 path's (the property the headline's identical
@@ -58,7 +59,8 @@ def _heads_vs_oracle(ctx, p, variant, D, frames, env, monkeypatch):
 
 
 KERNEL_MODES = {
-    "default": {},                                             # split t2d (32-ch trunk) + conv_fast
+    "default": {},                                             # split t2d (32-ch trunk) + conv_fast fused tiles
+    "virtual": {"PC_SPLIT_FUSED": "0"},                        # conv_fast walking the virtual [hi, lo, hi] K
     "t2d64": {"PC_T2D_SPLIT64": "1"},                          # + the opt-in 64-channel split t2d
     "fast": {"PC_CONV_T2D": "0"},                              # conv_fast everywhere it runs
     "igemm": {"PC_CONV_T2D": "0", "PC_CONV_FAST": "0"},        # the generic kernel
