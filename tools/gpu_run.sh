@@ -12,6 +12,8 @@
 #   probe <script> [args...]      python tools/<script> args
 #   ab <libA> <libB> <reps> <script> [args]
 #                                 interleaved A/B of two library builds (PC_LIB_PATH), one box
+# Leading KEY=VALUE words of a step are exported for that step only, e.g.
+#   "PC_BENCH_NOPROF=1 bench c3 --frames per-frame"
 set -o pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$ROOT" || exit 1
@@ -22,8 +24,12 @@ i=0
 for step in "$@"; do
   i=$((i + 1))
   read -r -a a <<< "$step"
+  envs=()
+  while [[ ${#a[@]} -gt 0 && ${a[0]} == *=* ]]; do envs+=("${a[0]}"); a=("${a[@]:1}"); done
   kind=${a[0]}
   log=$O/${i}_${kind}.log
+  (
+  [ ${#envs[@]} -gt 0 ] && export "${envs[@]}"
   case $kind in
     suite)
       timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread \
@@ -50,6 +56,7 @@ for step in "$@"; do
     *)
       echo "unknown step: $step" > "$log"; false ;;
   esac
+  )
   rc=$?
   echo "step $i ($step): rc=$rc"
   tail -3 "$log" | cut -c1-400
