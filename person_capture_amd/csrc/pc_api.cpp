@@ -25,6 +25,7 @@ hipError_t conv_launch(int f32, int rowb, int cfg, const ConvParams& p, hipStrea
 hipError_t conv_halo_launch(int f32, int cfg, const ConvParams& p, hipStream_t s);
 hipError_t conv_fast_launch(int f32, int rowb, int cfg, const ConvParams& p, hipStream_t s);
 int conv_fast_num_cfgs();
+constexpr int kFastSmallCfg0 = 15;   // conv_fast tiles 15.. are for small-batch plans (pc_conv_fast.hip)
 int conv_fast_tile(int cfg, int* bc, int* bp);
 int conv_fast_valid(int cfg, int rowb);
 int conv_fast_valid_sx(int cfg, int rowb);
@@ -453,7 +454,7 @@ struct StemPlan {
   float* bias = nullptr;    // [npad]
   float* slope = nullptr;   // [npad] or null
 };
-struct ProfRec { int a, b, kind; double flops; int op = -1; int code = -1; int small = 0; };
+struct ProfRec { int a, b, kind; double flops; int op = -1; int code = -1; int small = -1; };   // small: plan class
 // A run of IResNet identity blocks executed by the resident chain kernel
 // (pc_conv_chain.hip): ops [first, first + 2*nblk) of the program.
 struct ChainBlockH { const void* w1; const float* b1; const float* s1; const void* w2; const float* b2; };
@@ -477,8 +478,10 @@ struct pc_net {
   std::vector<void*> arrays;  // device copies (conv weights in act dtype, others f32)
   std::vector<long long> array_count;
   std::vector<ConvPlan> plans;
-  std::vector<ConvPlan> plans_small;   // tiles chosen for small_batch images, used for N <= small_batch
-  int small_batch = 0;
+  // small-batch plan classes: plans_cls[c] holds the tiles chosen for cls_batch[c] images
+  // (ascending); a run of N images takes the first class with N <= cls_batch[c], else `plans`
+  std::vector<std::vector<ConvPlan>> plans_cls;
+  std::vector<int> cls_batch;
   std::vector<StemPlan> stems;
   std::vector<ChainPlan> chains;
   std::vector<int> chain_at;      // op index -> chain id (first op of a chain) or -1
@@ -644,16 +647,26 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
     }
     if ((double)npad * w[15] * esz >= 4294967296.0) ok = false;
     if (ok) {
-      static const double cost[] = {1.0, 1.12, 1.12, 1.3, 1.3, 1.3, 1.15, 1.45, 1.3, 1.0, 0.9, 1.3, 1.6, 1.0, 1.0};
-      static const int occ[] = {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 1, 1, 1, 2};   // workgroups per CU
+      // (15-19: small-batch tiles, latency-bound K loops: a second round of them costs about
+      // as much as the first, hence the high factor of the smallest)
+      static const double cost[] = {1.0, 1.12, 1.12, 1.3, 1.3, 1.3, 1.15, 1.45, 1.3, 1.0, 0.9, 1.3, 1.6, 1.0, 1.0,
+                                    1.9, 1.6, 1.6, 3.0, 1.9};
+      static const int occ[] = {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 1, 1, 1, 2, 1, 1, 1, 1, 1};   // workgroups per CU
+      static_assert(sizeof(cost) / sizeof(cost[0]) == sizeof(occ) / sizeof(occ[0]), "tile tables");
       int best = -1, best_rowb = rowb;
       double best_t = 0;
+      bool rows256 = small && !n->f32 && !any_split && rowb == 128 && !getenv("PC_CONV_ROWB");
+      for (int sg = 0; sg < nseg && rows256; ++sg) rows256 = (n->tens[w[3 + 5 * sg]].C * esz) % 256 == 0;
+      const bool no_small_tiles = getenv("PC_SMALL_TILES") && atoi(getenv("PC_SMALL_TILES")) == 0;   // A/B
       for (int k = 0; k < conv_fast_num_cfgs(); ++k) {
         int bc = 0, bp = 0;
         conv_fast_tile(k, &bc, &bp);
-        const int rb = (k == 10 || k == 14) ? 64 : rowb;   // cfgs 10 and 14 run on 64-byte K rows only
+        // cfgs 10 and 14 run on 64-byte K rows only; the small-batch tiles 15-17 take 256-byte
+        // rows where every segment's channels allow (half the barrier-separated K tiles)
+        const int rb = (k == 10 || k == 14) ? 64 : (k >= 15 && k <= 17 && rows256) ? 256 : rowb;
         if (npad % bc || !conv_fast_valid(k, rb)) continue;
         if (force > 0 && k != force - 1) continue;
+        if (k >= kFastSmallCfg0 && (!small || no_small_tiles) && force <= 0) continue;   // small-batch tiles
         const long long t = (M + bp - 1) / bp * (npad / bc);
         const double rounds = (double)((t + 256 * occ[k] - 1) / (256 * occ[k]));
         const double est = rounds * bc * bp * occ[k] * cost[k];
@@ -666,6 +679,7 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
           int bc = 0, bp = 0;
           conv_fast_tile(k, &bc, &bp);
           if (npad % bc || (force > 0 && k != force - 1)) continue;
+          if (k >= kFastSmallCfg0 && (!small || no_small_tiles) && force <= 0) continue;
           for (int rb : {rowb, 64}) {
             if (!conv_fast_valid_sx(k, rb)) continue;
             const long long t = (M + bp - 1) / bp * (npad / bc);
@@ -1021,8 +1035,15 @@ extern "C" int pc_net_create(pc_ctx* c, const void* prog, size_t nbytes, int pre
   n->host_arrays.assign(narr, nullptr);
   for (int i = 0; i < narr; ++i) n->host_arrays[i] = data + arr[i].first;
   n->plans.resize(n->ops.size());
-  n->small_batch = max_batch > 2 && !getenv("PC_NO_SMALL_PLANS") ? std::max(1, std::min(16, max_batch / 4)) : 0;
-  n->plans_small.resize(n->ops.size());
+  // Small-batch classes 1, 4, 16, 32, 64 images up to a quarter of max_batch: a per-frame
+  // extract() runs SCRFD on 1 image and ArcFace on 2 x its faces (2-30 rows); a net of 64
+  // (SCRFD) keeps 1 / 4 / 16, so its 32-frame C3 chunks stay on the max-batch tiles (r03:
+  // the 16-image tiles at 32 images cost 0.4 ms per step).
+  n->cls_batch.clear();
+  if (max_batch > 2 && !getenv("PC_NO_SMALL_PLANS"))
+    for (int b : {1, 4, 16, 32, 64})
+      if (b <= std::max(1, max_batch / 4)) n->cls_batch.push_back(b);
+  n->plans_cls.assign(n->cls_batch.size(), std::vector<ConvPlan>(n->ops.size()));
   n->stems.resize(n->ops.size());
   size_t part = 0, stem_col_bytes = 0;
   for (size_t i = 0; i < n->ops.size() && rc == PC_OK; ++i) {
@@ -1032,11 +1053,13 @@ extern "C" int pc_net_create(pc_ctx* c, const void* prog, size_t nbytes, int pre
       if (rc) break;
       // small batches (per-frame extract: one frame's faces, prescan samples) get their own
       // tile choice: the max-batch tiles would leave most CUs idle
-      if (n->small_batch > 0) rc = plan_conv(n, op, n->plans_small[i], n->small_batch, true);
+      for (size_t c = 0; c < n->cls_batch.size() && rc == PC_OK; ++c) {
+        ConvPlan& sp = n->plans_cls[c][i];
+        rc = plan_conv(n, op, sp, n->cls_batch[c], true);
+        if (rc == PC_OK && sp.splitk > 1)
+          part = std::max(part, (size_t)((long long)sp.splitk * sp.M_per_image * n->cls_batch[c] * op.w[14] * 4));
+      }
       if (rc) break;
-      if (n->small_batch > 0 && n->plans_small[i].splitk > 1)
-        part = std::max(part, (size_t)((long long)n->plans_small[i].splitk * n->plans_small[i].M_per_image *
-                                       n->small_batch * op.w[14] * 4));
       const ConvPlan& pl = n->plans[i];
       if (pl.splitk > 1) part = std::max(part, (size_t)((long long)pl.splitk * pl.M_per_image * max_batch * op.w[14] * 4));
       const NetTensor& Y = n->tens[op.w[1]];
@@ -1124,6 +1147,13 @@ static int prof_event(pc_net* n, int* idx) {
   return PC_OK;
 }
 
+// plan class of a run of N images (-1: the max-batch plans)
+static int plan_class(const pc_net* n, int N) {
+  for (size_t c = 0; c < n->cls_batch.size(); ++c)
+    if (N <= n->cls_batch[c]) return (int)c;
+  return -1;
+}
+
 static int run_ops(pc_net* n, int N) {
   pc_ctx* c = n->ctx;
   hipStream_t s = c->stream;
@@ -1173,9 +1203,9 @@ static int run_ops(pc_net* n, int N) {
       }
     }
     if (w[0] == OP_CONV) {
-      const bool small = N <= n->small_batch;   // (N up to 2x measured worse: SCRFD at 32 of 64)
-      const ConvPlan& pl = small ? n->plans_small[i] : n->plans[i];
-      rec.small = small;
+      const int cls = plan_class(n, N);
+      const ConvPlan& pl = cls >= 0 ? n->plans_cls[cls][i] : n->plans[i];
+      rec.small = cls;
       ConvParams p;
       memset(&p, 0, sizeof(p));
       const NetTensor& Y = n->tens[w[1]];
@@ -1378,7 +1408,7 @@ extern "C" int pc_net_profile_read(pc_net* n, double* out) {
 }
 
 // Per-record detail of the profiled runs: 6 doubles per record
-// [op index, kind, ms, flops, kernel (100+k fast tile k, k halo tile k, -1 igemm), igemm cfg]; returns the count.
+// [op index, kind, ms, flops, kernel (100+k fast tile k, 200+v t2d variant v, 300 resident chain, k halo tile k, -1 igemm), igemm cfg]; returns the count.
 extern "C" int pc_net_profile_ops(pc_net* n, double* out, int max_recs) {
   if (!n || !out) return -PC_ERR_ARG;
   HIPCHK(n->ctx, hipStreamSynchronize(n->ctx->stream));
@@ -1390,9 +1420,12 @@ extern "C" int pc_net_profile_ops(pc_net* n, double* out, int max_recs) {
     double* o = out + 6 * k++;
     const bool conv = r.op >= 0 && n->ops[r.op].w[0] == OP_CONV;
     o[0] = r.op; o[1] = r.kind; o[2] = ms; o[3] = r.flops;
-    const ConvPlan* pl = conv ? (r.small ? &n->plans_small[r.op] : &n->plans[r.op]) : nullptr;
-    o[4] = r.code >= 0 ? r.code : conv ? (pl->t2d >= 0 ? 200 + pl->t2d : pl->fast >= 0 ? 100 + pl->fast : pl->halo)
-                                       : -1;
+    const ConvPlan* pl = conv ? (r.small >= 0 ? &n->plans_cls[r.small][r.op] : &n->plans[r.op]) : nullptr;
+    o[4] = r.code >= 0 ? r.code
+                       : conv ? (pl->t2d >= 0      ? 200 + pl->t2d
+                                 : pl->fast >= 0   ? 100 + pl->fast
+                                                   : pl->halo)
+                              : -1;
     o[5] = conv ? pl->cfg : -1;
   }
   return k;

@@ -21,7 +21,8 @@
 //
 // LDS rows are ROWB bytes (one tap x ROWB of channels for the im2col side, one
 // output channel x ROWB of K for the weights); 16-byte chunk c of row r sits at
-// c ^ ((r >> 1) & (CHUNKS - 1)) - bank-conflict-free ds_read_b128 fragment reads.
+// c ^ ((r >> 1) & (CHUNKS - 1)) - bank-conflict-free ds_read_b128 fragment reads (256-byte rows,
+// which all start at bank 0: c ^ (r & 15)).
 #include "pc_conv_common.h"
 
 namespace pc {
@@ -66,7 +67,11 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
   constexpr int SMEM = RING + TRASH > EPI ? RING + TRASH : EPI;
   static_assert(SMEM * OCC <= 163840, "LDS");
   static_assert(WTC % 16 == 0 && WTP % 16 == 0, "wave tile");
+  static_assert(ROWB == 64 || ROWB == 128 || (ROWB == 256 && ESZ == 2 && !SX), "K row width");
+  // LDS chunk swizzle of row r (a fragment read's 16 rows hit 16 distinct 4-bank groups)
+  auto swz = [](int r) __attribute__((always_inline)) { return ROWB == 256 ? (r & 15) : ((r >> 1) & (CHUNKS - 1)); };
   static_assert(NSTAGE >= 2, "ring depth");
+  static_assert((NSTAGE - 2) * NI <= 63, "DMAs in flight exceed the vmcnt range");
 
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
@@ -87,7 +92,7 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
   static_for<NIA>([&](auto ic) __attribute__((always_inline)) {
     constexpr int i = decltype(ic)::value;
     const int r = (i * NW + wave) * RPI + lrow;
-    woff[i] = (unsigned)((long long)(c0 + r) * p.ktot * ESZ) + ((pchunk ^ ((r >> 1) & (CHUNKS - 1))) << 4);
+    woff[i] = (unsigned)((long long)(c0 + r) * p.ktot * ESZ) + ((pchunk ^ swz(r)) << 4);
   });
   // im2col rows: window origin (ih0, iw0) and byte offset of the staged row's output
   // pixel under the current segment (recomputed from the pixel index at a segment switch)
@@ -111,7 +116,7 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
     static_for<NIB>([&](auto ic) __attribute__((always_inline)) {
       constexpr int i = decltype(ic)::value;
       const int r = (i * NW + wave) * RPI + lrow;
-      const unsigned lc = (unsigned)((pchunk ^ ((r >> 1) & (CHUNKS - 1))) << 4);
+      const unsigned lc = (unsigned)((pchunk ^ swz(r)) << 4);
       const int q = p0 + r;
       const int n = q / hw, rem = q - n * hw;
       const int oh = q < p.M ? rem / p.OW : -(1 << 16);   // rows past M never pass the bounds test
@@ -195,7 +200,7 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
 
   constexpr int KSTEPS = ESZ == 2 ? BKE / 32 : BKE / 4;
   const int fr = lane & 15;
-  const int sw = (fr >> 1) & (CHUNKS - 1);
+  const int sw = swz(fr);
   const unsigned a_row = (wr * WTC + fr) * ROWB;
   const unsigned b_row = (NH * BC + wc * WTP + fr) * ROWB;
   // Pinned two-k-substep schedule (f16, 128-byte K rows, two register sets fit beside the
@@ -373,6 +378,16 @@ static const FastCfg kFastCfgs[] = {
     {32, 256, 2},    // 12: 1x2 waves, 32x128 per wave (detector heads, npad 32)
     {256, 224, 8},   // 13: 4x2 waves, 64x112 per wave: 50176-pixel layers (b256 14x14) fill 224 CUs
     {128, 224, 4},   // 14: 2x2 waves, 64x112 per wave, ROWB 64 only, 3 stages, 2 workgroups per CU
+    // small-batch plans only (pc_api.cpp plan_conv): a per-frame extract()'s 12 ArcFace rows give a
+    // 14x14x256 conv 2352 output pixels - 80 of the tiles above; these cover the CUs. A small tile's
+    // K loop is a chain of L2/HBM round trips (a few MFMAs per K tile), so its ring is deep: the
+    // DMA runs NSTAGE-1 tiles ahead (r04: 3 stages left the 64x64 tile at ~18 us per 14x14x256
+    // conv of 12 images, 36 K tiles x ~0.5 us of exposed latency)
+    {64, 64, 4},     // 15: 2x2 waves, 32x32 per wave, 8 stages
+    {64, 128, 4},    // 16: 2x2 waves, 32x64 per wave, 6 stages
+    {128, 64, 4},    // 17: 2x2 waves, 64x32 per wave, 6 stages
+    {32, 64, 2},     // 18: 1x2 waves, 32x32 per wave, 8 stages (npad 32 / 96 / 160 / 224)
+    {96, 64, 2},     // 19: 1x2 waves, 96x32 per wave, 7 stages (ROWB 64: 8)
 };
 static const int kNumFastCfgs = sizeof(kFastCfgs) / sizeof(kFastCfgs[0]);
 
@@ -385,11 +400,22 @@ int conv_fast_tile(int cfg, int* bc, int* bp) {
   return 1;
 }
 
-// fused split tiles: two stages of the doubled tile (+ trash rows) and the epilogue image fit the LDS
-template <int BC, int BP, int ROWB, int NW, int OCC = 1>
+// fused split tiles: NS stages of the doubled tile (+ trash rows) fit the LDS
+template <int BC, int BP, int ROWB, int NW, int OCC = 1, int NS = 2>
 constexpr bool fast_sx_fits() {
-  constexpr int RING = 2 * 2 * (BC + BP) * ROWB + ((BP / (1024 / ROWB)) % NW ? NW * 1024 : 0);
+  constexpr int RING = NS * 2 * (BC + BP) * ROWB + ((BP / (1024 / ROWB)) % NW ? NW * 1024 : 0);
   return OCC == 1 && RING <= 163840;
+}
+// ring depth of a fused split tile: the plain tile's depth (at most 4 for the large tiles,
+// whose MFMA work per K tile hides the DMA), bounded by the LDS and by the 6-bit vmcnt
+// ((NS - 2) x DMAs in flight per wave <= 63)
+template <int BC, int BP, int ROWB, int NW, int NSTAGE>
+constexpr int fast_sx_stages() {
+  constexpr int NI = 2 * (BC / (1024 / ROWB) / NW + (BP / (1024 / ROWB) + NW - 1) / NW);
+  int ns = NSTAGE < 4 ? NSTAGE : (BC * BP >= 16384 ? 4 : NSTAGE);
+  while (ns > 2 && ((ns - 2) * NI > 63 || ns * 2 * (BC + BP) * ROWB + ((BP / (1024 / ROWB)) % NW ? NW * 1024 : 0) > 163840))
+    --ns;
+  return ns;
 }
 
 template <typename T, int BC, int BP, int ROWB, int WC, int WP, int NSTAGE, int OCC = 1>
@@ -398,9 +424,10 @@ static hipError_t launch_fast_cfg(const ConvParams& p, hipStream_t s) {
     return hipErrorInvalidValue;
   } else {
     const int nwg = (p.M + BP - 1) / BP * (p.npad / BC);
-    if (p.sx) {   // fused f16x3 tiles: always the split epilogue, two stages
-      if constexpr (sizeof(T) == 2 && fast_sx_fits<BC, BP, ROWB, WC * WP, OCC>()) {
-        hipLaunchKernelGGL((conv_fast<T, BC, BP, ROWB, WC, WP, 2, OCC, true, true>), dim3(nwg), dim3(64 * WC * WP), 0,
+    if (p.sx) {   // fused f16x3 tiles: always the split epilogue
+      constexpr int NS = fast_sx_stages<BC, BP, ROWB, WC * WP, NSTAGE>();
+      if constexpr (sizeof(T) == 2 && ROWB != 256 && fast_sx_fits<BC, BP, ROWB, WC * WP, OCC, NS>()) {
+        hipLaunchKernelGGL((conv_fast<T, BC, BP, ROWB, WC, WP, NS, OCC, true, true>), dim3(nwg), dim3(64 * WC * WP), 0,
                            s, p);
         return hipGetLastError();
       } else {
@@ -445,6 +472,22 @@ static hipError_t launch_fast_t(const ConvParams& p, int cfg, hipStream_t s) {
     case 14:
       if constexpr (ROWB == 64) return launch_fast_cfg<T, 128, 224, 64, 2, 2, 3, 2>(p, s);
       else return hipErrorInvalidValue;
+    case 15: return launch_fast_cfg<T, 64, 64, ROWB, 2, 2, 8>(p, s);
+    case 16: return launch_fast_cfg<T, 64, 128, ROWB, 2, 2, 6>(p, s);
+    case 17: return launch_fast_cfg<T, 128, 64, ROWB, 2, 2, 6>(p, s);
+    case 18: return launch_fast_cfg<T, 32, 64, ROWB, 1, 2, 8>(p, s);
+    case 19: return launch_fast_cfg<T, 96, 64, ROWB, 1, 2, ROWB == 128 ? 7 : 8>(p, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// 256-byte K rows (128 f16 channels, half the K tiles of 128-byte rows): the small-batch tiles,
+// whose K loop is a chain of barrier-separated K tiles
+static hipError_t launch_fast_256(const ConvParams& p, int cfg, hipStream_t s) {
+  switch (cfg) {
+    case 15: return launch_fast_cfg<f16, 64, 64, 256, 2, 2, 4>(p, s);
+    case 16: return launch_fast_cfg<f16, 64, 128, 256, 2, 2, 3>(p, s);
+    case 17: return launch_fast_cfg<f16, 128, 64, 256, 2, 2, 3>(p, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -462,6 +505,7 @@ int conv_fast_valid_sx(int cfg, int rowb) {
 
 // can cfg run convs whose K rows are rowb bytes?
 int conv_fast_valid(int cfg, int rowb) {
+  if (rowb == 256) return cfg >= 15 && cfg <= 17;   // f16 only (conv_fast_launch)
   if (cfg < 0 || cfg >= kNumFastCfgs || (rowb != 64 && rowb != 128)) return 0;
   const FastCfg& c = kFastCfgs[cfg];
   if ((cfg == 10 || cfg == 14) && rowb != 64) return 0;   // sized for 2 workgroups per CU at 64-byte K rows
@@ -471,8 +515,9 @@ int conv_fast_valid(int cfg, int rowb) {
 
 hipError_t conv_fast_launch(int f32, int rowb, int cfg, const ConvParams& p, hipStream_t s) {
   if (cfg < 0 || cfg >= kNumFastCfgs || p.splitk != 1 || p.npad % kFastCfgs[cfg].bc || p.nseg < 1 || p.nseg > 2 ||
-      (rowb != 64 && rowb != 128))
+      (rowb != 64 && rowb != 128 && rowb != 256))
     return hipErrorInvalidValue;
+  if (rowb == 256) return f32 || p.sx ? hipErrorInvalidValue : launch_fast_256(p, cfg, s);
   if (f32) return rowb == 128 ? launch_fast_t<float, 128>(p, cfg, s) : launch_fast_t<float, 64>(p, cfg, s);
   return rowb == 128 ? launch_fast_t<f16, 128>(p, cfg, s) : launch_fast_t<f16, 64>(p, cfg, s);
 }

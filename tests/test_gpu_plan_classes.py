@@ -1,0 +1,67 @@
+"""Small-batch plan classes (pc_api.cpp plan_conv / plan_class): a run of a few images takes
+the tiles planned for its batch class (1 / 4 / 16 / 32 / 64 images, up to a quarter of
+max_batch) - including the deep-ring small conv_fast tiles 15-19 that only those plans use.
+Tile shape and ring depth do not change any output's K order, so the same rows must come out
+bit for bit as inside a large batch (the max-batch plans): extract() and extract_batch() are
+bit-identical by contract (test_gpu_face_embedder). The f16x3 split program too."""
+import numpy as np
+import pytest
+
+from person_capture_amd import models
+from person_capture_amd._lib import PC_PREC_F16
+from person_capture_amd.runtime import Net
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(ctx, net, x, N, outs):
+    d = ctx.upload(np.ascontiguousarray(x[:N]))
+    net.profile(True)
+    net.run(d.ptr, N)
+    codes = [int(r[4]) for r in net.profile_ops()]
+    net.profile(False)
+    res = [net.read_output(k, N).copy() for k in range(outs)]
+    d.free()
+    return res, codes
+
+
+def _images(n, side, seed):
+    x = np.zeros((n, side, side, 4), np.float16)
+    x[..., :3] = np.random.default_rng(seed).uniform(-1, 1, (n, side, side, 3))
+    return x
+
+
+@pytest.mark.parametrize("depth", [100, 50])
+def test_arcface_small_batches_bit_identical_to_large_batch(gpu_ctx, depth):
+    P = models.compile_iresnet(models.synth_iresnet(depth, seed=4), depth)
+    net = Net(gpu_ctx, P.serialize(), PC_PREC_F16, max_batch=512)
+    try:
+        x = _images(200, 112, 9)
+        (large,), _ = _run(gpu_ctx, net, x, 200, 1)
+        ran_small = 0
+        for N in (1, 2, 5, 12, 30, 64):
+            (small,), codes = _run(gpu_ctx, net, x, N, 1)
+            ran_small += sum(1 for c in codes if 115 <= c < 120)   # conv_fast small-batch tiles
+            assert small.dtype == large.dtype
+            assert np.array_equal(small.view(np.uint8), large[:N].view(np.uint8)), \
+                (N, float(np.abs(small.astype(np.float64) - large[:N]).max()))
+        assert ran_small >= 100, ran_small
+    finally:
+        net.close()
+
+
+@pytest.mark.parametrize("split", [False, True])
+def test_scrfd_single_frame_bit_identical_to_batch(gpu_ctx, split):
+    P = models.compile_scrfd(models.synth_scrfd("10g", seed=2), "10g", 320, split=split)
+    net = Net(gpu_ctx, P.serialize(), PC_PREC_F16, max_batch=64)   # f16x3: a split program on an f16 net
+    try:
+        x = _images(40, 320, 3)
+        nout = len(P.outputs)
+        large, _ = _run(gpu_ctx, net, x, 40, nout)
+        for N in (1, 3, 16):
+            small, codes = _run(gpu_ctx, net, x, N, nout)
+            assert any(115 <= c < 120 for c in codes), codes
+            for k in range(nout):
+                assert np.array_equal(small[k].view(np.uint8), large[k][:N].view(np.uint8)), (N, k)
+    finally:
+        net.close()

@@ -1,6 +1,6 @@
 """Single-conv microbenchmark of the implicit-GEMM engine (HIP-event timed).
 usage: python tools/probe_conv.py [cfg[:rowb] ...]   (cfg "auto" = planner's choice)
-env PROBE_SHAPES=name1,name2 restricts the shapes; PROBE_SPLIT=1 probes the f16x3 split form
+env PROBE_SHAPES=name1,name2 restricts the shapes; PROBE_N=n overrides their batch; PROBE_SPLIT=1 probes the f16x3 split form
 (split input and output, DESIGN.md §3.6: a 1x1 conv writes the split input first; only the
 probed conv is timed)."""
 import os
@@ -56,6 +56,7 @@ def main():
     for name, N, H, cin, cout, k, s in SHAPES:
         if only and name not in only:
             continue
+        N = int(os.environ.get("PROBE_N", N))
         P = build(N, H, cin, cout, k, s)
         x = np.random.default_rng(1).standard_normal((N, H, H, cin)).astype(np.float16)
         d = ctx.upload(x)
@@ -85,7 +86,7 @@ def main():
             else:
                 os.environ["PC_CONV_CFG"] = c
             try:
-                net = Net(ctx, P.serialize(), PC_PREC_F16, max_batch=N)
+                net = Net(ctx, P.serialize(), PC_PREC_F16, max_batch=int(os.environ.get("PROBE_MAXB", N)))
             except RuntimeError as e:
                 print(f"{name:16s} cfg {spec:6s} n/a ({e})", flush=True)
                 continue
@@ -101,7 +102,7 @@ def main():
             us = ms * 1e3 / len(recs)
             tf = sum(r[3] for r in recs) / (ms * 1e-3) / 1e12
             code = int(recs[0][4])
-            ran = f"t{code - 200}" if code >= 200 else (f"f{code - 100}" if code >= 100 else
+            ran = "chain" if code == 300 else f"t{code - 200}" if code >= 200 else (f"f{code - 100}" if code >= 100 else
                                                          (f"h{code}" if code >= 0 else f"g{int(recs[0][5])}"))
             print(f"{name:16s} cfg {spec:6s} ran {ran:4s} {us:9.1f} us/launch  {tf:7.1f} TFLOP/s", flush=True)
             net.close()

@@ -1,6 +1,7 @@
 """Per-layer profile of the two trunks (HIP events around every launch, pc_net_profile_ops).
 usage: python tools/probe_layers.py [arc|scrfd|scrfdx3] [batch]   -> table grouped by conv shape.
-scrfdx3: the f16x3 split SCRFD program."""
+scrfdx3: the f16x3 split SCRFD program.
+PROBE_MAXB=N: create the net for N images (the small-batch plans then serve batch <= min(16, N/4))."""
 import sys
 from collections import defaultdict
 
@@ -37,7 +38,7 @@ def main():
         P = models.compile_scrfd(models.synth_scrfd("10g", seed=0, calibrate=False), "10g", 640,
                                  split=which == "scrfdx3")
     prec = PC_PREC_F32 if os.environ.get('PROBE_F32') else PC_PREC_F16
-    net = Net(ctx, P.serialize(), prec, max_batch=B)
+    net = Net(ctx, P.serialize(), prec, max_batch=int(os.environ.get('PROBE_MAXB', B)))   # FaceEmbedder: 512 for arc
     H, W, Cc = P.dims(P.input)
     x = np.zeros((B, H, W, Cc), np.float32 if prec == PC_PREC_F32 else np.float16)
     x[..., :3] = np.random.default_rng(0).standard_normal((B, H, W, 3))
@@ -56,7 +57,7 @@ def main():
         key = describe(P, P.ops[int(op)])
         a = agg[key]
         a[0] += 1; a[1] += ms; a[2] += fl
-        a[3] = (f"t{int(halo) - 200}" if halo >= 200 else f"f{int(halo) - 100}" if halo >= 100 else f"h{int(halo)}") \
+        a[3] = ("c" if halo == 300 else f"t{int(halo) - 200}" if halo >= 200 else f"f{int(halo) - 100}" if halo >= 100 else f"h{int(halo)}") \
             if halo >= 0 else \
             (f"g{int(cfg)}" if cfg >= 0 else "-")
         tot_ms += ms; tot_fl += fl
