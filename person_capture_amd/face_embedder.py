@@ -269,7 +269,7 @@ class FaceEmbedder(YoloFaceBranch):
         # host frames (extract / extract_batch without dev_frames) reach the device through the
         # native pinned staging ring on a copy stream of their own (pc_frame_stage)
         self._h2d = get_context(self._device_index, "h2d")
-        self._stage_threads = int(os.getenv("PERSON_CAPTURE_AMD_STAGE_THREADS", "4"))
+        self._stage_threads = int(os.getenv("PERSON_CAPTURE_AMD_STAGE_THREADS", "8"))
         self._arc = ArcFaceEngine(self._ectx, self._arc_params, self._arc_depth, precision=self.precision,
                                   max_batch=self._arc_batch)
         # HIP graphs for small net runs (unchanged callers' per-frame extract(): a SCRFD pass of one
