@@ -596,6 +596,7 @@ struct pc_net {
   size_t in_img_bytes = 0;
   // graph replay (runs of at most graph_max_batch images)
   int use_graph = 0;
+  int capturing = 0;   // inside hipStreamBeginCapture .. EndCapture
   int graph_max_batch = 1 << 30;
   // per-op HIP-event profiling (pc_net_profile)
   int prof = 0;
@@ -1254,7 +1255,8 @@ static int plan_class(const pc_net* n, int N) {
 static int run_ops(pc_net* n, int N) {
   pc_ctx* c = n->ctx;
   hipStream_t s = c->stream;
-  const bool prof = n->prof && !n->use_graph;
+  // eager runs are profiled; a captured run records no events (its replays are not profiled)
+  const bool prof = n->prof && !n->capturing;
   if (n->in_copy)
     HIPCHK(c, hipMemcpyAsync(n->in_copy, n->cur_input, n->in_img_bytes * N, hipMemcpyDeviceToDevice, s));
   // one event per op boundary: an op's end event is the next op's start event
@@ -1539,7 +1541,9 @@ extern "C" int pc_net_run(pc_net* n, const void* d_in, int N) {
   if (it == n->graphs.end()) {
     hipGraph_t g;
     HIPCHK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    n->capturing = 1;
     int rc = run_ops(n, N);
+    n->capturing = 0;
     hipError_t e = hipStreamEndCapture(c->stream, &g);
     if (rc != PC_OK) return rc;
     if (e != hipSuccess) return fail(c, PC_ERR_HIP, std::string("graph capture: ") + hipGetErrorString(e));

@@ -406,13 +406,14 @@ constexpr bool fast_sx_fits() {
   constexpr int RING = NS * 2 * (BC + BP) * ROWB + ((BP / (1024 / ROWB)) % NW ? NW * 1024 : 0);
   return OCC == 1 && RING <= 163840;
 }
-// ring depth of a fused split tile: the plain tile's depth (at most 4 for the large tiles,
-// whose MFMA work per K tile hides the DMA), bounded by the LDS and by the 6-bit vmcnt
-// ((NS - 2) x DMAs in flight per wave <= 63)
+// ring depth of a fused split tile: two stages, or the small-batch tiles' deep rings bounded by
+// the LDS and by the 6-bit vmcnt ((NS - 2) x DMAs in flight per wave <= 63)
 template <int BC, int BP, int ROWB, int NW, int NSTAGE>
 constexpr int fast_sx_stages() {
   constexpr int NI = 2 * (BC / (1024 / ROWB) / NW + (BP / (1024 / ROWB) + NW - 1) / NW);
-  int ns = NSTAGE < 4 ? NSTAGE : (BC * BP >= 16384 ? 4 : NSTAGE);
+  // (the deep-ring small-batch tiles only: 4 stages on the 32x256 split tiles cost SCRFD-x3 b64
+  // 13.0 -> 13.7 ms, r04l, against the 2 of round 4's first SX build)
+  int ns = NSTAGE >= 6 ? NSTAGE : 2;
   while (ns > 2 && ((ns - 2) * NI > 63 || ns * 2 * (BC + BP) * ROWB + ((BP / (1024 / ROWB)) % NW ? NW * 1024 : 0) > 163840))
     --ns;
   return ns;

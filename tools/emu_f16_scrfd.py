@@ -22,13 +22,13 @@ def _split(t):
     return hi, (t - hi).half().float()
 
 
-def run(p, x, keep32=lambda i: False, w16=True, a16=True, x3=False, w2=False):
+def run(p, x, keep32=lambda i: False, w16=True, a16=True, x3=False, w2=False, x3sel=None):
     i = [0]
 
     def conv(inp, w, b=None, *a, **k):
         j = i[0]
         i[0] += 1
-        if x3:   # f16x3: hi*hi + lo*hi + hi*lo, f32 accumulation (the dropped lo*lo ~2^-22)
+        if x3 or (x3sel is not None and x3sel(j)):   # f16x3: hi*hi + lo*hi + hi*lo, f32 accumulation
             xh, xl = _split(inp)
             wh, wl = _split(w)
             return _conv(xh, wh, b, *a, **k) + _conv(xl, wh, None, *a, **k) + _conv(xh, wl, None, *a, **k)
@@ -88,6 +88,13 @@ def main():
     print(f"{'f16 acts, W hi+lo (2x K)':26s}: {err(out)}", flush=True)
     out, _ = run(p, x, x3=True)
     print(f"{'f16x3 (hi/lo split)':26s}: {err(out)}", flush=True)
+    # mixed programs (r04): f16x3 on one group, plain f16 storage/weights elsewhere
+    mixed = {"x3 stem+backbone": lambda i: i < bb_end, "x3 backbone+neck": lambda i: i < neck_end,
+             "x3 all but heads": lambda i: i < neck_end, "x3 all but stem": lambda i: i >= 3,
+             "x3 heads+neck": lambda i: i >= bb_end, "x3 2nd half bb+": lambda i: i >= (3 + bb_end) // 2}
+    for name, k in mixed.items():
+        out, _ = run(p, x, x3sel=k)
+        print(f"{name:26s}: {err(out)}", flush=True)
 
 
 if __name__ == "__main__":
