@@ -1,7 +1,7 @@
 """Small-batch plan classes (pc_api.cpp plan_conv / plan_class): a run of a few images takes
 the tiles planned for its batch class (1 / 4 / 16 / 32 / 64 images, up to a quarter of
 max_batch) - including the deep-ring small conv_fast tiles 15-19 that only those plans use.
-Tile shape and ring depth do not change any output's K order, so the same rows must come out
+Tile shape, ring depth and K-row width do not change any output's K order, so the same rows must come out
 bit for bit as inside a large batch (the max-batch plans): extract() and extract_batch() are
 bit-identical by contract (test_gpu_face_embedder). The f16x3 split program too."""
 import numpy as np

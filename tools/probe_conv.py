@@ -102,7 +102,7 @@ def main():
             us = ms * 1e3 / len(recs)
             tf = sum(r[3] for r in recs) / (ms * 1e-3) / 1e12
             code = int(recs[0][4])
-            ran = "chain" if code == 300 else f"t{code - 200}" if code >= 200 else (f"f{code - 100}" if code >= 100 else
+            ran = f"i{code - 400}" if code >= 400 else "chain" if code == 300 else f"t{code - 200}" if code >= 200 else (f"f{code - 100}" if code >= 100 else
                                                          (f"h{code}" if code >= 0 else f"g{int(recs[0][5])}"))
             print(f"{name:16s} cfg {spec:6s} ran {ran:4s} {us:9.1f} us/launch  {tf:7.1f} TFLOP/s", flush=True)
             net.close()

@@ -57,7 +57,7 @@ def main():
         key = describe(P, P.ops[int(op)])
         a = agg[key]
         a[0] += 1; a[1] += ms; a[2] += fl
-        a[3] = ("c" if halo == 300 else f"t{int(halo) - 200}" if halo >= 200 else f"f{int(halo) - 100}" if halo >= 100 else f"h{int(halo)}") \
+        a[3] = (f"i{int(halo) - 400}" if halo >= 400 else "c" if halo == 300 else f"t{int(halo) - 200}" if halo >= 200 else f"f{int(halo) - 100}" if halo >= 100 else f"h{int(halo)}") \
             if halo >= 0 else \
             (f"g{int(cfg)}" if cfg >= 0 else "-")
         tot_ms += ms; tot_fl += fl
