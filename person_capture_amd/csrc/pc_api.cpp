@@ -28,7 +28,7 @@ hipError_t conv_launch(int f32, int rowb, int cfg, const ConvParams& p, hipStrea
 hipError_t conv_halo_launch(int f32, int cfg, const ConvParams& p, hipStream_t s);
 hipError_t conv_fast_launch(int f32, int rowb, int cfg, const ConvParams& p, hipStream_t s);
 int conv_fast_num_cfgs();
-constexpr int kFastSmallCfg0 = 15;   // conv_fast tiles 15.. are for small-batch plans (pc_conv_fast.hip)
+constexpr int kFastSmallCfg0 = 15, kFastSmallCfg1 = 19;   // conv_fast tiles 15..19: small-batch plans only
 int conv_fast_tile(int cfg, int* bc, int* bp);
 int conv_fast_valid(int cfg, int rowb);
 int conv_fast_valid_sx(int cfg, int rowb);
@@ -748,8 +748,8 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
       // (15-19: small-batch tiles, latency-bound K loops: a second round of them costs about
       // as much as the first, hence the high factor of the smallest)
       static const double cost[] = {1.0, 1.12, 1.12, 1.3, 1.3, 1.3, 1.15, 1.45, 1.3, 1.0, 0.9, 1.3, 1.6, 1.0, 1.0,
-                                    1.9, 1.6, 1.6, 3.0, 1.9};
-      static const int occ[] = {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 1, 1, 1, 2, 1, 1, 1, 1, 1};   // workgroups per CU
+                                    1.9, 1.6, 1.6, 3.0, 1.9, 1.3, 1.55};
+      static const int occ[] = {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 1, 1, 1, 2, 1, 1, 1, 1, 1, 1, 1};   // workgroups per CU
       static_assert(sizeof(cost) / sizeof(cost[0]) == sizeof(occ) / sizeof(occ[0]), "tile tables");
       int best = -1, best_rowb = rowb;
       double best_t = 0;
@@ -764,7 +764,7 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
         const int rb = (k == 10 || k == 14) ? 64 : (k >= 15 && k <= 17 && rows256) ? 256 : rowb;
         if (npad % bc || !conv_fast_valid(k, rb)) continue;
         if (force > 0 && k != force - 1) continue;
-        if (k >= kFastSmallCfg0 && (!small || no_small_tiles) && force <= 0) continue;   // small-batch tiles
+        if (k >= kFastSmallCfg0 && k <= kFastSmallCfg1 && (!small || no_small_tiles) && force <= 0) continue;   // small-batch tiles
         const long long t = (M + bp - 1) / bp * (npad / bc);
         const double rounds = (double)((t + 256 * occ[k] - 1) / (256 * occ[k]));
         const double est = rounds * bc * bp * occ[k] * cost[k];
@@ -777,7 +777,7 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
           int bc = 0, bp = 0;
           conv_fast_tile(k, &bc, &bp);
           if (npad % bc || (force > 0 && k != force - 1)) continue;
-          if (k >= kFastSmallCfg0 && (!small || no_small_tiles) && force <= 0) continue;
+          if (k >= kFastSmallCfg0 && k <= kFastSmallCfg1 && (!small || no_small_tiles) && force <= 0) continue;
           for (int rb : {rowb, 64}) {
             if (!conv_fast_valid_sx(k, rb)) continue;
             const long long t = (M + bp - 1) / bp * (npad / bc);

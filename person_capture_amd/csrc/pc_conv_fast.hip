@@ -388,6 +388,10 @@ static const FastCfg kFastCfgs[] = {
     {128, 64, 4},    // 17: 2x2 waves, 64x32 per wave, 6 stages
     {32, 64, 2},     // 18: 1x2 waves, 32x32 per wave, 8 stages (npad 32 / 96 / 160 / 224)
     {96, 64, 2},     // 19: 1x2 waves, 96x32 per wave, 7 stages (ROWB 64: 8)
+    // whole-width tiles for SCRFD's 224- and 96-channel layers (npad % 64 == 32: the other
+    // tiles split them into 32-channel slices that re-stage every pixel 7 or 3 times)
+    {224, 64, 2},    // 20: 1x2 waves, 224x32 per wave
+    {96, 128, 2},    // 21: 1x2 waves, 96x64 per wave
 };
 static const int kNumFastCfgs = sizeof(kFastCfgs) / sizeof(kFastCfgs[0]);
 
@@ -478,6 +482,8 @@ static hipError_t launch_fast_t(const ConvParams& p, int cfg, hipStream_t s) {
     case 17: return launch_fast_cfg<T, 128, 64, ROWB, 2, 2, 6>(p, s);
     case 18: return launch_fast_cfg<T, 32, 64, ROWB, 1, 2, 8>(p, s);
     case 19: return launch_fast_cfg<T, 96, 64, ROWB, 1, 2, ROWB == 128 ? 7 : 8>(p, s);
+    case 20: return launch_fast_cfg<T, 224, 64, ROWB, 1, 2, S3>(p, s);
+    case 21: return launch_fast_cfg<T, 96, 128, ROWB, 1, 2, S3>(p, s);
     default: return hipErrorInvalidValue;
   }
 }
