@@ -250,7 +250,9 @@ class FaceEmbedder(YoloFaceBranch):
         # images fill one round of the dominant 14x14x256 conv's 256x224 tiles over the CUs
         # (256 CUs x 224 px / 196 px per image / 2 images per face = 146); partial rounds
         # cost a whole round of that layer. 0 = full batches only. (Resident block chains
-        # change the round: see below.)
+        # change the round: see below. Beside the detection stream the quantum is 128 faces:
+        # their 256 rows fill 224 CUs and leave 32 to the SCRFD chunks - C3 r04: 1578 / 1596
+        # frames/s against 1561 / 1562 / 1567 with 146, profiles/r04sw_c3_pipeline_sweep.txt.)
         self._embed_quantum = int(os.getenv("PERSON_CAPTURE_AMD_EMBED_QUANTUM", "146"))
         # batched speculative fallback passes (TTA / edge pad / pre-scan rotations) per chunk
         self._fb_prefetch = os.getenv("PERSON_CAPTURE_AMD_FALLBACK_PREFETCH", "1") != "0"
@@ -266,6 +268,8 @@ class FaceEmbedder(YoloFaceBranch):
         # PERSON_CAPTURE_AMD_EMBED_STREAM=0: one stream.
         two = self.detector_backend == "scrfd" and os.getenv("PERSON_CAPTURE_AMD_EMBED_STREAM", "1") != "0"
         self._ectx = get_context(self._device_index, "embed") if two else self._ctx
+        if two and "PERSON_CAPTURE_AMD_EMBED_QUANTUM" not in os.environ:
+            self._embed_quantum = 128
         # host frames (extract / extract_batch without dev_frames) reach the device through the
         # native pinned staging ring on a copy stream of their own (pc_frame_stage)
         self._h2d = get_context(self._device_index, "h2d")
