@@ -27,6 +27,7 @@ namespace pc {
 hipError_t conv_launch(int f32, int rowb, int cfg, const ConvParams& p, hipStream_t s);
 hipError_t conv_halo_launch(int f32, int cfg, const ConvParams& p, hipStream_t s);
 hipError_t conv_fast_launch(int f32, int rowb, int cfg, const ConvParams& p, hipStream_t s);
+hipError_t conv_hx_launch(const ConvParams& p, hipStream_t s);
 int conv_fast_num_cfgs();
 constexpr int kFastSmallCfg0 = 15, kFastSmallCfg1 = 19;   // conv_fast tiles 15..19: small-batch plans only
 int conv_fast_tile(int cfg, int* bc, int* bp);
@@ -542,7 +543,7 @@ struct NetBuf { long long elems; int is_f32; void* d = nullptr; };
 struct NetTensor { int buf, H, W, C, cs, coff, is_f32, split; };
 struct NetOp { int w[32]; };
 // sx: fused f16x3 split tiles on conv_fast (pc_conv_fast.hip SX)
-struct ConvPlan { int rowb, cfg, splitk, halo = -1, fast = -1, t2d = -1, sx = 0; long long M_per_image; double flops_per_image; };
+struct ConvPlan { int rowb, cfg, splitk, halo = -1, fast = -1, t2d = -1, sx = 0, hx = 0; long long M_per_image; double flops_per_image; };
 // A stem (tiny Cin) runs as im2col + a 1x1 MFMA conv over 32-element K rows.
 struct StemPlan {
   int use_mfma = 0, npad = 0, cfg = 0, rowb = 0, cin_true = 0;
@@ -819,6 +820,20 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
         pl.sx = 0;
         pl.halo = -1;
       }
+    }
+  }
+  // f16x3 64 -> 64 channel 3x3 layers on the halo-staged split kernel (pc_conv_hx.hip), every
+  // plan alike (the choice does not depend on the batch). PC_CONV_HX=1 enables (evaluation).
+  pl.hx = 0;
+  if (getenv("PC_CONV_HX") && atoi(getenv("PC_CONV_HX")) == 1 && !n->f32 && nseg == 1 && pl.splitk == 1) {
+    const NetTensor& X = n->tens[w[3]];
+    if (X.split && X.C == 128 && X.cs == 128 && Y.split && Y.C == 128 && npad == 64 && w[4] == 3 && w[5] == 3 &&
+        w[6] == 1 && w[7] == 1 && X.H == Y.H && X.W == Y.W && w[15] == 9 * 192 &&
+        !(w[21] >= 0 && (w[22] == RES_UP2 || !n->tens[w[21]].split)) &&
+        (double)X.H * X.W * n->max_batch * X.cs * esz + kZeroTail < 4294967296.0) {
+      pl.hx = 1;
+      pl.fast = pl.halo = pl.t2d = -1;
+      pl.sx = 0;
     }
   }
   // small-batch plan: a long-K conv of a few images fills a fraction of the CUs (a 14x14x256
@@ -1357,7 +1372,9 @@ static int run_ops(pc_net* n, int N) {
       p.partial = n->partial;
       p.zero = c->zero;
       if (const char* e = getenv("PC_CONV_DBG")) p.dbg = atoi(e);
-      if (pl.t2d >= 0) {
+      if (pl.hx) {
+        HIPCHK(c, conv_hx_launch(p, s));
+      } else if (pl.t2d >= 0) {
         HIPCHK(c, conv_t2d_launch(p, pl.t2d, s));
       } else if (pl.fast >= 0) {
         HIPCHK(c, conv_fast_launch(n->f32, pl.rowb, pl.fast, p, s));
@@ -1507,7 +1524,7 @@ extern "C" int pc_net_profile_read(pc_net* n, double* out) {
 }
 
 // Per-record detail of the profiled runs: 6 doubles per record
-// [op index, kind, ms, flops, kernel (100+k fast tile k, 200+v t2d variant v, 300 resident chain, k halo tile k, -1 igemm), igemm cfg]; returns the count.
+// [op index, kind, ms, flops, kernel (100+k fast tile k, 200+v t2d variant v, 300 resident chain, 500 halo-staged f16x3, k halo tile k, -1 igemm), igemm cfg]; returns the count.
 extern "C" int pc_net_profile_ops(pc_net* n, double* out, int max_recs) {
   if (!n || !out) return -PC_ERR_ARG;
   HIPCHK(n->ctx, hipStreamSynchronize(n->ctx->stream));
@@ -1521,7 +1538,8 @@ extern "C" int pc_net_profile_ops(pc_net* n, double* out, int max_recs) {
     o[0] = r.op; o[1] = r.kind; o[2] = ms; o[3] = r.flops;
     const ConvPlan* pl = conv ? (r.small >= 0 ? &n->plans_cls[r.small][r.op] : &n->plans[r.op]) : nullptr;
     o[4] = r.code >= 0 ? r.code
-                       : conv ? (pl->t2d >= 0      ? 200 + pl->t2d
+                       : conv ? (pl->hx            ? 500
+                                 : pl->t2d >= 0    ? 200 + pl->t2d
                                  : pl->fast >= 0   ? 100 + pl->fast
                                                    : pl->halo)
                               : -1;
