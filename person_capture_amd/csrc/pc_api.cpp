@@ -822,10 +822,13 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
       }
     }
   }
-  // f16x3 64 -> 64 channel 3x3 layers on the halo-staged split kernel (pc_conv_hx.hip), every
-  // plan alike (the choice does not depend on the batch). PC_CONV_HX=1 enables (evaluation).
+  // f16x3 64 -> 64 channel 3x3 layers on the halo-staged split kernel (pc_conv_hx.hip: 160x160x64
+  // b64 524 vs 632 us on conv_fast's fused tile), every plan alike (the choice does not depend
+  // on the batch). Opt-in (PC_CONV_HX=1) until the full GPU suite has run with it on.
   pl.hx = 0;
-  if (getenv("PC_CONV_HX") && atoi(getenv("PC_CONV_HX")) == 1 && !n->f32 && nseg == 1 && pl.splitk == 1) {
+  if (getenv("PC_CONV_HX") && atoi(getenv("PC_CONV_HX")) == 1 && !getenv("PC_CONV_FAST") &&
+      !getenv("PC_CONV_CFG") && !getenv("PC_CONV_HALO") && !getenv("PC_CONV_T2D") && !getenv("PC_T2D_SPLIT64") &&
+      !getenv("PC_SPLIT_FUSED") && !n->f32 && nseg == 1 && pl.splitk == 1) {
     const NetTensor& X = n->tens[w[3]];
     if (X.split && X.C == 128 && X.cs == 128 && Y.split && Y.C == 128 && npad == 64 && w[4] == 3 && w[5] == 3 &&
         w[6] == 1 && w[7] == 1 && X.H == Y.H && X.W == Y.W && w[15] == 9 * 192 &&

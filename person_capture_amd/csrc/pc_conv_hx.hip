@@ -70,6 +70,7 @@ __global__ __launch_bounds__(256, 1) void conv_hx64(ConvParams p, int nby, int n
   issue_w(1, 1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // halo and the first two taps' weights
   __syncthreads();
+  if (p.dbg & 8) return;   // tuning only (PC_CONV_DBG): staging only
 
   f32x4 acc[TC][TP];
 #pragma unroll
@@ -91,7 +92,9 @@ __global__ __launch_bounds__(256, 1) void conv_hx64(ConvParams p, int nby, int n
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
-    if constexpr (tap + 2 < 9) issue_w(tap + 2, (tap + 2) % 3);
+    if constexpr (tap + 2 < 9) {
+      if (!(p.dbg & 1)) issue_w(tap + 2, (tap + 2) % 3);   // dbg 1: no weight stream (tuning only)
+    }
     const char* ws = wring + (tap % 3) * 16384;
     static_for<2>([&](auto kc) __attribute__((always_inline)) {
       constexpr int ks = decltype(kc)::value;
@@ -109,6 +112,7 @@ __global__ __launch_bounds__(256, 1) void conv_hx64(ConvParams p, int nby, int n
         bh[t] = *reinterpret_cast<const f16x8*>(halo + s * HX_SB + (((ks * 4 + g) ^ sw) << 4));
         bl[t] = *reinterpret_cast<const f16x8*>(halo + s * HX_SB + (((8 + ks * 4 + g) ^ sw) << 4));
       }
+      if (p.dbg & 2) return;   // tuning only: no MFMAs
 #pragma unroll
       for (int a = 0; a < TC; ++a)
 #pragma unroll
@@ -128,11 +132,85 @@ __global__ __launch_bounds__(256, 1) void conv_hx64(ConvParams p, int nby, int n
   });
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
+  if (p.dbg & 4) return;   // tuning only: no epilogue
+  // ---- epilogue through LDS: the per-fragment form (8-byte stores at a 256-byte pixel
+  // stride) took 60 % of the kernel (r04hxd). The accumulators go to a [pixel][channel] f32
+  // image over the halo; then every thread finishes 8 channels of a pixel - bias (per channel
+  // or border class), the activation select, split residual hi + lo - and stores the hi and
+  // lo halves as one 16-byte vector each (conv_epilogue_lds's arithmetic) ----
+  constexpr int RS = 68;                 // padded image row (floats)
+  __syncthreads();                       // every wave is done with the halo
+  float* im = reinterpret_cast<float*>(halo);
+#pragma unroll
+  for (int a = 0; a < TC; ++a)
+#pragma unroll
+    for (int t = 0; t < TP; ++t) {
+      const int pl = (wave * TP + t) * HX_TW + fr;   // block pixel (row-major 16x16)
+      *reinterpret_cast<f32x4*>(im + pl * RS + a * 16 + g * 4) = acc[a][t];
+    }
+  __syncthreads();
   const int OW = p.OW, OH = p.OH;
-  conv_epilogue_map<f16, TC, TP>(p, acc, 0, lane, 0, [&](int t) __attribute__((always_inline)) {
-    const int oy = oy0 + wave * TP + t, ox = ox0 + fr;
-    return oy < OH && ox < OW ? (n * OH + oy) * OW + ox : -1;
-  });
+  const int cg = threadIdx.x & 7, ch = cg * 8;
+  float bc[8], sl[8];
+  bool keep[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    bc[j] = p.bias_mode == BIAS_CHANNEL ? p.bias[ch + j] : 0.f;
+    sl[j] = p.act == ACT_PRELU ? p.slope[ch + j] : (p.act == ACT_RELU ? 0.f : 1.f);
+    keep[j] = ch + j < p.cout;
+  }
+  const bool smooth = p.act == ACT_SILU || p.act == ACT_GELU;
+  const bool has_res = p.res_mode != RES_NONE;
+  const bool pre_act = !p.act_after_res;
+  for (int pl = threadIdx.x >> 3; pl < HX_TH * HX_TW; pl += 32) {
+    const int oy = oy0 + (pl >> 4), ox = ox0 + (pl & 15);
+    if (oy >= OH || ox >= OW) continue;
+    const long long pix = ((long long)n * OH + oy) * OW + ox;
+    const f32x4 lo4 = *reinterpret_cast<const f32x4*>(im + pl * RS + ch);
+    const f32x4 hi4 = *reinterpret_cast<const f32x4*>(im + pl * RS + ch + 4);
+    float v[8] = {lo4[0] + bc[0], lo4[1] + bc[1], lo4[2] + bc[2], lo4[3] + bc[3],
+                  hi4[0] + bc[4], hi4[1] + bc[5], hi4[2] + bc[6], hi4[3] + bc[7]};
+    if (p.bias_mode == BIAS_BORDER9) {
+      const int rc = oy - 1 < 0 ? 0 : (oy + 1 >= H ? 2 : 1);
+      const int cc = ox - 1 < 0 ? 0 : (ox + 1 >= W ? 2 : 1);
+      const float* bp = p.bias + (rc * 3 + cc) * p.npad + ch;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += bp[j];
+    }
+    float r[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (has_res) {
+      const f16* rp = reinterpret_cast<const f16*>(p.res) + pix * p.rcs + ch;
+      const f16x8 rh = *reinterpret_cast<const f16x8*>(rp);
+      const f16x8 rl = *reinterpret_cast<const f16x8*>(rp + p.rsplit);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] = (float)rh[j] + (float)rl[j];
+    }
+    if (has_res && !pre_act) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += r[j];
+    }
+    if (smooth) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j], p.act, 0.f);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = v[j] > 0.f ? v[j] : v[j] * sl[j];
+    }
+    if (has_res && pre_act) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += r[j];
+    }
+    f16x8 yh, yl;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float x = keep[j] ? v[j] : 0.f;
+      yh[j] = (f16)x;
+      yl[j] = (f16)(x - (float)yh[j]);
+    }
+    f16* yp = reinterpret_cast<f16*>(p.y) + pix * p.ycs + ch;
+    *reinterpret_cast<f16x8*>(yp) = yh;
+    *reinterpret_cast<f16x8*>(yp + p.ysplit) = yl;
+  }
 }
 
 // can a conv run here: split 64-channel input (X.C 128 = [hi | lo]), 64 output channels
@@ -141,7 +219,8 @@ int conv_hx_ok(const ConvParams& p) {
   const ConvSeg& S = p.seg[0];
   return p.nseg == 1 && S.C == 128 && S.KH == 3 && S.KW == 3 && S.stride == 1 && S.pad == 1 &&
          S.H == p.OH && S.W == p.OW && p.npad == 64 && p.ysplit == 64 && p.splitk == 1 && !p.out_f32 &&
-         p.ktot == 9 * 192 && p.res_mode != RES_UP2 && (p.res_mode == RES_NONE || p.rsplit == 64);
+         p.ktot == 9 * 192 && p.res_mode != RES_UP2 && (p.res_mode == RES_NONE || (p.rsplit == 64 && p.rcs % 8 == 0)) &&
+         p.ycs % 8 == 0 && p.cwrite == 64;
 }
 
 hipError_t conv_hx_launch(const ConvParams& p, hipStream_t s) {

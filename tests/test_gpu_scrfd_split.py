@@ -64,7 +64,7 @@ KERNEL_MODES = {
     "t2d64": {"PC_T2D_SPLIT64": "1"},                          # + the opt-in 64-channel split t2d
     "fast": {"PC_CONV_T2D": "0"},                              # conv_fast everywhere it runs
     "igemm": {"PC_CONV_T2D": "0", "PC_CONV_FAST": "0"},        # the generic kernel
-    "hx": {"PC_CONV_HX": "1"},                                 # + the halo-staged 64-channel kernel
+    "hx": {"PC_CONV_HX": "1"},                                 # + the halo-staged 64-channel kernel (opt-in)
 }
 
 
