@@ -824,9 +824,9 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
   }
   // f16x3 64 -> 64 channel 3x3 layers on the halo-staged split kernel (pc_conv_hx.hip: 160x160x64
   // b64 524 vs 632 us on conv_fast's fused tile), every plan alike (the choice does not depend
-  // on the batch). Opt-in (PC_CONV_HX=1) until the full GPU suite has run with it on.
+  // on the batch). PC_CONV_HX=0 disables; the tuning overrides of the other kernels too.
   pl.hx = 0;
-  if (getenv("PC_CONV_HX") && atoi(getenv("PC_CONV_HX")) == 1 && !getenv("PC_CONV_FAST") &&
+  if (!(getenv("PC_CONV_HX") && atoi(getenv("PC_CONV_HX")) == 0) && !getenv("PC_CONV_FAST") &&
       !getenv("PC_CONV_CFG") && !getenv("PC_CONV_HALO") && !getenv("PC_CONV_T2D") && !getenv("PC_T2D_SPLIT64") &&
       !getenv("PC_SPLIT_FUSED") && !n->f32 && nseg == 1 && pl.splitk == 1) {
     const NetTensor& X = n->tens[w[3]];

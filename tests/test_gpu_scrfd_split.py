@@ -59,12 +59,12 @@ def _heads_vs_oracle(ctx, p, variant, D, frames, env, monkeypatch):
 
 
 KERNEL_MODES = {
-    "default": {},                                             # split t2d (32-ch trunk) + conv_fast fused tiles
+    "default": {},                                             # split t2d (32-ch trunk), halo-staged 64-ch, fused tiles
     "virtual": {"PC_SPLIT_FUSED": "0"},                        # conv_fast walking the virtual [hi, lo, hi] K
     "t2d64": {"PC_T2D_SPLIT64": "1"},                          # + the opt-in 64-channel split t2d
     "fast": {"PC_CONV_T2D": "0"},                              # conv_fast everywhere it runs
     "igemm": {"PC_CONV_T2D": "0", "PC_CONV_FAST": "0"},        # the generic kernel
-    "hx": {"PC_CONV_HX": "1"},                                 # + the halo-staged 64-channel kernel (opt-in)
+    "nohx": {"PC_CONV_HX": "0"},                               # 64-ch layers on conv_fast's fused tiles
 }
 
 
