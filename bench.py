@@ -146,9 +146,10 @@ def compare_faces(res_a, res_b, band: float = 1e-3) -> dict:
     `band` from the threshold (a flip inside the band is the f32-class noise of any
     non-bitwise-identical path: the device f32 mode flips there against the CPU oracle too).
     Frames with res_b None (the oracle's fallback frames) are skipped."""
-    n = count_mis = box_mis = acc32 = acc45 = out32 = out45 = 0
-    worst = 0.0
+    n = count_mis = box_mis = acc32 = acc45 = out32 = out45 = box_int = 0
+    worst = worst_same = 0.0
     near = []
+    margins = []
     for a_f, b_f in zip(res_a, res_b):
         if b_f is None:
             continue
@@ -159,9 +160,21 @@ def compare_faces(res_a, res_b, band: float = 1e-3) -> dict:
             if a is None:
                 box_mis += 1
                 continue
-            box_mis += int(not np.array_equal(a["bbox"], b["bbox"]))
+            same_box = np.array_equal(a["bbox"], b["bbox"])
+            box_mis += int(not same_box)
+            if not same_box and "bbox_f" in b:
+                # a box that differs by one pixel in coordinates whose reference float value lies
+                # next to an integer: the int() of _accumulate (face_embedder.py:2214-2239) on either
+                # side of it; margin = the reference coordinate's distance to that integer
+                d = np.abs(a["bbox"].astype(np.int64) - b["bbox"].astype(np.int64))
+                bf = np.asarray(b["bbox_f"], np.float64)
+                if d.max() == 1:
+                    box_int += 1
+                    margins.append(float(np.abs(bf[d == 1] - np.rint(bf[d == 1])).max()))
             fa, fb = float(a["fd"]), float(b["fd"])
             worst = max(worst, abs(fa - fb))
+            if same_box:
+                worst_same = max(worst_same, abs(fa - fb))
             for thr, key in ((0.32, 0), (0.45, 1)):
                 if (fa <= thr) != (fb <= thr):
                     far = abs(fb - thr) > band
@@ -172,9 +185,14 @@ def compare_faces(res_a, res_b, band: float = 1e-3) -> dict:
                     else:
                         acc45 += 1
                         out45 += far
-    return {"faces": n, "face_count_mismatch": count_mis, "box_mismatch": box_mis, "accept_mismatch_0.32": acc32,
-            "accept_mismatch_0.45": acc45, f"accept_mismatch_outside_{band:g}_band": out32 + out45,
-            "max_fd_diff": round(worst, 6), "flipped_ref_distance_to_0.32": sorted(near)}
+    out = {"faces": n, "face_count_mismatch": count_mis, "box_mismatch": box_mis, "accept_mismatch_0.32": acc32,
+           "accept_mismatch_0.45": acc45, f"accept_mismatch_outside_{band:g}_band": out32 + out45,
+           "max_fd_diff": round(worst, 6), "max_fd_diff_same_box": round(worst_same, 6),
+           "flipped_ref_distance_to_0.32": sorted(near)}
+    if margins or box_int:
+        out["box_mismatch_int_boundary"] = box_int
+        out["box_mismatch_int_margin_px"] = round(max(margins), 6)
+    return out
 
 
 def hbm_kernels(fe, devs, H: int, W: int, reps: int = 20, kinds=("letterbox", "warp", "maxpool")) -> dict:
@@ -271,6 +289,9 @@ def hbm_kernels(fe, devs, H: int, W: int, reps: int = 20, kinds=("letterbox", "w
     return out
 
 
+_F32_REF = {}
+
+
 def f16_parity(fe16, devs, bank_h, conf: float = 0.5) -> dict:
     """Outside the timed region: the same frames through an f32 FaceEmbedder (the parity mode,
     itself checked against the fp32 CPU oracle in tests/test_gpu_bench_config.py) against the
@@ -293,13 +314,18 @@ def f16_parity(fe16, devs, bank_h, conf: float = 0.5) -> dict:
         return r
 
     res16 = run(fe16, DeviceBank(fe16._ctx, bank_h))
-    old = {k: os.environ.get(k) for k in ("PERSON_CAPTURE_AMD_PRECISION", "PERSON_CAPTURE_AMD_DET_PRECISION")}
+    old = {k: os.environ.get(k) for k in ("PERSON_CAPTURE_AMD_PRECISION", "PERSON_CAPTURE_AMD_DET_PRECISION",
+                                          "PERSON_CAPTURE_AMD_ARC_PRECISION")}
     for k in old:
         os.environ[k] = "f32"
     try:
-        fe32 = FaceEmbedder(ctx=f"cuda:{_device(int(os.environ.get('LOCAL_RANK', '0')))}",
-                            yolo_model="scrfd_10g_bnkps", conf=conf)
-        res32 = run(fe32, DeviceBank(fe32._ctx, bank_h))
+        # the f32 reference run of these frames / bank / threshold is made once per bench process
+        key = (devs[0].ptr, len(devs), conf, float(bank_h.sum()))
+        if key not in _F32_REF:
+            fe32 = FaceEmbedder(ctx=f"cuda:{_device(int(os.environ.get('LOCAL_RANK', '0')))}",
+                                yolo_model="scrfd_10g_bnkps", conf=conf)
+            _F32_REF[key] = (fe32, run(fe32, DeviceBank(fe32._ctx, bank_h)))
+        fe32, res32 = _F32_REF[key]
         chips16 = [f["chip"] for r in res16 for f in r]
         e32_on16 = fe32._arc.embed(np.stack(chips16), flip=True) if chips16 else np.zeros((0, 512), np.float32)
     finally:
@@ -349,22 +375,30 @@ def f16_parity(fe16, devs, bank_h, conf: float = 0.5) -> dict:
                 "kps_abs_diff_px": {"median": round(float(np.median(kps_d)), 5), "max": round(float(kps_d.max()), 5)},
                 "arcface_only_max_fd_diff": round(worst_arc, 6),
                 "arcface_only_accept_flips_0.32": arc_flip,
-                "note": "arcface_only: f16 fd vs the f32 ArcFace on the f16 pass's own chips; the rest of the "
-                        "difference enters through the SCRFD f16 landmarks (a different aligned chip; the "
+                "note": "arcface_only: this mode's fd vs the f32 ArcFace on this mode's own chips; the rest of the "
+                        "difference enters through the detector's landmarks (a different aligned chip; the "
                         "bench frames are u8 noise, so a sub-pixel landmark shift resamples the chip)"}}
 
 
-def smooth_parity(fe16, frames: np.ndarray, bank_rows: int) -> dict:
-    """The f16-vs-f32 comparison on the bench frames low-pass filtered (Gaussian, sigma 1.5 px):
-    u8 noise frames resample to unrelated chips under a sub-pixel landmark shift, smooth
-    frames (like camera images) do not. Same planted-bank construction, own bank."""
+def smooth_frames(frames: np.ndarray) -> np.ndarray:
+    """The bench frames low-pass filtered (Gaussian, sigma 1.5 px), contrast restored x2.5 about
+    the noise mean 127.5 (camera-like images: a sub-pixel landmark shift no longer resamples the
+    chip into unrelated pixels)."""
     from scipy.ndimage import gaussian_filter
-    from person_capture_amd.face_embedder import _DevImage
-    from person_capture_amd.match import DeviceBank
     sm = np.empty_like(frames)
-    for i, f in enumerate(frames):   # blur, then restore contrast about the noise mean 127.5
+    for i, f in enumerate(frames):
         g = gaussian_filter(f.astype(np.float32), sigma=(1.5, 1.5, 0))
         sm[i] = np.clip(np.rint(128.0 + 2.5 * (g - 127.5)), 0, 255).astype(np.uint8)
+    return sm
+
+
+def smooth_parity(fe16, frames: np.ndarray, bank_rows: int) -> dict:
+    """The timed-mode-vs-f32 comparison on smooth_frames(frames): u8 noise frames resample to
+    unrelated chips under a sub-pixel landmark shift, smooth frames (like camera images) do not.
+    Same planted-bank construction, own bank."""
+    from person_capture_amd.face_embedder import _DevImage
+    from person_capture_amd.match import DeviceBank
+    sm = smooth_frames(frames)
     ctx = fe16._ctx
     d = ctx.alloc(sm.nbytes)
     ctx.upload(sm, d)
@@ -394,6 +428,10 @@ def _kernel_of(code: float, cfg: float) -> str:
     c = int(code)
     if c == 300:
         return "conv_chain (resident IResNet block chain, pc_conv_chain.hip)"
+    if c >= 600:
+        return f"conv_fast C8 tile cfg {c - 600} (f16c8, pc_conv_fast.hip kFastCfgs)"
+    if c == 500:
+        return "conv_hx64 (halo-staged f16x3, pc_conv_hx.hip)"
     if c >= 200:
         return f"conv_t2d (2-D block kernel, variant {c - 200})"
     if c >= 100:
@@ -462,11 +500,15 @@ def main():
     ap.add_argument("--bank", type=int, default=32)
     ap.add_argument("--cpu-sample", type=int, default=48)
     ap.add_argument("--cpu-sample-1t", type=int, default=4)
-    ap.add_argument("--c5-samples", type=int, default=256,
-                    help="C5: samples of the one clip whose positions are sharded over the ranks (strong scaling)")
+    ap.add_argument("--c5-samples", type=int, default=1024,
+                    help="C5: samples of the one clip whose positions are sharded over the ranks (strong scaling; "
+                         "1024 = 128 per rank at 8 GPUs, two full speculative chunks of the default batch 64)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-parity", action="store_true", help="skip the f16-vs-f32 decision parity pass")
-    ap.add_argument("--precision", default="f16", choices=["f16", "f32"])
+    ap.add_argument("--precision", default="f16", choices=["f16", "f32", "f16x3", "f16c8"],
+                    help="c3/c4/c5: f16 = the timed mode (SCRFD and ArcFace f16x3 by default, DESIGN.md §3.6-3.7), "
+                         "f32 = the f32 parity mode; c2: the ArcFace program's precision (f16 = BASELINE C2's fp16, "
+                         "f16x3 = the split program C3 embeds with)")
     ap.add_argument("--frames", default="resident", choices=["resident", "host", "per-frame"],
                     help="C3 frame source: resident in HBM (the headline), host arrays through extract_batch "
                          "(H2D inside the timed region), or one extract() per host frame")
@@ -505,7 +547,7 @@ def main():
     os.environ.setdefault("PERSON_CAPTURE_AMD_PRECISION", args.precision)
     os.environ.setdefault("PERSON_CAPTURE_AMD_DET_BATCH", str(args.batch))
     os.environ.setdefault("PERSON_CAPTURE_AMD_ARC_BATCH", "512")
-    from person_capture_amd._lib import PC_PREC_F16X3, PC_PREC_F32
+    from person_capture_amd._lib import PC_PREC_F16C8, PC_PREC_F16X3, PC_PREC_F32
     from person_capture_amd.face_embedder import FaceEmbedder, _DevImage
     from person_capture_amd.match import DeviceBank, fd_min
 
@@ -612,6 +654,8 @@ def main():
                    "faces_per_frame": round(nfaces / args.batch, 3), "accepted_faces_per_step": accept,
                    "accepted_faces_per_step_cli_0.32": accept_cli, "bank_planted_rows": n_plant,
                    "detector_dtype": {PC_PREC_F32: "f32", PC_PREC_F16X3: "f16x3"}.get(fe.det_precision, "f16"),
+                   "arcface_dtype": {PC_PREC_F32: "f32", PC_PREC_F16X3: "f16x3", PC_PREC_F16C8: "f16c8"}.get(
+                       fe.arc_precision, "f16"),
                    "parallelism": f"frame-shard x{world} (no collective)"},
         "roofline": {"bound": "mfma", "achieved": dom["achieved_tflops"], "peak": peak, "unit": "TFLOP/s",
                      "frac": round(dom["achieved_tflops"] / peak, 4),
@@ -640,21 +684,24 @@ def main():
             fe.detector_backend == "scrfd":
         out["parity"] = f16_parity(fe, devs, bank_h)
         res32, res16 = out["parity"].pop("_res32"), out["parity"].pop("_res16")
-        out["parity"]["timed_mode"] = "SCRFD " + out["config"]["detector_dtype"] + " + ArcFace f16"
+        out["parity"]["timed_mode"] = "SCRFD " + out["config"]["detector_dtype"] + " + ArcFace " + \
+            out["config"]["arcface_dtype"]
 
-        # the same pipeline with the detector in another precision: its throughput and decisions
-        # (f32: the f32 SCRFD kernels, chips identical to the f32 mode's; f16: plain f16 SCRFD,
-        # the round-3 headline, whose sub-pixel landmark shifts flip decisions on noise frames)
-        def alt_mode(dp):
-            old_dp = os.environ.get("PERSON_CAPTURE_AMD_DET_PRECISION")
-            os.environ["PERSON_CAPTURE_AMD_DET_PRECISION"] = dp
+        # the same pipeline with the nets in other precisions: their throughput and decisions
+        # (detector f32: the f32 SCRFD kernels, chips identical to the f32 mode's; ArcFace f16: the
+        # round-4 timed mode, the reference's TensorRT precision, fd within ~2e-4 only; both f16: the
+        # round-3 headline, whose sub-pixel landmark shifts flip decisions on noise frames)
+        def alt_mode(env):
+            olds = {k: os.environ.get(k) for k in env}
+            os.environ.update(env)
             try:
                 fe_d = FaceEmbedder(ctx=f"cuda:{local}", yolo_model="scrfd_10g_bnkps", conf=0.5)
             finally:
-                if old_dp is None:
-                    os.environ.pop("PERSON_CAPTURE_AMD_DET_PRECISION", None)
-                else:
-                    os.environ["PERSON_CAPTURE_AMD_DET_PRECISION"] = old_dp
+                for k, v in olds.items():
+                    if v is None:
+                        os.environ.pop(k, None)
+                    else:
+                        os.environ[k] = v
             run_d = lambda: fe_d.extract_batch([None] * args.batch, dev_frames=devs, bank=bank)
             run_d()
             fe_d._ctx.sync()
@@ -671,11 +718,15 @@ def main():
                                           "accept_mismatch_0.32_outside_0.001_band")},
                     "chips_identical": pd["attribution"]["chips_identical"]}
 
-        out["parity"]["detector_f32_mode"] = dict(alt_mode("f32"), note=(
-            "SCRFD f32 + ArcFace f16 (PERSON_CAPTURE_AMD_DET_PRECISION=f32): the f32 mode's SCRFD kernels, identical "
-            "chips; the remaining differences are the f16 ArcFace's"))
-        out["parity"]["detector_f16_mode"] = dict(alt_mode("f16"), note=(
-            "plain f16 SCRFD + ArcFace f16 (PERSON_CAPTURE_AMD_DET_PRECISION=f16, the round-3 headline)"))
+        out["parity"]["detector_f32_mode"] = dict(alt_mode({"PERSON_CAPTURE_AMD_DET_PRECISION": "f32"}), note=(
+            "SCRFD f32 + the timed mode's ArcFace (PERSON_CAPTURE_AMD_DET_PRECISION=f32): the f32 mode's SCRFD "
+            "kernels, identical chips"))
+        out["parity"]["arcface_f16_mode"] = dict(alt_mode({"PERSON_CAPTURE_AMD_ARC_PRECISION": "f16"}), note=(
+            "the timed mode's SCRFD + plain f16 ArcFace (PERSON_CAPTURE_AMD_ARC_PRECISION=f16, round 4's timed mode: "
+            "the reference's TensorRT fp16 precision; its fd moves ~2e-4 on identical chips)"))
+        out["parity"]["trt_f16_mode"] = dict(alt_mode({"PERSON_CAPTURE_AMD_DET_PRECISION": "f16",
+                                                       "PERSON_CAPTURE_AMD_ARC_PRECISION": "f16"}), note=(
+            "plain f16 SCRFD + plain f16 ArcFace (round 3's headline): sub-pixel landmark shifts resample noise chips"))
         out["parity"]["timed_mode_speedup_vs_detector_f32_mode"] = round(
             value / out["parity"]["detector_f32_mode"]["frames_per_s"], 3)
         out["parity"]["smooth_frames"] = smooth_parity(fe, frames, args.bank)
@@ -723,12 +774,12 @@ def main_c2(args):
     world, rank, local = _dist_init()
     local = _device(local)
     from person_capture_amd import models
-    from person_capture_amd._lib import PC_PREC_F16, PC_PREC_F32
+    from person_capture_amd._lib import PC_PREC_F16, PC_PREC_F16C8, PC_PREC_F16X3, PC_PREC_F32
     from person_capture_amd.engines import ArcFaceEngine
     from person_capture_amd.runtime import GpuContext
     B = 256
     ctx = GpuContext(local)
-    prec = PC_PREC_F16 if args.precision == "f16" else PC_PREC_F32
+    prec = {"f16": PC_PREC_F16, "f16x3": PC_PREC_F16X3, "f16c8": PC_PREC_F16C8}.get(args.precision, PC_PREC_F32)
     arc_params = models.synth_iresnet(100, seed=0)
     eng = ArcFaceEngine(ctx, arc_params, 100, precision=prec, max_batch=2 * B)
     chips = np.random.default_rng(20260505 + rank).integers(0, 256, (B, 112, 112, 3), dtype=np.uint8)
@@ -746,7 +797,11 @@ def main_c2(args):
     dom = dominant_conv([eng.net], ("arcface",))
     recs = eng.net.profile_ops()
     eng.net.profile(False)
-    peak = PEAK_F16_TFLOPS if args.precision == "f16" else PEAK_F32_TFLOPS
+    # f16x3 issues 3 f16 MFMAs per algorithmic product: its roofline is a third of dense f16
+    # (f16c8: 2 f16 MFMAs + 1 block-scaled e4m3 MFMA per 64-channel K tile where f16 takes 2; its
+    # roofline is the f16 peak x 2 / 3 at the e4m3 instruction's measured equal issue time)
+    peak = {"f16": PEAK_F16_TFLOPS, "f16x3": PEAK_F16_TFLOPS / 3,
+            "f16c8": PEAK_F16_TFLOPS * 2 / 3}.get(args.precision, PEAK_F32_TFLOPS)
     fl = eng.flops_per_forward * B
     ms = elapsed / args.steps * 1e3
     net_tf = fl / (ms * 1e-3) / 1e12
@@ -950,8 +1005,12 @@ def main_other(args):
                 stats["faces"] = sum(x.n_faces for x in recs)
                 stats["extracted_samples"] = sum(1 for x in recs if x.extracted)
                 stats["spans"] = len(spans)
-                stats["merge"] = {"reused": ms.reused, "reextracted_on_rank0": ms.reextracted,
-                                  "skipped": ms.skipped, "speculated_per_rank": ms.per_rank_spec}
+                # the serial part of a sharded clip: rank 0's replay (host logic over every sample) and
+                # its batched chunks for speculation misses
+                stats["merge"] = {"reused": ms.reused, "misses": ms.misses, "rank0_chunks": ms.rechunks,
+                                  "reextracted_on_rank0": ms.reextracted, "served_by_rank0_chunks": ms.from_rechunks,
+                                  "skipped": ms.skipped, "speculated_per_rank": ms.per_rank_spec,
+                                  "merge_serial_ms": round(ms.merge_s * 1e3, 2)}
             return r
         wl = (f"C5: pre-scan of one clip of {S} samples at stride {stride} (4K frames -> INTER_AREA 416 wide, "
               f"fast pre-scan SCRFD-10G, ArcFace-R100 1 forward / 2 while a span is active, fd vs a {bank_n}-embedding "

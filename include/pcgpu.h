@@ -66,6 +66,9 @@ extern "C" {
  * exact f32 (parity runs against the CPU oracle). */
 #define PC_PREC_F16 0
 #define PC_PREC_F32 1
+/* pc_arcface_prep only: the centred chip x - 127.5 in f16 (exact), the input of the f16x3 IResNet
+ * program (its stem weights carry the 1/127.5; models.compile_iresnet(split=True)) */
+#define PC_PREC_F16X3 2
 
 typedef struct pc_ctx pc_ctx;
 typedef struct pc_net pc_net;
@@ -211,9 +214,15 @@ int pc_net_set_graph_max_batch(pc_net* net, int32_t max_batch);
 /* HIP-event timing of every op of every later (non-graph) run; enable resets the counters.
  * read: [0] conv ms, [1] conv launches, [2] conv FLOPs (algorithmic), [3] other ms, [4] other launches */
 int pc_net_profile(pc_net* net, int enable);
+/* f16c8 nets: run the program once on N images at d_in and set every f16c8 tensor's
+ * e4m3 scale exponents from its largest magnitude, 2^headroom_log2 below the format's range. Clears the
+ * net's captured graphs. h_absmax (optional, [n_tensor] floats): the measured max |x| per tensor (0 where
+ * not measured). Replaces no reference interface (the reference's TensorRT engines carry no such
+ * scales: f16c8 is this build's f32-class arithmetic on the f16 / fp8 MFMA path). */
+int pc_net_calibrate(pc_net* net, const void* d_in, int N, int headroom_log2, float* h_absmax);
 int pc_net_profile_read(pc_net* net, double* h_out5);
 /* Per-launch detail of the profiled runs, 6 doubles per record: op index, op kind, ms, FLOPs,
-   kernel (100+k: static-schedule tile k, k >= 0: halo tile k, -1: generic implicit-GEMM), implicit-GEMM tile. Returns the record count (<0: -status). */
+   kernel (100+k: static-schedule tile k, 600+k: its f16c8 form, 200+v: t2d variant v, 300: resident chain, 500: halo-staged f16x3, k >= 0: halo tile k, -1: generic implicit-GEMM), implicit-GEMM tile. Returns the record count (<0: -status). */
 int pc_net_profile_ops(pc_net* net, double* h_out, int max_recs);
 
 /* ---- image kernels ---- */
@@ -221,6 +230,8 @@ int pc_letterbox(pc_ctx* ctx, int precision, const pc_letterbox_desc* h_descs, i
 int pc_warp_affine(pc_ctx* ctx, const pc_warp_desc* h_descs, int n);
 int pc_resize_linear(pc_ctx* ctx, const pc_resize_desc* h_descs, int n);
 int pc_face_quality(pc_ctx* ctx, const uint8_t* d_chips, int n, int side, double* d_out);
+/* precision PC_PREC_F16 / PC_PREC_F32: x/127.5 - 1 in that dtype (face_embedder.py:1281-1288);
+ * PC_PREC_F16X3: x - 127.5 in f16 (the f16x3 program's centred input) */
 int pc_arcface_prep(pc_ctx* ctx, int precision, const uint8_t* d_chips, int n, int side, int flip, void* d_out);
 int pc_rotate_pad(pc_ctx* ctx, const uint8_t* d_src, int H, int W, int row_stride, int deg, int pad, uint8_t* d_dst);
 /* cv2.resize INTER_AREA at an exact integer ratio isx x isy (OpenCV resizeAreaFast). */
@@ -242,7 +253,8 @@ int pc_scrfd_detect(pc_net* net, const pc_letterbox_desc* h_descs, int n, int D,
 
 /* ---- embedding / match ---- */
 int pc_embed_finalize(pc_ctx* ctx, const float* d_e, int ld, int n, int dim, int flip, float* d_out);
-/* chips: [n][side][side][3] BGR u8 (side == net input side). d_feat: [n][dim] unit f32 */
+/* chips: [n][side][side][3] BGR u8 (side == net input side). d_feat: [n][dim] unit f32. A net whose
+ * program flags a centred input (f16x3 IResNet) gets the PC_PREC_F16X3 preprocessing. */
 int pc_arcface_embed(pc_net* net, const uint8_t* d_chips, int n, int flip, float* d_feat);
 int pc_bank_match(pc_ctx* ctx, const float* d_q, int n, const float* d_bank, int b, int dim, float* d_fd,
                   int32_t* d_idx);

@@ -158,7 +158,7 @@ def extract_frame(frame: np.ndarray, scrfd_params, variant: str, arc_params, dep
             continue
         pts = np.asarray([[float(px) - xa1, float(py) - ya1] for (px, py) in np.asarray(kp, np.float32).reshape(-1, 2)],
                          np.float32)[:5]
-        dets.append(((xa1, ya1, xa2, ya2), pts, float(bb[4])))
+        dets.append(((xa1, ya1, xa2, ya2), pts, float(bb[4]), np.asarray(bb[:4], np.float64)))
     dets = [d for d in dets if d[0][2] - d[0][0] >= 8 and d[0][3] - d[0][1] >= 8]
     if not dets:
         return NEEDS_FALLBACK
@@ -167,14 +167,15 @@ def extract_frame(frame: np.ndarray, scrfd_params, variant: str, arc_params, dep
     for d in dets:
         if all(ra.iou(d[0], k[0]) < 0.45 for k in kept):
             kept.append(d)
-    chips, boxes, kps5 = [], [], []
-    for (x1, y1, x2, y2), pts, _ in kept:
+    chips, boxes, kps5, boxes_f = [], [], [], []
+    for (x1, y1, x2, y2), pts, _, bf in kept:
         face = frame[y1:y2, x1:x2]
         canon = ra.canon_5pts(pts)
         if canon is None:
             raise NotImplementedError("eye-roll fallback")
         chips.append(align_chip(face, canon))
         boxes.append((x1, y1, x2, y2))
+        boxes_f.append(bf)
         kps5.append(pts)
     chips = np.stack(chips)
     q = [cv_ops.face_quality(c) for c in chips]
@@ -183,8 +184,9 @@ def extract_frame(frame: np.ndarray, scrfd_params, variant: str, arc_params, dep
     feats = ra.arcface_postprocess(e, ef)
     out = []
     for i, b in enumerate(boxes):
+        # bbox_f: the detector's float box before the int() of _accumulate (face_embedder.py:2214-2239)
         f = {"bbox": np.array(b, np.int32), "feat": feats[i], "quality": float(q[i]), "chip": chips[i],
-             "kps5": kps5[i]}
+             "kps5": kps5[i], "bbox_f": boxes_f[i]}
         if bank is not None:
             f["fd"] = ra.fd_min(feats[i], bank)
         out.append(f)

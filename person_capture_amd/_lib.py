@@ -21,11 +21,14 @@ PC_PREC_F32 = 1
 # host-side mode (not a pc_net_create precision): an f16 net running the f16x3 split program
 # (models.compile_scrfd(split=True)) - f32-class detections on f16 MFMA
 PC_PREC_F16X3 = 2
+# host-side mode: an f16 net running the f16c8 program (models.compile_iresnet(c8=True), DESIGN.md
+# §3.7) - f16 hi with e4m3 lo / hi bytes, x_hi*W_hi on f16 MFMA + the corrections on block-scaled e4m3
+PC_PREC_F16C8 = 3
 
 
 def net_precision(mode: int) -> int:
     """The pc_net_create precision of a host precision mode."""
-    return PC_PREC_F16 if mode == PC_PREC_F16X3 else mode
+    return PC_PREC_F16 if mode in (PC_PREC_F16X3, PC_PREC_F16C8) else mode
 
 _lib = None
 
@@ -113,6 +116,7 @@ SIGNATURES = {
     "pc_net_set_graph": ([_P, _I], _I),
     "pc_net_set_graph_max_batch": ([_P, C.c_int32], _I),
     "pc_net_profile": ([_P, _I], _I),
+    "pc_net_calibrate": ([_P, _P, _I, _I, C.POINTER(C.c_float)], _I),
     "pc_net_profile_read": ([_P, C.POINTER(C.c_double)], _I),
     "pc_net_profile_ops": ([_P, C.POINTER(C.c_double), _I], _I),
     "pc_letterbox": ([_P, _I, C.POINTER(LetterboxDesc), _I, _I, _P], _I),

@@ -16,6 +16,8 @@
 #include <algorithm>
 #include <thread>
 #include <mutex>
+#include <memory>
+#include <cmath>
 #include <atomic>
 #include <condition_variable>
 #include <functional>
@@ -33,6 +35,7 @@ constexpr int kFastSmallCfg0 = 15, kFastSmallCfg1 = 19;   // conv_fast tiles 15.
 int conv_fast_tile(int cfg, int* bc, int* bp);
 int conv_fast_valid(int cfg, int rowb);
 int conv_fast_valid_sx(int cfg, int rowb);
+int conv_fast_valid_c8(int cfg, int rowb);
 int conv_halo_num_cfgs();
 int conv_halo_tile(int cfg, int* bc, int* bp);
 int conv_halo_fits(int cfg, int KH, int KW, int W);
@@ -48,6 +51,7 @@ int stem_fused_ok(int f32, int cin, int cin_true, int KH, int KW, int npad, int 
 hipError_t stem_fused_launch(const StemParams& p, const void* wpk, const float* bias, const float* slope, int npad,
                              int cwrite, hipStream_t s);
 hipError_t splitk_finish_launch(int f32, const ConvParams& p, hipStream_t s);
+hipError_t absmax_f16_launch(const void* x, long long npix, int C, int cs, unsigned* out, hipStream_t s);
 hipError_t splitk_reduce_launch(int f32, const float* part, int splitk, int M, int npad, int cout, const float* bias,
                                 const float* slope, int act, void* y, int ycs, int out_f32, hipStream_t s);
 hipError_t stem_launch(int f32, const StemParams& p, hipStream_t s);
@@ -61,7 +65,7 @@ hipError_t resize_linear_launch(const ResizeDesc* d_descs, int N, int max_pixels
 hipError_t letterbox_launch(int f32, const LetterboxDesc* d_descs, int N, int D, void* out, hipStream_t s);
 hipError_t warp_launch(const WarpDesc* d_descs, int N, int max_pixels, hipStream_t s);
 hipError_t quality_launch(const uint8_t* chips, int N, int side, double* out, hipStream_t s);
-hipError_t arcprep_launch(int f32, const uint8_t* chips, int N, int side, int flip, void* out, hipStream_t s);
+hipError_t arcprep_launch(int mode, const uint8_t* chips, int N, int side, int flip, void* out, hipStream_t s);
 hipError_t rotate_pad_launch(const uint8_t* src, int H, int W, int row_stride, int deg, int pad, uint8_t* dst, int OH,
                              int OW, hipStream_t s);
 hipError_t resize_area_fast_launch(const uint8_t* src, int row_stride, int isx, int isy, uint8_t* dst, int OH, int OW,
@@ -142,18 +146,30 @@ static_assert(sizeof(pc_yolo_scale) == 20, "yolo scale layout");
 // chunks taken in order by the workers, and the caller's thread issues each chunk's H2D as soon
 // as it is packed, so the copy engine runs behind the packing instead of after it (r04: the
 // 6.2 MB of a 1080p frame cost ~0.3 ms of packing with per-call threads, then the H2D).
+// One frame's packing job: chunks are taken from `next`; done[c] and active are guarded by the pool's
+// mutex. A job lives until its last holder drops it; the caller waits for active == 0 before its
+// frame (which the job's function refers to) goes out of scope.
+struct StageJob {
+  std::function<void(int)> fn;
+  int nchunks = 0;
+  std::atomic<int> next{0};
+  std::vector<char> done;
+  int active = 0;                    // workers inside fn
+};
+
+// Persistent packing workers of pc_frame_stage. A worker takes the current job under the lock (a
+// snapshot: the job's function, chunk count and counters belong to that frame alone), works it
+// without the lock, and never sees another frame's job in between - a late wake-up finds either no
+// job or the next frame's, whose state is its own object (the shared job / nchunks
+// fields were re-assigned while a late worker still read them).
 struct StagePool {
   std::vector<std::thread> th;
   std::mutex mu;
   std::condition_variable cv;        // workers: a new job
-  std::condition_variable done_cv;   // caller: a chunk finished
-  std::function<void(int)> job;
-  int nchunks = 0;
-  unsigned gen = 0;
-  std::atomic<int> next{0};
-  std::vector<char> done;            // per chunk (guarded by mu)
+  std::condition_variable done_cv;   // caller: a chunk finished / a worker left the job
+  std::shared_ptr<StageJob> cur;     // the frame being packed (guarded by mu)
+  unsigned gen = 0;                  // bumped per job (guarded by mu)
   bool stop = false;
-  int busy = 0;                      // workers inside the current job
   void start(int n) {
     for (int i = 0; i < n; ++i) {
       try {
@@ -167,23 +183,24 @@ struct StagePool {
     unsigned seen = 0;
     std::unique_lock<std::mutex> lk(mu);
     for (;;) {
-      cv.wait(lk, [&] { return stop || gen != seen; });
+      cv.wait(lk, [&] { return stop || (cur && gen != seen); });
       if (stop) return;
       seen = gen;
-      ++busy;
+      std::shared_ptr<StageJob> j = cur;
+      ++j->active;
       lk.unlock();
-      work();
+      work(*j);
       lk.lock();
-      --busy;
+      --j->active;
       done_cv.notify_all();
     }
   }
-  // take chunks until none is left (the caller runs this too)
-  void work() {
-    for (int c; (c = next.fetch_add(1)) < nchunks;) {
-      job(c);
+  // take chunks of job j until none is left (the caller runs this too)
+  void work(StageJob& j) {
+    for (int c; (c = j.next.fetch_add(1)) < j.nchunks;) {
+      j.fn(c);
       std::lock_guard<std::mutex> g(mu);
-      done[c] = 1;
+      j.done[c] = 1;
       done_cv.notify_all();
     }
   }
@@ -455,12 +472,13 @@ extern "C" int pc_frame_stage(pc_ctx* c, void* d_dst, const void* h_src, size_t 
     // ~512 KB chunks: the first H2D starts after one chunk, the last follows the last pack
     const int nch = (int)std::min<size_t>(64, std::max<size_t>(nt, (n + (512u << 10) - 1) / (512u << 10)));
     const size_t per = (rows + nch - 1) / nch;
+    auto job = std::make_shared<StageJob>();
+    job->fn = [&](int ch) { pack(std::min(rows, ch * per), std::min(rows, (ch + 1) * per)); };
+    job->nchunks = nch;
+    job->done.assign(nch, 0);
     {
       std::lock_guard<std::mutex> g(P.mu);
-      P.job = [&](int ch) { pack(std::min(rows, ch * per), std::min(rows, (ch + 1) * per)); };
-      P.nchunks = nch;
-      P.done.assign(nch, 0);
-      P.next.store(0);
+      P.cur = job;
       ++P.gen;
     }
     P.cv.notify_all();
@@ -471,17 +489,17 @@ extern "C" int pc_frame_stage(pc_ctx* c, void* d_dst, const void* h_src, size_t 
       for (;;) {
         {
           std::unique_lock<std::mutex> lk(P.mu);
-          if (P.done[ch]) break;
-          if (P.next.load() >= nch) {   // everything taken: wait for chunk ch
-            P.done_cv.wait(lk, [&] { return P.done[ch] != 0; });
+          if (job->done[ch]) break;
+          if (job->next.load() >= nch) {   // everything taken: wait for chunk ch
+            P.done_cv.wait(lk, [&] { return job->done[ch] != 0; });
             break;
           }
         }
-        const int mine = P.next.fetch_add(1);
+        const int mine = job->next.fetch_add(1);
         if (mine < nch) {
-          P.job(mine);
+          job->fn(mine);
           std::lock_guard<std::mutex> g(P.mu);
-          P.done[mine] = 1;
+          job->done[mine] = 1;
         }
       }
       const size_t r0 = std::min(rows, ch * per), r1 = std::min(rows, (ch + 1) * per);
@@ -489,10 +507,11 @@ extern "C" int pc_frame_stage(pc_ctx* c, void* d_dst, const void* h_src, size_t 
         herr = hipMemcpyAsync((char*)d_dst + r0 * row_bytes, fs.h + r0 * row_bytes, (r1 - r0) * row_bytes,
                               hipMemcpyHostToDevice, c->stream);
     }
-    {   // the job's lambda refers to this frame: no worker may still be inside it
+    {   // the job's function refers to this frame: no worker may still be inside it, and none may
+        // pick it up later (it stops being the current job)
       std::unique_lock<std::mutex> lk(P.mu);
-      P.done_cv.wait(lk, [&] { return P.busy == 0; });
-      P.job = nullptr;
+      P.done_cv.wait(lk, [&] { return job->active == 0; });
+      P.cur.reset();
     }
     if (herr != hipSuccess) return fail(c, PC_ERR_HIP, std::string("frame_stage H2D: ") + hipGetErrorString(herr));
   }
@@ -540,10 +559,14 @@ enum { OP_CONV = 1, OP_STEM = 2, OP_MAXPOOL = 3, OP_UPSAMPLE = 4, OP_LAYERNORM =
 struct NetBuf { long long elems; int is_f32; void* d = nullptr; };
 // split: f16x3 tensor (detector precision mode): C physical channels = [hi | lo],
 // C / 2 each; the lo half of a pixel is C / 2 elements after its hi half
-struct NetTensor { int buf, H, W, C, cs, coff, is_f32, split; };
+// c8: f16c8 tensor: split storage whose second half holds, per 32
+// channels, the e4m3 bytes [lo8 | hi8]; lo8 = e4m3(lo * 2^e_lo), hi8 = e4m3(hi * 2^e_hi) with
+// per-tensor exponents set by pc_net_calibrate (provisional values before it)
+struct NetTensor { int buf, H, W, C, cs, coff, is_f32, split; int c8 = 0, e_lo = 15, e_hi = 4; };
 struct NetOp { int w[32]; };
-// sx: fused f16x3 split tiles on conv_fast (pc_conv_fast.hip SX)
-struct ConvPlan { int rowb, cfg, splitk, halo = -1, fast = -1, t2d = -1, sx = 0, hx = 0; long long M_per_image; double flops_per_image; };
+// sx: fused f16x3 split tiles on conv_fast (pc_conv_fast.hip SX); c8: its f16c8 form (C8);
+// wf8s: E8M0 exponents of the conv's W_hi8 | W_lo8 << 8 bytes (c8 weights)
+struct ConvPlan { int rowb, cfg, splitk, halo = -1, fast = -1, t2d = -1, sx = 0, hx = 0, c8 = 0, wf8s = 0; long long M_per_image; double flops_per_image; };
 // A stem (tiny Cin) runs as im2col + a 1x1 MFMA conv over 32-element K rows.
 struct StemPlan {
   int use_mfma = 0, npad = 0, cfg = 0, rowb = 0, cin_true = 0;
@@ -569,6 +592,7 @@ struct pc_net {
   int f32 = 0;
   int max_batch = 0;
   int in_tensor = 0;
+  int in_centered = 0;        // the input is the centred image x - 127.5 (program input tensor flag bit 1)
   std::vector<NetBuf> bufs;
   std::vector<NetTensor> tens;
   std::vector<NetOp> ops;
@@ -598,6 +622,8 @@ struct pc_net {
   // graph replay (runs of at most graph_max_batch images)
   int use_graph = 0;
   int capturing = 0;   // inside hipStreamBeginCapture .. EndCapture
+  hipStream_t cap_stream = nullptr;   // private capture stream (pc_net_run)
+  std::mutex graph_mu;
   int graph_max_batch = 1 << 30;
   // per-op HIP-event profiling (pc_net_profile)
   int prof = 0;
@@ -605,6 +631,11 @@ struct pc_net {
   size_t ev_used = 0;
   std::vector<ProfRec> recs;
   std::map<std::pair<int, const void*>, hipGraphExec_t> graphs;
+  // f16c8 convs: per op, E8M0 exponents of the weight bytes' scales (W_hi8 | W_lo8 << 8), 0 elsewhere
+  std::vector<int> wf8s;
+  // absmax calibration of the f16c8 tensors (pc_net_calibrate): per tensor max |x| slots
+  int calib = 0;
+  float* d_absmax = nullptr;
   // arcface scratch
   void* prep = nullptr;
   size_t prep_bytes = 0;
@@ -732,6 +763,13 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
   // PC_SPLIT_FUSED=0: walk the virtual [hi, lo, hi] blocks as plain tiles instead.
   bool all_split = nseg > 0 && !n->f32;
   for (int sg = 0; sg < nseg; ++sg) all_split = all_split && n->tens[w[3 + 5 * sg]].split;
+  // f16c8 inputs: every segment f16c8, conv_fast's C8 tiles only
+  int nc8 = 0;
+  for (int sg = 0; sg < nseg; ++sg) nc8 += n->tens[w[3 + 5 * sg]].c8;
+  const bool in_c8 = nc8 > 0;
+  if (in_c8 && nc8 != nseg) return fail(n->ctx, PC_ERR_FORMAT, "conv mixes f16c8 and other input segments");
+  if (in_c8 && (w[24] > 1 || n->f32 || (getenv("PC_SPLIT_FUSED") && atoi(getenv("PC_SPLIT_FUSED")) == 0)))
+    return fail(n->ctx, PC_ERR_FORMAT, "f16c8 convs run on conv_fast's fused C8 tiles only (no split-K)");
   const bool try_sx = all_split && pl.splitk == 1 && !(getenv("PC_SPLIT_FUSED") && atoi(getenv("PC_SPLIT_FUSED")) == 0);
   {
     const char* e = getenv("PC_CONV_FAST");
@@ -780,6 +818,9 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
           if (npad % bc || (force > 0 && k != force - 1)) continue;
           if (k >= kFastSmallCfg0 && k <= kFastSmallCfg1 && (!small || no_small_tiles) && force <= 0) continue;
           for (int rb : {rowb, 64}) {
+            // f16c8 inputs: tiles with the LDS epilogue (PC_C8_ROWB pins the K row width: tuning)
+            if (in_c8 && (!conv_fast_valid_c8(k, rb) ||
+                          (getenv("PC_C8_ROWB") && atoi(getenv("PC_C8_ROWB")) != rb))) continue;
             if (!conv_fast_valid_sx(k, rb)) continue;
             const long long t = (M + bp - 1) / bp * (npad / bc);
             const double est = (double)((t + 255) / 256) * bc * bp * cost[k];
@@ -787,7 +828,8 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
             break;
           }
         }
-        if (bsx >= 0) { best = bsx; best_rowb = bsx_rowb; pl.sx = 1; }
+        if (bsx >= 0) { best = bsx; best_rowb = bsx_rowb; pl.sx = 1; pl.c8 = in_c8 ? 1 : 0; }
+        else if (in_c8) best = -1;
       }
       pl.fast = best;
       if (best >= 0) { pl.halo = -1; pl.rowb = best_rowb; }
@@ -804,7 +846,8 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
     // split (f16x3): split input -> split output (and split residual, if any) only
     const int sp = X.split ? 1 : 0;
     const bool split_ok = !sp ? !any_split
-                              : (Y.split && (w[21] < 0 || n->tens[w[21]].split) && Y.C / 2 >= 8 && (Y.C / 2) % 8 == 0);
+                              : (Y.split && !Y.c8 && !in_c8 && (w[21] < 0 || (n->tens[w[21]].split && !n->tens[w[21]].c8)) &&
+                                 Y.C / 2 >= 8 && (Y.C / 2) % 8 == 0);
     const int cin_l = sp ? X.C / 2 : X.C;
     const int var = (mode > 0 && !n->f32 && nseg == 1 && pl.splitk == 1 && X.H == Y.H && X.W == Y.W && split_ok)
                         ? conv_t2d_select(cin_l, npad, w[4], w[5], w[6], w[7], w[20], Y.is_f32, Y.cs, Y.coff, sp)
@@ -830,9 +873,9 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
       !getenv("PC_CONV_CFG") && !getenv("PC_CONV_HALO") && !getenv("PC_CONV_T2D") && !getenv("PC_T2D_SPLIT64") &&
       !getenv("PC_SPLIT_FUSED") && !n->f32 && nseg == 1 && pl.splitk == 1) {
     const NetTensor& X = n->tens[w[3]];
-    if (X.split && X.C == 128 && X.cs == 128 && Y.split && Y.C == 128 && npad == 64 && w[4] == 3 && w[5] == 3 &&
+    if (X.split && !X.c8 && !Y.c8 && X.C == 128 && X.cs == 128 && Y.split && Y.C == 128 && npad == 64 && w[4] == 3 && w[5] == 3 &&
         w[6] == 1 && w[7] == 1 && X.H == Y.H && X.W == Y.W && w[15] == 9 * 192 &&
-        !(w[21] >= 0 && (w[22] == RES_UP2 || !n->tens[w[21]].split)) &&
+        !(w[21] >= 0 && (w[22] == RES_UP2 || !n->tens[w[21]].split || n->tens[w[21]].c8)) &&
         (double)X.H * X.W * n->max_batch * X.cs * esz + kZeroTail < 4294967296.0) {
       pl.hx = 1;
       pl.fast = pl.halo = pl.t2d = -1;
@@ -860,10 +903,21 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
       }
     }
   }
+  if (in_c8) {   // nothing else runs f16c8 inputs
+    if (pl.fast < 0 || !pl.c8) return fail(n->ctx, PC_ERR_FORMAT, "no conv_fast C8 tile fits this f16c8 conv");
+    pl.halo = pl.t2d = -1;
+    pl.hx = 0;
+    pl.splitk = 1;
+  }
+  if ((Y.c8 || (w[21] >= 0 && n->tens[w[21]].c8)) && (pl.fast < 0 || !pl.sx || pl.t2d >= 0 || pl.hx || pl.halo >= 0))
+    return fail(n->ctx, PC_ERR_FORMAT, "f16c8 outputs and residuals are written / read by conv_fast's fused tiles only");
   if ((Y.split ? Y.C / 2 : Y.C) > npad) return fail(n->ctx, PC_ERR_FORMAT, "conv output tensor wider than npad");
   if (Y.split && (Y.is_f32 || Y.cs != Y.C || (Y.C / 2) % 8))
     return fail(n->ctx, PC_ERR_FORMAT, "split conv output must be a dense f16 [hi | lo] tensor");
-  if (pl.splitk > 1 && any_split) return fail(n->ctx, PC_ERR_FORMAT, "split-K over split tensors");
+  // split-K reads split inputs (the K iterator's virtual blocks) into f32 partials; the finish
+  // kernel writes plain tensors only (the f16x3 IResNet's FC: split 7x7x512 -> f32 embedding)
+  if (pl.splitk > 1 && (Y.split || (w[21] >= 0 && n->tens[w[21]].split)))
+    return fail(n->ctx, PC_ERR_FORMAT, "split-K into a split output");
   return PC_OK;
 }
 
@@ -1040,6 +1094,75 @@ static int plan_chains(pc_net* n) {
   return PC_OK;
 }
 
+// OCP e4m3fn encoding (round to nearest even, saturating at +-448): the host side of the f16c8
+// weight bytes; the device encodes activations with v_cvt_pk_fp8_f32 (pc_conv_common.h f8_pack8)
+static uint8_t e4m3_encode(float v) {
+  const uint8_t sgn = std::signbit(v) ? 0x80 : 0;
+  const float a = std::fabs(v);
+  if (!(a == a)) return 0x7f;
+  if (a >= 448.f) return sgn | 0x7e;
+  int e2 = 0;
+  std::frexp(a, &e2);
+  int E = e2 - 1;                                 // a in [2^E, 2^(E+1))
+  if (a == 0.f || E < -6) {                       // subnormals: steps of 2^-9
+    const int q = (int)std::nearbyint(std::ldexp(a, 9));
+    return sgn | (uint8_t)q;                      // q == 8 is the smallest normal's encoding
+  }
+  int q = (int)std::nearbyint(std::ldexp(a, 3 - E));   // 8 .. 16
+  if (q == 16) { q = 8; ++E; }
+  if (E > 8 || (E == 8 && q > 14)) return sgn | 0x7e;
+  return sgn | (uint8_t)(((E + 7) << 3) | (q - 8));
+}
+
+// f16c8 conv weights: the program holds the split form [W_hi, W_hi, W_lo] per tap and
+// segment; the W_lo block's bytes become, per 32 input channels, [W_hi8 x 32 | W_lo8 x 32] (e4m3 of
+// W_hi * 2^sh and W_lo * 2^sl, one exponent pair per conv). *wf8s gets their E8M0 scales.
+static int pack_c8_weights(pc_net* n, const NetOp& op, const float* wf, long long cnt, std::vector<_Float16>& h,
+                           int* wf8s) {
+  const int* w = op.w;
+  const int npad = w[14];
+  const long long ktot = w[15];
+  if ((long long)npad * ktot != cnt) return fail(n->ctx, PC_ERR_FORMAT, "f16c8 weights: array size");
+  float mh = 0.f, ml = 0.f;
+  struct Blk { long long k0; int cp, taps; };
+  std::vector<Blk> segs;
+  long long k0 = 0;
+  for (int sg = 0; sg < w[2]; ++sg) {
+    const NetTensor& X = n->tens[w[3 + 5 * sg]];
+    if (!X.c8) return fail(n->ctx, PC_ERR_FORMAT, "f16c8 weights: non-f16c8 segment");
+    const int cp = X.C / 2, taps = w[4 + 5 * sg] * w[5 + 5 * sg];
+    segs.push_back({k0, cp, taps});
+    k0 += (long long)taps * 3 * cp;
+  }
+  if (k0 != ktot) return fail(n->ctx, PC_ERR_FORMAT, "f16c8 weights: K layout");
+  for (const Blk& b : segs)
+    for (int r = 0; r < npad; ++r)
+      for (int t = 0; t < b.taps; ++t) {
+        const float* row = wf + (long long)r * ktot + b.k0 + (long long)t * 3 * b.cp;
+        for (int c = 0; c < b.cp; ++c) {
+          mh = std::max(mh, std::fabs(row[c]));
+          ml = std::max(ml, std::fabs(row[2 * b.cp + c]));
+        }
+      }
+  // the largest magnitude of each half lands in [224, 448)
+  const int sh = mh > 0.f ? (int)std::floor(std::log2(448.f / mh)) : 0;
+  const int sl = ml > 0.f ? (int)std::floor(std::log2(448.f / ml)) : 0;
+  if (127 - sh < 1 || 127 - sh > 254 || 127 - sl < 1 || 127 - sl > 254)
+    return fail(n->ctx, PC_ERR_FORMAT, "f16c8 weights: scale out of range");
+  for (const Blk& b : segs)
+    for (int r = 0; r < npad; ++r)
+      for (int t = 0; t < b.taps; ++t) {
+        const long long base = (long long)r * ktot + b.k0 + (long long)t * 3 * b.cp;
+        uint8_t* dst = reinterpret_cast<uint8_t*>(&h[base + 2 * b.cp]);
+        for (int c = 0; c < b.cp; ++c) {
+          dst[(c >> 5) * 64 + (c & 31)] = e4m3_encode(std::ldexp(wf[base + c], sh));
+          dst[(c >> 5) * 64 + 32 + (c & 31)] = e4m3_encode(std::ldexp(wf[base + 2 * b.cp + c], sl));
+        }
+      }
+  *wf8s = (127 - sh) | ((127 - sl) << 8);
+  return PC_OK;
+}
+
 extern "C" int pc_net_create(pc_ctx* c, const void* prog, size_t nbytes, int precision, int max_batch, pc_net** out) {
   if (!c || !prog || !out || max_batch <= 0) return fail(c, PC_ERR_ARG, "pc_net_create: bad arguments");
   *out = nullptr;
@@ -1067,6 +1190,8 @@ extern "C" int pc_net_create(pc_ctx* c, const void* prog, size_t nbytes, int pre
   }
   for (int i = 0; i < nten; ++i, pos += 8) {
     NetTensor t{P[pos], P[pos + 1], P[pos + 2], P[pos + 3], P[pos + 4], P[pos + 5], P[pos + 6], P[pos + 7] & 1};
+    t.c8 = (P[pos + 7] >> 2) & 1;
+    if (i == n->in_tensor && (P[pos + 7] & 2)) n->in_centered = 1;
     n->tens.push_back(t);
   }
   std::vector<std::pair<long long, long long>> arr;
@@ -1090,6 +1215,21 @@ extern "C" int pc_net_create(pc_ctx* c, const void* prog, size_t nbytes, int pre
       delete n;
       return fail(c, PC_ERR_FORMAT, "split tensor: f16 net, dense [hi | lo] activation buffer");
     }
+  // f16c8 tensors: split storage of whole 32-channel blocks, written by convs and the fused stem,
+  // read by convs (conv_fast C8) and as a conv residual
+  for (auto& t : n->tens)
+    if (t.c8 && (!t.split || (t.C / 2) % 32)) {
+      delete n;
+      return fail(c, PC_ERR_FORMAT, "f16c8 tensor: split storage of 32-channel blocks");
+    }
+  for (auto& op : n->ops) {
+    const int k = op.w[0];
+    auto c8t = [&](int t) { return t >= 0 && t < (int)n->tens.size() && n->tens[t].c8; };
+    if ((k == OP_MAXPOOL || k == OP_UPSAMPLE || k == OP_LAYERNORM || k == OP_ATTENTION) && (c8t(op.w[1]) || c8t(op.w[2]))) {
+      delete n;
+      return fail(c, PC_ERR_FORMAT, "op cannot read or write f16c8 tensors");
+    }
+  }
   for (auto& op : n->ops) {
     const int k = op.w[0];
     auto bad = [&](int t) { return t >= 0 && t < (int)n->tens.size() && n->tens[t].split; };
@@ -1102,9 +1242,15 @@ extern "C" int pc_net_create(pc_ctx* c, const void* prog, size_t nbytes, int pre
     }
   }
   // which arrays are conv weights (uploaded in the activation dtype)
-  std::vector<int> is_w(narr, 0);
-  for (auto& op : n->ops)
-    if (op.w[0] == OP_CONV && op.w[13] >= 0) is_w[op.w[13]] = 1;
+  std::vector<int> is_w(narr, 0), c8_op(narr, -1);
+  n->wf8s.assign(n->ops.size(), 0);
+  for (size_t i = 0; i < n->ops.size(); ++i) {
+    const NetOp& op = n->ops[i];
+    if (op.w[0] == OP_CONV && op.w[13] >= 0) {
+      is_w[op.w[13]] = 1;
+      if (op.w[2] >= 1 && n->tens[op.w[3]].c8) c8_op[op.w[13]] = (int)i;
+    }
+  }
   n->arrays.assign(narr, nullptr);
   n->array_count.assign(narr, 0);
   int rc = PC_OK;
@@ -1115,6 +1261,8 @@ extern "C" int pc_net_create(pc_ctx* c, const void* prog, size_t nbytes, int pre
     if (is_w[i] && !n->f32) {
       std::vector<_Float16> h(cnt);
       for (long long k = 0; k < cnt; ++k) h[k] = (_Float16)data[off + k];
+      if (c8_op[i] >= 0 && (rc = pack_c8_weights(n, n->ops[c8_op[i]], data + off, cnt, h, &n->wf8s[c8_op[i]])) != PC_OK)
+        break;
       if (hipMalloc(&n->arrays[i], cnt * 2 + 16) != hipSuccess ||
           hipMemcpy(n->arrays[i], h.data(), cnt * 2, hipMemcpyHostToDevice) != hipSuccess)
         rc = fail(c, PC_ERR_HIP, "weight upload failed");
@@ -1233,6 +1381,8 @@ extern "C" int pc_net_destroy(pc_net* n) {
   hipSetDevice(n->ctx->device);
   hipStreamSynchronize(n->ctx->stream);
   for (auto& kv : n->graphs) hipGraphExecDestroy(kv.second);
+  if (n->cap_stream) hipStreamDestroy(n->cap_stream);
+  if (n->d_absmax) hipFree(n->d_absmax);
   for (void* a : n->arrays) if (a) hipFree(a);
   for (auto& b : n->bufs) if (b.d) hipFree(b.d);
   if (n->partial) hipFree(n->partial);
@@ -1270,9 +1420,8 @@ static int plan_class(const pc_net* n, int N) {
   return -1;
 }
 
-static int run_ops(pc_net* n, int N) {
+static int run_ops(pc_net* n, int N, hipStream_t s) {
   pc_ctx* c = n->ctx;
-  hipStream_t s = c->stream;
   // eager runs are profiled; a captured run records no events (its replays are not profiled)
   const bool prof = n->prof && !n->capturing;
   if (n->in_copy)
@@ -1337,6 +1486,7 @@ static int run_ops(pc_net* n, int N) {
         S.H = X.H; S.W = X.W; S.C = X.C; S.cs = X.cs;
         S.KH = w[4 + 5 * sg]; S.KW = w[5 + 5 * sg]; S.stride = w[6 + 5 * sg]; S.pad = w[7 + 5 * sg];
         S.cblk = X.C / bke;
+        if (X.c8) S.f8s = (127 - X.e_lo) | ((127 - X.e_hi) << 8);
         if (X.split && pl.sx) {   // fused split tiles: the hi blocks; lo block = hi block + vwrap
           S.cblk = S.cblk / 2;
           S.vwrap = S.cblk;
@@ -1371,6 +1521,17 @@ static int run_ops(pc_net* n, int N) {
       p.act_after_res = w[23];
       p.kt_total = kt;
       p.sx = pl.sx;
+      p.c8 = pl.c8;
+      p.wf8s = n->wf8s[i];
+      if (Y.c8) {
+        p.yc8 = 1;
+        p.ylo_mul = std::ldexp(1.f, Y.e_lo);
+        p.yhi_mul = std::ldexp(1.f, Y.e_hi);
+      }
+      if (w[21] >= 0 && n->tens[w[21]].c8) {
+        p.rc8 = 1;
+        p.rlo_inv = std::ldexp(1.f, -n->tens[w[21]].e_lo);
+      }
       p.splitk = pl.splitk;
       p.partial = n->partial;
       p.zero = c->zero;
@@ -1408,6 +1569,11 @@ static int run_ops(pc_net* n, int N) {
       const StemPlan& st = n->stems[i];
       const int st_cwrite = std::min(Y.split ? Y.C / 2 : Y.C, st.npad);
       p.ysplit = Y.split ? Y.C / 2 : 0;
+      if (Y.c8) {
+        p.yc8 = 1;
+        p.ylo_mul = std::ldexp(1.f, Y.e_lo);
+        p.yhi_mul = std::ldexp(1.f, Y.e_hi);
+      }
       // fused gather + MFMA stem (pc_stem.hip) unless PC_STEM_UNFUSED is set
       // (stem_fused stores f16: an f32 output tensor inside an f16 net takes the unfused path)
       const bool fused = st.use_mfma && !getenv("PC_STEM_UNFUSED") && !Y.is_f32 &&
@@ -1492,6 +1658,12 @@ static int run_ops(pc_net* n, int N) {
       p.scale = 1.0f / sqrtf((float)w[4]);
       HIPCHK(c, attention_launch(n->f32, p, w[4], s));
     }
+    if (n->calib && (w[0] == OP_CONV || w[0] == OP_STEM)) {   // pc_net_calibrate: max |x| of the op's output
+      const NetTensor& Y = n->tens[w[1]];
+      if (!Y.is_f32 && !n->f32)
+        HIPCHK(c, absmax_f16_launch(tensor_ptr(n, w[1]), (long long)N * Y.H * Y.W, Y.split ? Y.C / 2 : Y.C, Y.cs,
+                                    reinterpret_cast<unsigned*>(n->d_absmax) + w[1], s));
+    }
     if (prof) {
       int rc = prof_event(n, &rec.b);
       if (rc) return rc;
@@ -1499,6 +1671,40 @@ static int run_ops(pc_net* n, int N) {
       open_ev = rec.b;
     }
   }
+  return PC_OK;
+}
+
+// f16c8 scale calibration: one eager run over N images records every conv / stem
+// output's largest magnitude; each f16c8 tensor then gets e_hi with max * 2^e_hi in
+// [448 / 2^(headroom+1), 448 / 2^headroom) and e_lo = e_hi + 11 (|lo| <= 2^-11 |x|). The
+// activations may grow 2^headroom times past the calibration before the e4m3 bytes saturate.
+extern "C" int pc_net_calibrate(pc_net* n, const void* d_in, int N, int headroom_log2, float* h_absmax) {
+  if (!n || !d_in || N <= 0 || N > n->max_batch || headroom_log2 < 0 || headroom_log2 > 8) return PC_ERR_ARG;
+  pc_ctx* c = n->ctx;
+  std::lock_guard<std::mutex> lk(n->graph_mu);
+  const size_t nt = n->tens.size();
+  if (!n->d_absmax) HIPCHK(c, hipMalloc((void**)&n->d_absmax, nt * 4));
+  HIPCHK(c, hipMemsetAsync(n->d_absmax, 0, nt * 4, c->stream));
+  n->cur_input = d_in;
+  n->calib = 1;
+  const int rc = run_ops(n, N, c->stream);
+  n->calib = 0;
+  if (rc) return rc;
+  std::vector<float> mx(nt);
+  HIPCHK(c, hipMemcpyAsync(mx.data(), n->d_absmax, nt * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (size_t t = 0; t < nt; ++t) {
+    NetTensor& T = n->tens[t];
+    if (h_absmax) h_absmax[t] = mx[t];
+    if (!T.c8 || !(mx[t] > 0.f) || !std::isfinite(mx[t])) continue;
+    const int e = (int)std::floor(std::log2(448.f / mx[t])) - headroom_log2;
+    if (127 - e < 1 || 127 - (e + 11) < 1 || 127 - e > 254) return fail(c, PC_ERR_FORMAT, "f16c8 scale out of range");
+    T.e_hi = e;
+    T.e_lo = e + 11;
+  }
+  // captured graphs hold the old scales as kernel arguments
+  for (auto& kv : n->graphs) hipGraphExecDestroy(kv.second);
+  n->graphs.clear();
   return PC_OK;
 }
 
@@ -1542,6 +1748,7 @@ extern "C" int pc_net_profile_ops(pc_net* n, double* out, int max_recs) {
     const ConvPlan* pl = conv ? (r.small >= 0 ? &n->plans_cls[r.small][r.op] : &n->plans[r.op]) : nullptr;
     o[4] = r.code >= 0 ? r.code
                        : conv ? (pl->hx            ? 500
+                                 : pl->c8          ? 600 + pl->fast
                                  : pl->t2d >= 0    ? 200 + pl->t2d
                                  : pl->fast >= 0   ? 100 + pl->fast
                                                    : pl->halo)
@@ -1556,16 +1763,24 @@ extern "C" int pc_net_run(pc_net* n, const void* d_in, int N) {
   pc_ctx* c = n->ctx;
   if (N <= 0 || N > n->max_batch) return fail(c, PC_ERR_ARG, "batch out of range");
   n->cur_input = d_in;
-  if (!n->use_graph || N > n->graph_max_batch) return run_ops(n, N);
+  if (!n->use_graph || N > n->graph_max_batch) return run_ops(n, N, c->stream);
+  // Graphs are captured on a stream private to the net, never on the context stream: a context
+  // (and its stream) is shared by every FaceEmbedder of the process, and work another host thread
+  // enqueued there during an open capture would be recorded into this graph (not run now, replayed
+  // later) or invalidate it. Capturing executes nothing, so the private stream needs no ordering
+  // with the context stream; the instantiated graph is launched on the context stream. The lock
+  // serialises capture and the graph table of one net between host threads.
+  std::lock_guard<std::mutex> lk(n->graph_mu);
   auto key = std::make_pair(N, d_in);
   auto it = n->graphs.find(key);
   if (it == n->graphs.end()) {
+    if (!n->cap_stream) HIPCHK(c, hipStreamCreateWithFlags(&n->cap_stream, hipStreamNonBlocking));
     hipGraph_t g;
-    HIPCHK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    HIPCHK(c, hipStreamBeginCapture(n->cap_stream, hipStreamCaptureModeThreadLocal));
     n->capturing = 1;
-    int rc = run_ops(n, N);
+    int rc = run_ops(n, N, n->cap_stream);
     n->capturing = 0;
-    hipError_t e = hipStreamEndCapture(c->stream, &g);
+    hipError_t e = hipStreamEndCapture(n->cap_stream, &g);
     if (rc != PC_OK) return rc;
     if (e != hipSuccess) return fail(c, PC_ERR_HIP, std::string("graph capture: ") + hipGetErrorString(e));
     hipGraphExec_t ge;
@@ -1678,7 +1893,9 @@ extern "C" int pc_face_quality(pc_ctx* c, const uint8_t* chips, int n, int side,
 extern "C" int pc_arcface_prep(pc_ctx* c, int prec, const uint8_t* chips, int n, int side, int flip, void* out) {
   if (!c || n < 0) return fail(c, PC_ERR_ARG, "pc_arcface_prep: bad arguments");
   if (n == 0) return PC_OK;
-  HIPCHK(c, arcprep_launch(prec == PC_PREC_F32, chips, n, side, flip, out, c->stream));
+  if (prec != PC_PREC_F16 && prec != PC_PREC_F32 && prec != PC_PREC_F16X3)
+    return fail(c, PC_ERR_ARG, "pc_arcface_prep: bad precision");
+  HIPCHK(c, arcprep_launch(prec, chips, n, side, flip, out, c->stream));
   return PC_OK;
 }
 
@@ -1744,7 +1961,8 @@ extern "C" int pc_arcface_embed(pc_net* net, const uint8_t* chips, int n, int fl
     HIPCHK(c, hipMalloc(&net->prep, need));
     net->prep_bytes = need;
   }
-  HIPCHK(c, arcprep_launch(net->f32, chips, n, I.H, flip, net->prep, c->stream));
+  HIPCHK(c, arcprep_launch(net->f32 ? PC_PREC_F32 : (net->in_centered ? PC_PREC_F16X3 : PC_PREC_F16), chips, n, I.H,
+                           flip, net->prep, c->stream));
   int rc = pc_net_run(net, net->prep, rows);
   if (rc) return rc;
   const NetTensor& O = net->tens[net->outs[0]];

@@ -10,6 +10,8 @@ typedef _Float16 f16;
 typedef f16 f16x8 __attribute__((ext_vector_type(8)));
 typedef f16 f16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((address_space(1))) void* gptr_t;
 
@@ -31,6 +33,10 @@ struct ConvSeg {
   // x_hi*W_hi + x_lo*W_hi + x_hi*W_lo accumulate in f32. cblk counts the
   // virtual blocks; a virtual block >= vwrap reads physical block (block - vwrap). 0: plain.
   int vwrap;
+  // f16c8 tensors: the second half of a pixel holds, per 32-channel block, the
+  // e4m3 bytes [lo8 x 32 | hi8 x 32]; f8s = E8M0 exponents of their scales, lo | hi << 8
+  // (true lo = lo8 * 2^(e_lo - 127))
+  int f8s;
 };
 
 struct ConvParams {
@@ -64,6 +70,15 @@ struct ConvParams {
   // f16x3 fused split tiles (conv_fast SX): a K tile is one (tap, hi channel block) staged with
   // its lo block and both weight halves; seg cblk counts hi blocks, vwrap is the lo block offset
   int sx;
+  // f16c8 convs (conv_fast C8): the K tile's f16 halves give x_hi*W_hi; the f8 rows
+  // ([lo8 | hi8] against [W_hi8 | W_lo8]) give x_lo*W_hi + x_hi*W_lo in one block-scaled e4m3 MFMA.
+  // wf8s: E8M0 exponents of the weight bytes' scales, W_hi8 | W_lo8 << 8.
+  int c8;
+  int wf8s;
+  // f16c8 output / residual (ysplit / rsplit locate the f8 region): y: lo8 = e4m3(lo * ylo_mul),
+  // hi8 = e4m3(hi * yhi_mul); residual: hi + lo8 * rlo_inv
+  int yc8, rc8;
+  float ylo_mul, yhi_mul, rlo_inv;
 };
 
 // Direct convolution for tiny input channel counts (network stems, Cin <= 4).
@@ -79,6 +94,8 @@ struct StemParams {
   void* y;
   int cpad;            // channels written (>= cout, the tail is zero-filled)
   int ysplit;          // f16x3 split output: lo half at +ysplit elements (0: plain)
+  int yc8;             // f16c8 output: the f8 region at +ysplit elements (ConvParams)
+  float ylo_mul, yhi_mul;
 };
 
 struct PoolParams {

@@ -28,6 +28,31 @@ __device__ __forceinline__ float act_apply(float v, int act, float slope) {
   return v;
 }
 
+// e4m3 (OCP e4m3fn, gfx950 v_cvt_pk_fp8_f32 / v_cvt_f32_fp8) bytes of the f16c8 activations
+// (DESIGN.md §3.7): 8 values times a power-of-two scale, saturated to the format's +-448
+__device__ __forceinline__ float f8_sat(float v) { return fminf(fmaxf(v, -448.f), 448.f); }
+__device__ __forceinline__ uint2 f8_pack8(const float* v, float mul) {
+  int w0 = __builtin_amdgcn_cvt_pk_fp8_f32(f8_sat(v[0] * mul), f8_sat(v[1] * mul), 0, false);
+  w0 = __builtin_amdgcn_cvt_pk_fp8_f32(f8_sat(v[2] * mul), f8_sat(v[3] * mul), w0, true);
+  int w1 = __builtin_amdgcn_cvt_pk_fp8_f32(f8_sat(v[4] * mul), f8_sat(v[5] * mul), 0, false);
+  w1 = __builtin_amdgcn_cvt_pk_fp8_f32(f8_sat(v[6] * mul), f8_sat(v[7] * mul), w1, true);
+  return uint2{(unsigned)w0, (unsigned)w1};
+}
+__device__ __forceinline__ void f8_unpack8(uint2 q, float* out) {
+  out[0] = __builtin_amdgcn_cvt_f32_fp8((int)q.x, 0);
+  out[1] = __builtin_amdgcn_cvt_f32_fp8((int)q.x, 1);
+  out[2] = __builtin_amdgcn_cvt_f32_fp8((int)q.x, 2);
+  out[3] = __builtin_amdgcn_cvt_f32_fp8((int)q.x, 3);
+  out[4] = __builtin_amdgcn_cvt_f32_fp8((int)q.y, 0);
+  out[5] = __builtin_amdgcn_cvt_f32_fp8((int)q.y, 1);
+  out[6] = __builtin_amdgcn_cvt_f32_fp8((int)q.y, 2);
+  out[7] = __builtin_amdgcn_cvt_f32_fp8((int)q.y, 3);
+}
+// byte offset of channel ch's lo8 byte inside a pixel's f8 region (per 32-channel block: lo8 x 32,
+// then hi8 x 32, i.e. the hi8 byte is kF8Hi further)
+constexpr int kF8Hi = 32;
+__device__ __forceinline__ int f8_lo_byte(int ch) { return ((ch >> 5) << 6) + (ch & 31); }
+
 template <typename T>
 __device__ __forceinline__ void store4(T* dst, const float* v, int n);
 
@@ -327,6 +352,7 @@ __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, f32x4 (&a
       for (int kg = 0; kg < IT; kg += RG) {
       RV rv[RG][RN];
       RV rv2[SPLIT ? RG : 1][RN];   // f16x3: the residual's lo half
+      uint2 rq[SPLIT ? RG : 1];     // f16c8: the residual's lo8 bytes
       if (p.res_mode != RES_NONE) {
 #pragma unroll
         for (int kk = 0; kk < RG; ++kk) {
@@ -337,6 +363,7 @@ __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, f32x4 (&a
           if constexpr (SPLIT) {
 #pragma unroll
             for (int j = 0; j < RN; ++j) rv2[k][j] = RV{};
+            rq[k] = uint2{0u, 0u};
           }
           if (pix < p.M && full) {
             long long rpix = pix;
@@ -349,7 +376,10 @@ __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, f32x4 (&a
 #pragma unroll
             for (int j = 0; j < RN; ++j) rv[k][j] = *reinterpret_cast<const RV*>(rp + j * (8 / RN));
             if constexpr (SPLIT) {
-              if (p.rsplit) {
+              if (p.rc8) {
+                rq[k] = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(rp - ch + p.rsplit) +
+                                                         f8_lo_byte(ch));
+              } else if (p.rsplit) {
 #pragma unroll
                 for (int j = 0; j < RN; ++j) rv2[k][j] = *reinterpret_cast<const RV*>(rp + p.rsplit + j * (8 / RN));
               }
@@ -391,8 +421,17 @@ __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, f32x4 (&a
           if (full) {
             if constexpr (ESZ == 2) {
               if constexpr (SPLIT) {   // hi + lo first: the f32 value of the split residual
+                float rl[8];
+                if (p.rc8) {
+                  f8_unpack8(rq[k], rl);
 #pragma unroll
-                for (int j = 0; j < 8; ++j) v[j] += (float)rv[k][0][j] + (float)rv2[k][0][j];
+                  for (int j = 0; j < 8; ++j) rl[j] *= p.rlo_inv;
+                } else {
+#pragma unroll
+                  for (int j = 0; j < 8; ++j) rl[j] = (float)rv2[k][0][j];
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] += (float)rv[k][0][j] + rl[j];
               } else {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) v[j] += (float)rv[k][0][j];
@@ -405,7 +444,12 @@ __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, f32x4 (&a
             long long rpix = pix;
             if (p.res_mode == RES_UP2) rpix = ((long long)n * p.rH + (oh >> 1)) * p.rW + (ow >> 1);
             const T* rp = reinterpret_cast<const T*>(p.res) + rpix * p.rcs + ch;
-            for (int j = 0; j < nv; ++j) v[j] += SPLIT && p.rsplit ? (float)rp[j] + (float)rp[p.rsplit + j] : (float)rp[j];
+            if (SPLIT && p.rc8) {
+              const unsigned char* rb = reinterpret_cast<const unsigned char*>(rp - ch + p.rsplit) + f8_lo_byte(ch);
+              for (int j = 0; j < nv; ++j) v[j] += (float)rp[j] + __builtin_amdgcn_cvt_f32_fp8((int)rb[j], 0) * p.rlo_inv;
+            } else {
+              for (int j = 0; j < nv; ++j) v[j] += SPLIT && p.rsplit ? (float)rp[j] + (float)rp[p.rsplit + j] : (float)rp[j];
+            }
           }
         }
         act8(v);   // the one activation point
@@ -413,8 +457,17 @@ __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, f32x4 (&a
           if (full) {
             if constexpr (ESZ == 2) {
               if constexpr (SPLIT) {   // hi + lo first: the f32 value of the split residual
+                float rl[8];
+                if (p.rc8) {
+                  f8_unpack8(rq[k], rl);
 #pragma unroll
-                for (int j = 0; j < 8; ++j) v[j] += (float)rv[k][0][j] + (float)rv2[k][0][j];
+                  for (int j = 0; j < 8; ++j) rl[j] *= p.rlo_inv;
+                } else {
+#pragma unroll
+                  for (int j = 0; j < 8; ++j) rl[j] = (float)rv2[k][0][j];
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] += (float)rv[k][0][j] + rl[j];
               } else {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) v[j] += (float)rv[k][0][j];
@@ -427,7 +480,12 @@ __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, f32x4 (&a
             long long rpix = pix;
             if (p.res_mode == RES_UP2) rpix = ((long long)n * p.rH + (oh >> 1)) * p.rW + (ow >> 1);
             const T* rp = reinterpret_cast<const T*>(p.res) + rpix * p.rcs + ch;
-            for (int j = 0; j < nv; ++j) v[j] += SPLIT && p.rsplit ? (float)rp[j] + (float)rp[p.rsplit + j] : (float)rp[j];
+            if (SPLIT && p.rc8) {
+              const unsigned char* rb = reinterpret_cast<const unsigned char*>(rp - ch + p.rsplit) + f8_lo_byte(ch);
+              for (int j = 0; j < nv; ++j) v[j] += (float)rp[j] + __builtin_amdgcn_cvt_f32_fp8((int)rb[j], 0) * p.rlo_inv;
+            } else {
+              for (int j = 0; j < nv; ++j) v[j] += SPLIT && p.rsplit ? (float)rp[j] + (float)rp[p.rsplit + j] : (float)rp[j];
+            }
           }
         }
 #pragma unroll
@@ -451,7 +509,25 @@ __device__ __forceinline__ void conv_epilogue_lds(const ConvParams& p, f32x4 (&a
               for (int j = 0; j < nv; ++j) yp[j] = h[j];
             }
             if constexpr (SPLIT) {
-              if (p.ysplit) {   // f16x3 output: lo = f16(v - f16(v))
+              if (p.yc8) {   // f16c8 output: lo8 = e4m3((v - hi) * ylo_mul), hi8 = e4m3(hi * yhi_mul)
+                float lo[8], hf[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                  hf[j] = (float)h[j];
+                  lo[j] = v[j] - hf[j];
+                }
+                const uint2 ql = f8_pack8(lo, p.ylo_mul), qh = f8_pack8(hf, p.yhi_mul);
+                char* fb = reinterpret_cast<char*>(yp - ch + p.ysplit) + f8_lo_byte(ch);
+                if (full) {
+                  *reinterpret_cast<uint2*>(fb) = ql;
+                  *reinterpret_cast<uint2*>(fb + kF8Hi) = qh;
+                } else {
+                  for (int j = 0; j < nv; ++j) {
+                    fb[j] = (char)((j < 4 ? ql.x : ql.y) >> (8 * (j & 3)));
+                    fb[kF8Hi + j] = (char)((j < 4 ? qh.x : qh.y) >> (8 * (j & 3)));
+                  }
+                }
+              } else if (p.ysplit) {   // f16x3 output: lo = f16(v - f16(v))
                 f16x8 l;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) l[j] = (f16)(v[j] - (float)h[j]);

@@ -42,8 +42,11 @@ __host__ __device__ constexpr int fast_epi_bytes() {
 // W_hi*x_hi, W_lo*x_hi, W_hi*x_lo (2/3 of the staging and fragment reads of walking the virtual
 // [hi, lo, hi] blocks as plain tiles). The weight rows keep the [W_hi, W_hi, W_lo] per-tap layout
 // of the virtual K (the duplicate is skipped).
+// C8 (with SX staging): f16c8 inputs - per K tile (32 or 64 channels) the f16 MFMAs for
+// x_hi*W_hi, then one block-scaled e4m3 MFMA (v_mfma_scale_f32_16x16x128_f8f6f4) over the f8 rows
+// [lo8 | hi8] x [W_hi8 | W_lo8] for x_lo*W_hi + x_hi*W_lo: 3 MFMA issues per tile where SX takes 6.
 template <typename T, int BC, int BP, int ROWB, int WC, int WP, int NSTAGE, int OCC = 1, bool SPLIT = false,
-          bool SX = false>
+          bool SX = false, bool C8 = false>
 __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fast(ConvParams p) {
   constexpr int NW = WC * WP;
   constexpr int NH = SX ? 2 : 1;              // staged halves per tile
@@ -57,6 +60,7 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
   // the waves past NB goes to a trash area, so every wave still issues NIB (static vmcnt)
   constexpr int NIA = NA / NW, NIB = (NB + NW - 1) / NW, NI = NH * (NIA + NIB);
   static_assert(!SX || sizeof(T) == 2, "fused split tiles: f16 only");
+  static_assert(!C8 || (SX && (ROWB == 128 || ROWB == 64)), "f16c8 tiles: fused split staging");
   constexpr int WTC = BC / WC, WTP = BP / WP;
   constexpr int TC = WTC / 16, TP = WTP / 16;
   constexpr int BUF = NH * (BC + BP) * ROWB;
@@ -233,11 +237,62 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
       });
     });
   };
-  auto compute = [&](auto slotc) __attribute__((always_inline)) {
+  // f16c8: per-lane E8M0 scale operands of the block-scaled MFMA. The scale VGPR of lane L covers K
+  // block L >> 4 (K 32 (L >> 4) .. +31) of row / column L & 15 (measured, tools/mx_probe.hip); the f8
+  // rows hold [lo8 | hi8] ([W_hi8 | W_lo8]) per 32 channels, so even K blocks are lo8, odd ones hi8
+  const bool klo = ((lane >> 4) & 1) == 0;
+  const int wsc = klo ? (p.wf8s & 0xff) : ((p.wf8s >> 8) & 0xff);
+  const int xsc0 = klo ? (p.seg[0].f8s & 0xff) : ((p.seg[0].f8s >> 8) & 0xff);
+  const int xsc1 = klo ? (p.seg[1].f8s & 0xff) : ((p.seg[1].f8s >> 8) & 0xff);
+  const int kt0 = p.seg[0].kt;
+  auto compute = [&](auto slotc, int tix) __attribute__((always_inline)) {
     constexpr int slot = decltype(slotc)::value;
     const char* base = smem + slot * BUF;
     if constexpr (PINNED) {
       compute_pinned(slotc);
+      return;
+    }
+    if constexpr (C8) {
+#pragma unroll
+      for (int ks = 0; ks < KSTEPS; ++ks) {
+        const unsigned ko = ((ks * 4 + (lane >> 4)) ^ sw) << 4;
+        f16x8 fah[TC], fbh[TP];
+#pragma unroll
+        for (int t = 0; t < TC; ++t) fah[t] = *reinterpret_cast<const f16x8*>(base + a_row + ko + t * 16 * ROWB);
+#pragma unroll
+        for (int t = 0; t < TP; ++t) fbh[t] = *reinterpret_cast<const f16x8*>(base + b_row + ko + t * 16 * ROWB);
+#pragma unroll
+        for (int a = 0; a < TC; ++a)
+#pragma unroll
+          for (int b = 0; b < TP; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fah[a], fbh[b], acc[a][b], 0, 0, 0);
+        if constexpr (TC * TP >= 16) __builtin_amdgcn_sched_barrier(0);
+      }
+      // f8 rows: a lane's 32 operand bytes are K 16g..16g+15 (chunk g) and 64+16g.. (chunk 4+g); a
+      // 64-byte row (32 channels) fills K 0-63 and the MFMA's K 64-127 are zeros
+      const unsigned k0 = ((lane >> 4) ^ sw) << 4, k1 = ((4 + (lane >> 4)) ^ sw) << 4;
+      i32x8 a8[TC], b8[TP];
+#pragma unroll
+      for (int t = 0; t < TC; ++t) {
+        const i32x4 u = *reinterpret_cast<const i32x4*>(base + a_row + BC * ROWB + k0 + t * 16 * ROWB);
+        i32x4 v = i32x4{0, 0, 0, 0};
+        if constexpr (ROWB == 128) v = *reinterpret_cast<const i32x4*>(base + a_row + BC * ROWB + k1 + t * 16 * ROWB);
+        a8[t] = i32x8{u[0], u[1], u[2], u[3], v[0], v[1], v[2], v[3]};
+      }
+#pragma unroll
+      for (int t = 0; t < TP; ++t) {
+        const i32x4 u = *reinterpret_cast<const i32x4*>(base + b_row + BP * ROWB + k0 + t * 16 * ROWB);
+        i32x4 v = i32x4{0, 0, 0, 0};
+        if constexpr (ROWB == 128) v = *reinterpret_cast<const i32x4*>(base + b_row + BP * ROWB + k1 + t * 16 * ROWB);
+        b8[t] = i32x8{u[0], u[1], u[2], u[3], v[0], v[1], v[2], v[3]};
+      }
+      const int xsc = tix < kt0 ? xsc0 : xsc1;
+#pragma unroll
+      for (int a = 0; a < TC; ++a)
+#pragma unroll
+        for (int b = 0; b < TP; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a8[a], b8[b], acc[a][b], 0, 0, 0, wsc, 0, xsc);
+      if constexpr (TC * TP >= 16) __builtin_amdgcn_sched_barrier(0);
       return;
     }
     if constexpr (SX) {
@@ -323,6 +378,7 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
     advance(more);
     kiss += more ? 1 : 0;
   });
+  int it = 0;
   // one step: retire tile `it`, refill the slot of tile it-1 with tile it+NSTAGE-1
   auto step = [&](auto jc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
@@ -332,9 +388,8 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
     const bool more = kiss + 1 < nk;
     advance(more);
     kiss += more ? 1 : 0;
-    if (!(p.dbg & 2)) compute(std::integral_constant<int, j>{});
+    if (!(p.dbg & 2)) compute(std::integral_constant<int, j>{}, it + j);
   };
-  int it = 0;
   if (p.dbg & 8) return;   // tuning only: prologue only
   for (; it + NSTAGE <= nk; it += NSTAGE)
     static_for<NSTAGE>([&](auto jc) __attribute__((always_inline)) { step(jc); });
@@ -423,15 +478,28 @@ constexpr int fast_sx_stages() {
   return ns;
 }
 
+// power-of-two channel tiles: the LDS epilogue (the only one that writes f16c8 outputs)
+template <int BC>
+constexpr bool LDS_EPI_OK() { return ((BC / 8) & (BC / 8 - 1)) == 0 && ((BC / 16) & (BC / 16 - 1)) == 0; }
+
 template <typename T, int BC, int BP, int ROWB, int WC, int WP, int NSTAGE, int OCC = 1>
 static hipError_t launch_fast_cfg(const ConvParams& p, hipStream_t s) {
   if constexpr (!fast_valid<BC, BP, ROWB, WC * WP>()) {
     return hipErrorInvalidValue;
   } else {
     const int nwg = (p.M + BP - 1) / BP * (p.npad / BC);
-    if (p.sx) {   // fused f16x3 tiles: always the split epilogue
+    if (p.sx) {   // fused f16x3 / f16c8 tiles: always the split epilogue
       constexpr int NS = fast_sx_stages<BC, BP, ROWB, WC * WP, NSTAGE>();
       if constexpr (sizeof(T) == 2 && ROWB != 256 && fast_sx_fits<BC, BP, ROWB, WC * WP, OCC, NS>()) {
+        if (p.c8) {
+          if constexpr (LDS_EPI_OK<BC>()) {
+            hipLaunchKernelGGL((conv_fast<T, BC, BP, ROWB, WC, WP, NS, OCC, true, true, true>), dim3(nwg),
+                               dim3(64 * WC * WP), 0, s, p);
+            return hipGetLastError();
+          } else {
+            return hipErrorInvalidValue;
+          }
+        }
         hipLaunchKernelGGL((conv_fast<T, BC, BP, ROWB, WC, WP, NS, OCC, true, true>), dim3(nwg), dim3(64 * WC * WP), 0,
                            s, p);
         return hipGetLastError();
@@ -508,6 +576,13 @@ int conv_fast_valid_sx(int cfg, int rowb) {
   if ((c.bc / rpi) % c.nw || c.bp % rpi) return 0;
   const int ring = 2 * 2 * (c.bc + c.bp) * rowb + ((c.bp / rpi) % c.nw ? c.nw * 1024 : 0);
   return ring <= 163840;
+}
+
+// can cfg run f16c8 convs at K rows of rowb bytes (fused split staging, LDS epilogue)?
+int conv_fast_valid_c8(int cfg, int rowb) {
+  if (!conv_fast_valid_sx(cfg, rowb)) return 0;
+  const int bc = kFastCfgs[cfg].bc;
+  return ((bc / 8) & (bc / 8 - 1)) == 0 && ((bc / 16) & (bc / 16 - 1)) == 0;
 }
 
 // can cfg run convs whose K rows are rowb bytes?

@@ -45,7 +45,10 @@ __global__ __launch_bounds__(256, 1) void conv_hx64(ConvParams p, int nby, int n
     const int s = bb >> 8, q = (bb >> 4) & 15;
     const int iy = oy0 - 1 + s / HX_PW, ix = ox0 - 1 + (s - (s / HX_PW) * HX_PW);
     const bool ok = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
-    unsigned off = ok ? (unsigned)(((n * H + iy) * W + ix) * S.cs * 2 + ((q ^ (s & 15)) << 4)) : S.zero_off;
+    // unsigned byte offset: the pixel index fits 31 bits, its byte offset only 32 (the planner
+    // keeps every activation buffer below 4 GiB); signed int arithmetic would overflow past 2 GiB
+    unsigned off = ok ? (unsigned)((n * H + iy) * W + ix) * (unsigned)(S.cs * 2) + (unsigned)((q ^ (s & 15)) << 4)
+                      : S.zero_off;
     asm volatile("" : "+v"(off));
     __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)(halo + i * 1024), 16, off, 0, 0, 0);
   }

@@ -303,16 +303,17 @@ __global__ __launch_bounds__(256) void face_quality(const uint8_t* __restrict__ 
 // ArcFace input: BGR u8 chip -> RGB, x/127.5 - 1 (f32 division as numpy does),
 // NHWC with 4 channels; optionally the horizontally flipped copy at n + N.
 // ---------------------------------------------------------------------------
-template <typename T>
+// CENTRED: x - 127.5 instead (exact in f16), the f16x3 IResNet's input (1/127.5 in its stem).
+template <typename T, bool CENTRED = false>
 __global__ void arcface_prep(const uint8_t* __restrict__ chips, int N, int side, int flip, T* __restrict__ out) {
   const int n = blockIdx.y;
   const int pix = blockIdx.x * blockDim.x + threadIdx.x;
   if (pix >= side * side) return;
   const int y = pix / side, x = pix - (pix / side) * side;
   const uint8_t* s = chips + ((long long)n * side * side + pix) * 3;
-  const float r = (float)s[2] / 127.5f - 1.0f;
-  const float g = (float)s[1] / 127.5f - 1.0f;
-  const float b = (float)s[0] / 127.5f - 1.0f;
+  const float r = CENTRED ? (float)s[2] - 127.5f : (float)s[2] / 127.5f - 1.0f;
+  const float g = CENTRED ? (float)s[1] - 127.5f : (float)s[1] / 127.5f - 1.0f;
+  const float b = CENTRED ? (float)s[0] - 127.5f : (float)s[0] / 127.5f - 1.0f;
   T* o = out + ((long long)n * side * side + pix) * 4;
   T* of = out + ((long long)(n + N) * side * side + y * side + (side - 1 - x)) * 4;
   if constexpr (sizeof(T) == 2) {
@@ -444,9 +445,11 @@ hipError_t quality_launch(const uint8_t* chips, int N, int side, double* out, hi
   return hipGetLastError();
 }
 
-hipError_t arcprep_launch(int f32, const uint8_t* chips, int N, int side, int flip, void* out, hipStream_t s) {
+// mode: 0 f16 x/127.5 - 1, 1 f32 x/127.5 - 1, 2 f16 x - 127.5 (pcgpu.h PC_PREC_*)
+hipError_t arcprep_launch(int mode, const uint8_t* chips, int N, int side, int flip, void* out, hipStream_t s) {
   dim3 grid((side * side + 255) / 256, N);
-  if (f32) hipLaunchKernelGGL(arcface_prep<float>, grid, dim3(256), 0, s, chips, N, side, flip, (float*)out);
+  if (mode == 2) hipLaunchKernelGGL((arcface_prep<f16, true>), grid, dim3(256), 0, s, chips, N, side, flip, (f16*)out);
+  else if (mode == 1) hipLaunchKernelGGL(arcface_prep<float>, grid, dim3(256), 0, s, chips, N, side, flip, (float*)out);
   else hipLaunchKernelGGL(arcface_prep<f16>, grid, dim3(256), 0, s, chips, N, side, flip, (f16*)out);
   return hipGetLastError();
 }

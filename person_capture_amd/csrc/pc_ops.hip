@@ -13,6 +13,7 @@
 // head, 64 queries) with the head's K and V staged in LDS; the 4 waves split the
 // keys, each keeps an online-softmax state per query, and the partial states are
 // merged through LDS (the flash-decoding combine).
+#include <algorithm>
 #include "pc_common.h"
 
 namespace pc {
@@ -318,6 +319,36 @@ hipError_t attention_launch(int f32, const AttnParams& p, int head_dim, hipStrea
   dim3 grid((unsigned)(p.N * p.heads * nqb));
   if (f32) hipLaunchKernelGGL(mha_tokens<float>, grid, dim3(64 * ATT_WAVES), 0, s, p);
   else hipLaunchKernelGGL(mha_tokens<f16>, grid, dim3(64 * ATT_WAVES), 0, s, p);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Largest |x| of the first C channels of npix f16 pixels at pixel stride cs (the hi half of a split
+// / f16c8 tensor): f16c8 scale calibration (pc_net_calibrate). Non-negative floats order like
+// their bit patterns, so the per-wave maxima meet in one unsigned atomicMax.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void absmax_f16(const f16* __restrict__ x, long long npix, int C, int cs,
+                                                  unsigned* __restrict__ out) {
+  const int c8 = C / 8;
+  const long long n = npix * c8;
+  float m = 0.f;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const long long pix = i / c8;
+    const int cq = (int)(i - pix * c8);
+    const f16x8 v = *reinterpret_cast<const f16x8*>(x + pix * cs + cq * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf((float)v[j]));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+}
+
+hipError_t absmax_f16_launch(const void* x, long long npix, int C, int cs, unsigned* out, hipStream_t s) {
+  if (C % 8 || cs % 8 || npix <= 0) return hipErrorInvalidValue;
+  const long long n = npix * (C / 8);
+  const int grid = (int)std::min<long long>(2048, (n + 255) / 256);
+  hipLaunchKernelGGL(absmax_f16, dim3(grid), dim3(256), 0, s, reinterpret_cast<const f16*>(x), npix, C, cs, out);
   return hipGetLastError();
 }
 

@@ -105,10 +105,22 @@ __global__ __launch_bounds__(256) void stem_fused(StemParams p, const f16* __res
       }
       const f16x4 h = f16x4{(f16)o[0], (f16)o[1], (f16)o[2], (f16)o[3]};
       *reinterpret_cast<f16x4*>(my + fr * PITCH + ch * 2) = h;
-      if constexpr (SPLIT)
-        *reinterpret_cast<f16x4*>(my + fr * PITCH + (NPAD + ch) * 2) =
-            f16x4{(f16)(o[0] - (float)h[0]), (f16)(o[1] - (float)h[1]), (f16)(o[2] - (float)h[2]),
-                  (f16)(o[3] - (float)h[3])};
+      if constexpr (SPLIT) {
+        if (p.yc8) {   // f16c8 output: the second half holds [lo8 | hi8] per 32 channels
+          const float hf[4] = {(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+          const float lo[4] = {o[0] - hf[0], o[1] - hf[1], o[2] - hf[2], o[3] - hf[3]};
+          int wl = __builtin_amdgcn_cvt_pk_fp8_f32(f8_sat(lo[0] * p.ylo_mul), f8_sat(lo[1] * p.ylo_mul), 0, false);
+          wl = __builtin_amdgcn_cvt_pk_fp8_f32(f8_sat(lo[2] * p.ylo_mul), f8_sat(lo[3] * p.ylo_mul), wl, true);
+          int wh = __builtin_amdgcn_cvt_pk_fp8_f32(f8_sat(hf[0] * p.yhi_mul), f8_sat(hf[1] * p.yhi_mul), 0, false);
+          wh = __builtin_amdgcn_cvt_pk_fp8_f32(f8_sat(hf[2] * p.yhi_mul), f8_sat(hf[3] * p.yhi_mul), wh, true);
+          *reinterpret_cast<int*>(my + fr * PITCH + NPAD * 2 + f8_lo_byte(ch)) = wl;
+          *reinterpret_cast<int*>(my + fr * PITCH + NPAD * 2 + f8_lo_byte(ch) + kF8Hi) = wh;
+        } else {
+          *reinterpret_cast<f16x4*>(my + fr * PITCH + (NPAD + ch) * 2) =
+              f16x4{(f16)(o[0] - (float)h[0]), (f16)(o[1] - (float)h[1]), (f16)(o[2] - (float)h[2]),
+                    (f16)(o[3] - (float)h[3])};
+        }
+      }
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -8,7 +8,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import models
-from ._lib import PC_PREC_F16, PC_PREC_F16X3, PC_PREC_F32, LetterboxDesc, check, net_precision
+from ._lib import PC_PREC_F16, PC_PREC_F16C8, PC_PREC_F16X3, PC_PREC_F32, LetterboxDesc, check, net_precision
 from .runtime import DeviceBuffer, GpuContext, Net
 
 
@@ -21,12 +21,31 @@ class ArcFaceEngine:
         self.ctx = ctx
         self.depth = depth
         self.precision = precision
-        self.program = models.compile_iresnet(params, depth)
-        self.net = Net(ctx, self.program.serialize(), precision=precision, max_batch=max_batch)
+        # PC_PREC_F16X3 / PC_PREC_F16C8: the split / f16c8 program on an f16 net (f32-class embeddings,
+        # DESIGN.md §3.6-3.7)
+        self.program = models.compile_iresnet(params, depth, split=precision == PC_PREC_F16X3,
+                                              c8=precision == PC_PREC_F16C8)
+        self.net = Net(ctx, self.program.serialize(), precision=net_precision(precision), max_batch=max_batch)
         self.dim = params["fc.weight"].shape[0]
         self.max_batch = max_batch
+        self.absmax = None
+        if precision == PC_PREC_F16C8:
+            self.calibrate(calibration_chips())
         if graph:
             self.net.set_graph(True)
+
+    def calibrate(self, chips_bgr: np.ndarray, headroom_log2: int = 5) -> None:
+        """The f16c8 tensors' e4m3 scales from these chips (flip-TTA rows, as embedded): every
+        activation may then grow 2^headroom_log2 past the calibration's largest before its e4m3
+        bytes saturate (and degrade to f16 precision there, no further)."""
+        chips = np.ascontiguousarray(chips_bgr, dtype=np.uint8)
+        n = min(chips.shape[0], self.max_batch // 2)
+        d = self.ctx.scratch("arc_calib_chips", chips[:n].nbytes)
+        self.ctx.upload(chips[:n], d)
+        x = self.ctx.scratch("arc_calib_input", 2 * n * 112 * 112 * 4 * 2)
+        check(self.ctx.lib.pc_arcface_prep(self.ctx.handle, PC_PREC_F16X3, C.c_void_p(d.ptr), n, 112, 1,
+                                           C.c_void_p(x.ptr)), self.ctx.handle, "arcface_prep")
+        self.absmax = self.net.calibrate(x.ptr, 2 * n, headroom_log2, n_tensors=len(self.program.tensors))
 
     @property
     def flops_per_forward(self) -> float:
@@ -57,6 +76,22 @@ class ArcFaceEngine:
             self.embed_device(d_in.ptr, m, flip, d_out.ptr)
             outs.append(self.ctx.download(d_out.ptr, (m, self.dim), np.float32))
         return np.concatenate(outs, axis=0)
+
+
+def calibration_chips(n: int = 16, seed: int = 20260518) -> np.ndarray:
+    """Synthetic 112x112 chips for the f16c8 scale calibration: u8 noise (the bench's content) and
+    smooth random fields at full contrast (camera-like images)."""
+    rng = np.random.default_rng(seed)
+    noise = rng.integers(0, 256, (n // 2, 112, 112, 3), dtype=np.uint8)
+    f = rng.standard_normal((n - n // 2, 112 + 32, 112 + 32, 3))
+    for ax in (1, 2):   # 17-tap box blur twice along each axis
+        for _ in range(2):
+            c = np.cumsum(f, axis=ax)
+            f = (np.take(c, range(16, c.shape[ax]), axis=ax) - np.take(c, range(0, c.shape[ax] - 16), axis=ax)) / 16.0
+    f = f[:, :112, :112]
+    f = (f - f.mean(axis=(1, 2, 3), keepdims=True)) / (f.std(axis=(1, 2, 3), keepdims=True) + 1e-9)
+    smooth = np.clip(np.rint(127.5 + 60.0 * f), 0, 255).astype(np.uint8)
+    return np.concatenate([noise, smooth], axis=0)
 
 
 class BankMatcher:

@@ -44,7 +44,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import imageops, models, onnx_models
-from ._lib import PC_PREC_F16, PC_PREC_F16X3, PC_PREC_F32, ResizeDesc, WarpDesc, check
+from ._lib import PC_PREC_F16, PC_PREC_F16C8, PC_PREC_F16X3, PC_PREC_F32, ResizeDesc, WarpDesc, check
 from .engines import ArcFaceEngine, ScrfdEngine, opencv_vresize_simd_end
 from .face_yolo import YoloFaceBranch
 from .runtime import GpuContext
@@ -105,6 +105,26 @@ def _det_precision() -> int:
         return PC_PREC_F32
     if v in ("f16x3", "x3", "split"):
         return PC_PREC_F16X3
+    return PC_PREC_F16
+
+
+def _arc_precision() -> int:
+    """ArcFace precision. Default f16c8: f16 hi with e4m3 lo / hi bytes, x_hi*W_hi on
+    the f16 MFMA and x_lo*W_hi + x_hi*W_lo on the block-scaled e4m3 MFMA - embeddings and cosine
+    distances within 1e-4 of the fp32 path (measured ~1e-5), where plain f16 (the reference's TensorRT
+    precision, face_embedder.py:445) moved fd by up to 2.2e-4 on identical chips. f16x3 (the split
+    program, 3 f16 MFMAs per product) is the same class at twice the MFMA issues.
+    PERSON_CAPTURE_AMD_ARC_PRECISION=f16c8 / f16x3 / f16 / f32 select; with
+    PERSON_CAPTURE_AMD_PRECISION=f32 (the parity mode) ArcFace is f32 too."""
+    v = os.getenv("PERSON_CAPTURE_AMD_ARC_PRECISION", "").strip().lower()
+    if not v:
+        return PC_PREC_F32 if _precision() == PC_PREC_F32 else PC_PREC_F16C8
+    if v in ("f32", "fp32", "float32"):
+        return PC_PREC_F32
+    if v in ("f16x3", "x3", "split"):
+        return PC_PREC_F16X3
+    if v in ("f16c8", "c8"):
+        return PC_PREC_F16C8
     return PC_PREC_F16
 
 
@@ -199,6 +219,7 @@ class FaceEmbedder(YoloFaceBranch):
         # detector precision (default: the embedder's): SCRFD f32 + ArcFace f16 gives the f32
         # chips (the f16 landmarks move noise-frame chips, bench.py f16_parity attribution)
         self.det_precision = _det_precision()
+        self.arc_precision = _arc_precision()
         self._ctx = get_context(self._device_index)
         self._scrfd_ctx_id = self._device_index
         seed = int(os.getenv("PERSON_CAPTURE_AMD_SEED", "0"))
@@ -274,7 +295,7 @@ class FaceEmbedder(YoloFaceBranch):
         # native pinned staging ring on a copy stream of their own (pc_frame_stage)
         self._h2d = get_context(self._device_index, "h2d")
         self._stage_threads = int(os.getenv("PERSON_CAPTURE_AMD_STAGE_THREADS", "8"))
-        self._arc = ArcFaceEngine(self._ectx, self._arc_params, self._arc_depth, precision=self.precision,
+        self._arc = ArcFaceEngine(self._ectx, self._arc_params, self._arc_depth, precision=self.arc_precision,
                                   max_batch=self._arc_batch)
         # HIP graphs for small net runs (unchanged callers' per-frame extract(): a SCRFD pass of one
         # frame and an ArcFace pass of its faces are ~60 and ~100 small launches each): runs of at

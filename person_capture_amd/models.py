@@ -113,13 +113,24 @@ def synth_iresnet(depth: int = 100, seed: int = 0, calibrate: bool = True, emb: 
     return p
 
 
-def compile_iresnet(p: Params, depth: int = 100) -> Program:
-    """IResNet -> program. Input: NHWC4 preprocessed chip (RGB, x/127.5-1, channel 3 = 0)."""
-    P = Program()
+def compile_iresnet(p: Params, depth: int = 100, split: bool = False, c8: bool = False) -> Program:
+    """IResNet -> program. Input: NHWC4 preprocessed chip (RGB, x/127.5-1, channel 3 = 0).
+    split: the f16x3 form (program.Program) - every activation and weight hi + lo,
+    f32-class embeddings on the f16 MFMA path. Its input is the centred chip x - 127.5 (exact in
+    f16, where x/127.5 - 1 is not: that one rounding alone moved embeddings by ~2e-4,
+    tools/emu_mixed_iresnet.py), with the 1/127.5 folded into the stem weights; the program
+    flags it (Program.input_centered) and pc_arcface_embed preprocesses accordingly.
+    c8: the f16c8 form (Program(c8=True)): the same f32-class embeddings from half
+    the MFMA issues of split; the last trunk tensor stays split for the FC's split-K kernel."""
+    split = split or c8
+    P = Program(split=split, c8=c8)
     x = P.input_tensor(112, 112, 4)
     # stem: conv1 + bn1 + prelu, folded
     s, b = bn_fold(p, "bn1")
     w = p["conv1.weight"].astype(np.float64) * s[:, None, None, None]
+    if split:
+        P.input_centered = True
+        w = w / 127.5
     w4 = np.zeros((64, 3, 3, 4))
     w4[:, :, :, :3] = np.transpose(w, (0, 2, 3, 1))
     t = P.act(112, 112, 64)
@@ -167,6 +178,7 @@ def compile_iresnet(p: Params, depth: int = 100) -> Program:
     wf = Wfc * s2[None, :, None, None] * sf[:, None, None, None]
     bias = sf * (np.einsum("ochw,c->o", Wfc, b2) + p["fc.bias"].astype(np.float64)) + bf
     e = P.act(1, 1, emb, is_f32=1)
+    P.plain_split(t)
     P.conv(e, [(t, 7, 7, 1, 0, 512)], pack_conv_weights([wf], [512], cpad(emb)), emb,
            bias=pad_vec(bias, cpad(emb)), bias_mode=BIAS_CHANNEL, splitk=16)
     P.outputs = [e]

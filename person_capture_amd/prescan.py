@@ -118,6 +118,7 @@ class SpecRecord:
     state_in: tuple
     state_out: tuple
     faces: list
+    dims: Tuple[int, int] = (0, 0)   # (H, W) of the sample after the pre-scan downscale
 
 
 class PrescanRunner:
@@ -159,6 +160,45 @@ class PrescanRunner:
         im = self._downscale(im, 0)
         res = f.extract_batch([None], dev_frames=[im])
         return res[0], f.policy_state()
+
+    def spec_chunk(self, frame_at, st: "_LoopState", k: int, stop: int):
+        """One speculative chunk from sample position k (at most `batch` positions, < stop) under
+        the current regime and the FaceEmbedder's current policy state: the gate decisions are
+        predicted assuming the last extracted sample's outcome repeats, every predicted extraction
+        runs in ONE extract_batch. Returns (plan [(pos, skip)], regime, policy state before,
+        {pos: faces}, {pos: policy state after}, {pos: (H, W) after the downscale})."""
+        f = self.face
+        samples = self.samples()
+        sim = st.copy()
+        plan = []   # (sample position, skip)
+        for j in range(k, min(stop, k + self.batch)):
+            skip, _ = self._gate(sim)
+            plan.append((j, skip))
+            # regime assumption: the last extracted sample's outcome repeats (faces with a finite
+            # distance keep the fd9 streak at 0, an empty sample grows it; skipped samples grow it)
+            sim.fd9_streak = 0 if (not skip and sim.last_found) else sim.fd9_streak + 1
+        active0 = st.active
+        f._prescan_rr_mode = "full" if active0 else "rr"
+        f.set_prescan_hint(escalate=active0)
+        todo = [j for j, skip in plan if not skip]
+        ims = []
+        for j in todo:
+            im = frame_at(samples[j])
+            if not hasattr(im, "ptr"):
+                im = f._upload(np.ascontiguousarray(im), key=f"prescan_src{j % self.batch}")
+            ims.append(self._downscale(im, j - k))
+        state0 = f.policy_state()
+        f.state_trace = []
+        try:
+            res = f.extract_batch([None] * len(ims), dev_frames=ims) if ims else []
+        finally:
+            trace = f.state_trace
+            f.state_trace = None
+        by_pos = {j: r for j, r in zip(todo, res)}
+        state_after = {todo[t]: s for t, (_, s) in enumerate(trace)}
+        dims = {j: (int(im.H), int(im.W)) for j, im in zip(todo, ims)}
+        self.chunks += 1
+        return plan, active0, state0, by_pos, state_after, dims
 
     def close(self, st: "_LoopState") -> List[Tuple[int, int]]:
         """End of the loop: close an open span at the last frame, then bridge short gaps
@@ -284,35 +324,7 @@ class PrescanRunner:
         st = _LoopState(self.ref_feat)
         k = pos.start
         while k < pos.stop:
-            # ---- predict the next chunk under the current regime ----
-            sim = st.copy()
-            plan = []   # (sample position, skip)
-            for j in range(k, min(pos.stop, k + self.batch)):
-                skip, _ = self._gate(sim)
-                plan.append((j, skip))
-                # regime assumption: the last extracted sample's outcome repeats (faces with a finite
-                # distance keep the fd9 streak at 0, an empty sample grows it; skipped samples grow it)
-                sim.fd9_streak = 0 if (not skip and sim.last_found) else sim.fd9_streak + 1
-            active0 = st.active
-            f._prescan_rr_mode = "full" if active0 else "rr"
-            f.set_prescan_hint(escalate=active0)
-            todo = [j for j, skip in plan if not skip]
-            ims = []
-            for j in todo:
-                im = frame_at(samples[j])
-                if not hasattr(im, "ptr"):
-                    im = f._upload(np.ascontiguousarray(im), key=f"prescan_src{j % self.batch}")
-                ims.append(self._downscale(im, j - k))
-            state0 = f.policy_state()
-            f.state_trace = []
-            try:
-                res = f.extract_batch([None] * len(ims), dev_frames=ims) if ims else []
-            finally:
-                trace = f.state_trace
-                f.state_trace = None
-            by_pos = {j: r for j, r in zip(todo, res)}
-            state_after = {todo[t]: s for t, (_, s) in enumerate(trace)}
-            self.chunks += 1
+            plan, active0, state0, by_pos, state_after, dims = self.spec_chunk(frame_at, st, k, pos.stop)
             # ---- replay; cut at the first divergence ----
             last_state = state0
             cut = None
@@ -326,7 +338,8 @@ class PrescanRunner:
                 self.records.append(rec)
                 if not skip:
                     if speculate:
-                        self.spec.append(SpecRecord(j, active0, last_state, state_after[j], _host_faces(by_pos[j])))
+                        self.spec.append(SpecRecord(j, active0, last_state, state_after[j], _host_faces(by_pos[j]),
+                                                    dims[j]))
                     last_state = state_after[j]
             if cut is not None:
                 self.cuts += 1

@@ -21,14 +21,15 @@ only on the regime and on a small part of the FaceEmbedder's policy state
 
 The result - spans, per-sample records, grown bank and the embedder's final policy state -
 is the single-stream loop's (tests/test_gpu_prescan_shard.py against oracle/prescan.py).
-Speculation misses cost one re-extraction each on rank 0; they occur near shard starts and
-regime changes.
+A speculation miss costs one batched speculative chunk on rank 0 (from the missed sample under
+the true state); misses occur near shard starts and regime changes.
 """
 from __future__ import annotations
 
 import os
+import time
 from dataclasses import dataclass, field
-from typing import Callable, List, Optional, Sequence, Tuple
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -40,8 +41,12 @@ from .shard import shard_bounds
 class MergeStats:
     samples: int = 0
     skipped: int = 0
-    reused: int = 0        # speculative results taken
-    reextracted: int = 0   # extracted again on rank 0 under the true state
+    reused: int = 0        # speculative results of the ranks taken
+    misses: int = 0        # samples whose policy key or regime matched no rank's record
+    rechunks: int = 0      # speculative chunks rank 0 ran for them (one extract_batch each)
+    reextracted: int = 0   # samples extracted on rank 0 in those chunks
+    from_rechunks: int = 0  # samples taken from rank 0's own chunks
+    merge_s: float = 0.0   # wall time of the merge on rank 0 (the serial part of a sharded clip)
     per_rank_spec: List[int] = field(default_factory=list)
 
 
@@ -57,38 +62,68 @@ def sample_dims(runner: PrescanRunner, im) -> Tuple[int, int]:
     return H, W
 
 
+def _pick(f, cands: Sequence[SpecRecord], active: bool, pol: tuple) -> Optional[SpecRecord]:
+    """The first candidate record of a sample that ran in the true regime with the true policy key
+    (its dims were recorded by the rank that extracted it: no frame is fetched for the check)."""
+    for r in cands:
+        if r.active == active:
+            H, W = r.dims
+            if f.prescan_policy_key(r.state_in, r.active, H, W) == f.prescan_policy_key(pol, active, H, W):
+                return r
+    return None
+
+
 def merge(runner: PrescanRunner, frame_at: Callable[[int], object], spec: Sequence[SpecRecord],
           initial_state: tuple):
     """Rank 0: the single-stream loop over all samples, reusing speculative results whose
-    policy key matches. `runner` is rank 0's PrescanRunner (its FaceEmbedder re-extracts
-    misses). Returns (spans, bank, records, MergeStats)."""
+    policy key matches. A sample no rank's record serves (a miss: near shard starts and regime
+    changes, or a whole shard speculated at the other round-robin parity) starts a speculative
+    chunk on rank 0 from that sample under the TRUE regime and policy state - one batched
+    extract_batch of up to `batch` samples (PrescanRunner.spec_chunk), whose records then serve the
+    following samples too - instead of one extraction per missed sample. `runner` is rank 0's
+    PrescanRunner. Returns (spans, bank, records, MergeStats)."""
+    t0 = time.perf_counter()
     f = runner.face
     runner.setup_face()
     samples = runner.samples()
-    by_pos = {r.pos: r for r in spec}
+    cands: Dict[int, List[SpecRecord]] = {}
+    for r in spec:
+        cands.setdefault(r.pos, []).append(r)
     st = _LoopState(runner.ref_feat)
     pol = tuple(initial_state)
     stats = MergeStats(samples=len(samples))
     records: List[SampleRecord] = []
+    own = set()   # ids of the records rank 0 extracted in its own chunks
     for j, idx in enumerate(samples):
         skip, _ = runner._gate(st)
         faces: list = []
         if skip:
             stats.skipped += 1
         else:
-            r = by_pos.get(j)
-            hit = False
-            if r is not None and r.active == st.active:
-                H, W = sample_dims(runner, frame_at(idx))
-                hit = f.prescan_policy_key(r.state_in, r.active, H, W) == f.prescan_policy_key(pol, st.active, H, W)
-            if hit:
-                faces = r.faces
-                pol = f.policy_transfer(r.state_in, r.state_out, pol)
-                stats.reused += 1
+            r = _pick(f, cands.get(j, ()), st.active, pol)
+            if r is None:
+                stats.misses += 1
+                f.set_policy_state(pol)
+                plan, active0, state0, by_pos, state_after, dims = runner.spec_chunk(frame_at, st, j, len(samples))
+                stats.rechunks += 1
+                last, fresh = state0, []
+                for jj, sk in plan:
+                    if not sk:
+                        fresh.append(SpecRecord(jj, active0, last, state_after[jj], _host_faces(by_pos[jj]), dims[jj]))
+                        last = state_after[jj]
+                stats.reextracted += len(fresh)
+                for x in fresh:
+                    own.add(id(x))
+                    cands.setdefault(x.pos, []).insert(0, x)
+                r = _pick(f, cands.get(j, ()), st.active, pol)
+                if r is None:   # the chunk ran sample j from exactly this regime and state
+                    raise RuntimeError(f"pre-scan merge: sample {j} unmatched after re-extraction")
+            faces = r.faces
+            pol = f.policy_transfer(r.state_in, r.state_out, pol)
+            if id(r) in own:
+                stats.from_rechunks += 1
             else:
-                got, pol = runner.extract_one(frame_at, j, st.active, pol)
-                faces = _host_faces(got)
-                stats.reextracted += 1
+                stats.reused += 1
         rec = runner._finish_sample(st, idx, st.processed, faces, not skip)
         st.processed += 1
         records.append(rec)
@@ -97,6 +132,7 @@ def merge(runner: PrescanRunner, frame_at: Callable[[int], object], spec: Sequen
     f.set_prescan_fast(False)
     f.set_prescan_hint(escalate=False)
     runner.final_state = st
+    stats.merge_s = time.perf_counter() - t0
     return spans, st.bank, records, stats
 
 

@@ -11,7 +11,9 @@ Binary format (little-endian int32 words, then float32 data):
   magic 'PCNT', version 1, n_buf, n_tensor, n_array, n_op, n_out, input_tensor
   buffers : n_buf   x [elems_per_image lo, hi, is_f32, 0]
   tensors : n_tensor x [buf, H, W, C, cs, coff, is_f32, split]
-            (split: f16x3 tensor, C physical channels = [hi | lo] halves of C/2)
+            (split bit 0: f16x3 tensor, C physical channels = [hi | lo] halves of C/2, DESIGN.md §3.6;
+             bit 1, input tensor only: centred u8 input x - 127.5, Program.input_centered;
+             bit 2: f16c8 tensor, the second half e4m3 [lo8 | hi8] per 32 channels, Program(c8=True))
   arrays  : n_array x [offset lo, hi, count lo, hi]   (in floats, into data)
   outputs : n_out tensor ids
   ops     : n_op x 32 words (layouts below, mirrored in pc_api.cpp)
@@ -44,8 +46,14 @@ class Program:
     relative). The models compile unchanged: act() allocates the halves and conv()
     expands the weight columns."""
 
-    def __init__(self, split: bool = False) -> None:
-        self.split = bool(split)
+    def __init__(self, split: bool = False, c8: bool = False) -> None:
+        """c8: the f16c8 form - split storage whose second half holds e4m3 bytes
+        [lo8 | hi8] per 32 channels; convs read it as x_hi*W_hi (f16 MFMA) + one block-scaled e4m3
+        MFMA for x_lo*W_hi + x_hi*W_lo. Every split activation of 64-channel blocks is f16c8 unless
+        plain_split() marks it (a tensor read by an op without the f16c8 path)."""
+        self.split = bool(split) or bool(c8)
+        self.c8 = bool(c8)
+        self.tc8: List[int] = []                  # per tensor: 1 = f16c8
         self.vbufs: List[List[int]] = []          # [elems_per_image, is_f32]
         self.tensors: List[List[int]] = []        # [vbuf, H, W, C, cs, coff, is_f32]  (C, cs physical)
         self.tsplit: List[int] = []               # per tensor: 1 = f16x3 split
@@ -53,6 +61,9 @@ class Program:
         self.ops: List[List[int]] = []
         self.outputs: List[int] = []
         self.input: Optional[int] = None
+        # the input holds the centred u8 image (x - 127.5, exact in f16) instead of the model's own
+        # normalisation; the scale is folded into the first op (models.compile_iresnet(split=True))
+        self.input_centered = False
         self.flops_per_image = 0.0
 
     # ---- tensors -------------------------------------------------------
@@ -60,6 +71,7 @@ class Program:
         t = len(self.tensors)
         self.tensors.append([-1, H, W, C, C, 0, 0])
         self.tsplit.append(0)
+        self.tc8.append(0)
         self.input = t
         return t
 
@@ -72,7 +84,12 @@ class Program:
         t = len(self.tensors)
         self.tensors.append([vb, H, W, Cp, Cp, 0, is_f32])
         self.tsplit.append(sp)
+        self.tc8.append(1 if (sp and self.c8 and C % 32 == 0) else 0)
         return t
+
+    def plain_split(self, t: int) -> None:
+        """Keep tensor t in the f16x3 [hi | lo] form in an f16c8 program."""
+        self.tc8[t] = 0
 
     def view(self, t: int, coff: int, C: int) -> int:
         """Channel slice [coff, coff+C) of tensor t (same buffer and pixel stride):
@@ -82,6 +99,7 @@ class Program:
         assert coff + C <= C0
         self.tensors.append([vb, H, W, C, cs, off + coff, f32])
         self.tsplit.append(0)
+        self.tc8.append(0)
         return len(self.tensors) - 1
 
     def dims(self, t: int) -> Tuple[int, int, int]:
@@ -253,7 +271,11 @@ class Program:
                             len(self.outputs), self.input]
         for elems, f32, _ in phys:
             words += [elems & 0xFFFFFFFF, elems >> 32, f32, 0]
-        for (vb, H, W, C, cs, coff, f32), sp in zip(self.tensors, self.tsplit):
+        for i, ((vb, H, W, C, cs, coff, f32), sp, c8) in enumerate(zip(self.tensors, self.tsplit, self.tc8)):
+            if i == self.input and self.input_centered:
+                sp |= 2
+            if c8:
+                sp |= 4
             words += [mapping[vb] if vb >= 0 else -1, H, W, C, cs, coff, f32, sp]
         off = 0
         for a in self.arrays:

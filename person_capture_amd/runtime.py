@@ -3,7 +3,9 @@ and compiled networks. No torch types cross the boundary; device memory is
 owned by the native library (hipMalloc) and addressed by integer pointers."""
 from __future__ import annotations
 
+import atexit
 import ctypes as C
+import weakref
 from typing import Dict, Optional, Tuple
 
 import numpy as np
@@ -88,8 +90,24 @@ class Fence:
             pass
 
 
+# Every live context, closed at interpreter exit before the HIP runtime's own teardown: a native
+# object destroyed from a garbage-collection finaliser after the runtime is gone (or after its
+# context) is what aborted the r04n suite process at exit (teardown order).
+_LIVE_CONTEXTS: "weakref.WeakSet[GpuContext]" = weakref.WeakSet()
+
+
+@atexit.register
+def _close_all_contexts() -> None:
+    for c in list(_LIVE_CONTEXTS):
+        try:
+            c.close()
+        except Exception:
+            pass
+
+
 class GpuContext:
-    """One context per (GPU, consumer): stream, zero page, staging ring."""
+    """One context per (GPU, consumer): stream, zero page, staging ring. Nets created on it are
+    destroyed before it (close() closes them first; pc_net_destroy needs its context)."""
 
     def __init__(self, device_id: int = 0):
         self.lib = _lib.load()
@@ -103,9 +121,13 @@ class GpuContext:
         self._bufs: Dict[str, DeviceBuffer] = {}
         self._pinned: Dict[str, PinnedBuffer] = {}
         self._fences: Dict[str, Fence] = {}
+        self._nets: "weakref.WeakSet[Net]" = weakref.WeakSet()
+        _LIVE_CONTEXTS.add(self)
 
     def close(self) -> None:
         if self.handle:
+            for n in list(self._nets):
+                n.close()
             self._bufs.clear()
             self._pinned.clear()
             self._fences.clear()
@@ -218,6 +240,7 @@ class Net:
         check(ctx.lib.pc_net_create(ctx.handle, buf, len(program), self.precision, self.max_batch, C.byref(h)),
               ctx.handle, "net_create")
         self.handle = h
+        ctx._nets.add(self)
         d = (C.c_int32 * 4)()
         check(ctx.lib.pc_net_input_dims(h, d), ctx.handle, "input_dims")
         self.input_dims = tuple(d)
@@ -232,9 +255,10 @@ class Net:
         return 4 if self.precision == PC_PREC_F32 else 2
 
     def close(self) -> None:
-        if getattr(self, "handle", None):
+        # a closed context has destroyed its nets already (GpuContext.close)
+        if getattr(self, "handle", None) and self.ctx.handle:
             self.ctx.lib.pc_net_destroy(self.handle)
-            self.handle = None
+        self.handle = None
 
     def __del__(self):
         try:
@@ -262,6 +286,14 @@ class Net:
         if max_batch is not None:
             check(self.ctx.lib.pc_net_set_graph_max_batch(self.handle, int(max_batch)), self.ctx.handle,
                   "set_graph_max_batch")
+
+    def calibrate(self, d_input: int, batch: int, headroom_log2: int = 5, n_tensors: int = 0) -> Optional[np.ndarray]:
+        """pc_net_calibrate: the f16c8 tensors' e4m3 scales from one run over `batch` images at
+        d_input. Returns the measured max |x| per tensor when n_tensors is given."""
+        buf = (C.c_float * n_tensors)() if n_tensors else None
+        check(self.ctx.lib.pc_net_calibrate(self.handle, C.c_void_p(int(d_input)), int(batch), int(headroom_log2), buf),
+              self.ctx.handle, "net_calibrate")
+        return np.frombuffer(buf, dtype=np.float32).copy() if n_tensors else None
 
     def profile(self, enable: bool) -> None:
         check(self.ctx.lib.pc_net_profile(self.handle, 1 if enable else 0), self.ctx.handle, "profile")

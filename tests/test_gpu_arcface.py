@@ -4,17 +4,17 @@ Oracle: oracle/nets_torch.iresnet_forward on the unfolded params, fed the
 reference preprocessing (face_embedder.py:1281-1288), combined with the
 reference's flip-TTA sum and L2 normalisation (face_embedder.py:1383-1389,
 restated in oracle/ref_algos.arcface_postprocess, pinned by golden vectors).
-Tolerances: f32 path (PC_PREC_F32) max-abs 1e-4 on unit embeddings and on
-cosine distances (north_star); f16 path (the throughput configuration, like the
-reference's TRT fp16 engines) max-abs 1e-2 on embeddings, 5e-3 on cosine
-distances — measured error is reported in the assertion messages."""
+Tolerances: f32 path (PC_PREC_F32), the f16x3 split path (PC_PREC_F16X3) and the f16c8 path
+(PC_PREC_F16C8, the default of FaceEmbedder) max-abs 1e-4 on unit embeddings and on cosine distances
+(north_star); plain f16 (the reference's TRT fp16 precision) max-abs 1e-2 on embeddings,
+5e-3 on cosine distances — measured error is reported in the assertion messages."""
 import numpy as np
 import pytest
 
 from oracle import nets_torch as nt
 from oracle import ref_algos as ra
 from person_capture_amd import models
-from person_capture_amd._lib import PC_PREC_F16, PC_PREC_F32
+from person_capture_amd._lib import PC_PREC_F16, PC_PREC_F16C8, PC_PREC_F16X3, PC_PREC_F32
 from person_capture_amd.engines import ArcFaceEngine, BankMatcher
 
 pytestmark = pytest.mark.gpu
@@ -31,7 +31,8 @@ def _oracle_embed(p, chips, flip=True):
     return ra.arcface_postprocess(e, ef)
 
 
-@pytest.mark.parametrize("prec,tol_e,tol_fd", [(PC_PREC_F32, 1e-4, 1e-4), (PC_PREC_F16, 1e-2, 5e-3)])
+@pytest.mark.parametrize("prec,tol_e,tol_fd", [(PC_PREC_F32, 1e-4, 1e-4), (PC_PREC_F16X3, 1e-4, 1e-4),
+                                              (PC_PREC_F16C8, 1e-4, 1e-4), (PC_PREC_F16, 1e-2, 5e-3)])
 def test_arcface_embed_parity(gpu_ctx, r100, prec, tol_e, tol_fd):
     rng = np.random.default_rng(11)
     chips = rng.integers(0, 256, size=(6, 112, 112, 3), dtype=np.uint8)
@@ -58,3 +59,52 @@ def test_arcface_no_flip_and_graph(gpu_ctx, r100):
     ref = _oracle_embed(r100, chips, flip=False)
     assert np.abs(a - ref).max() < 1e-4
     assert np.array_equal(a, b)
+
+
+def test_arcface_f16x3_program_and_prep(gpu_ctx, r100):
+    """The f16x3 program: a centred input (x - 127.5 exact in f16, the 1/127.5 in the split stem
+    weights), split-K FC over the split 7x7x512 map; no resident chains (they are f16 only). The
+    centred preprocessing itself is exact: pc_arcface_prep(PC_PREC_F16X3) == chip - 127.5."""
+    import ctypes as C
+    from person_capture_amd._lib import check
+    eng = ArcFaceEngine(gpu_ctx, r100, 100, precision=PC_PREC_F16X3, max_batch=8)
+    assert eng.program.split and eng.program.input_centered
+    assert eng.net.chain_info()[0] == 0
+    rng = np.random.default_rng(13)
+    chips = rng.integers(0, 256, size=(2, 112, 112, 3), dtype=np.uint8)
+    d = gpu_ctx.upload(chips)
+    out = gpu_ctx.alloc(4 * 112 * 112 * 4 * 2)
+    check(gpu_ctx.lib.pc_arcface_prep(gpu_ctx.handle, PC_PREC_F16X3, C.c_void_p(d.ptr), 2, 112, 1,
+                                      C.c_void_p(out.ptr)), gpu_ctx.handle, "arcface_prep")
+    got = gpu_ctx.download(out.ptr, (4, 112, 112, 4), np.float16).astype(np.float32)
+    want = chips[..., ::-1].astype(np.float32) - 127.5
+    assert np.array_equal(got[:2, ..., :3], want) and np.array_equal(got[2:, ..., :3], want[:, :, ::-1])
+    assert not got[..., 3].any()
+
+
+def test_arcface_f16c8_program(gpu_ctx, r100):
+    """The f16c8 program: every trunk activation f16c8 but the FC's input (plain split), calibrated
+    e4m3 scales (finite maxima for every conv output), every conv reading f16c8 on conv_fast's C8
+    tiles (profile code 600 + tile) and no resident chains; 12 chips within 1e-4 of the oracle
+    with and without graph replay."""
+    eng = ArcFaceEngine(gpu_ctx, r100, 100, precision=PC_PREC_F16C8, max_batch=24, graph=True)
+    P = eng.program
+    assert P.input_centered and P.c8 and eng.net.chain_info()[0] == 0
+    c8_convs = [i for i, w in enumerate(P.ops) if w[0] == 1 and P.tc8[w[3]]]
+    assert len(c8_convs) == len([w for w in P.ops if w[0] == 1]) - 1   # all but the FC
+    assert eng.absmax is not None and all(eng.absmax[t] > 0 for t in range(len(P.tc8)) if P.tc8[t])
+    rng = np.random.default_rng(14)
+    chips = rng.integers(0, 256, size=(12, 112, 112, 3), dtype=np.uint8)
+    eng.net.set_graph(False)
+    eng.net.profile(True)
+    a = eng.embed(chips, flip=True)
+    codes = {int(r[0]): int(r[4]) for r in eng.net.profile_ops()}
+    eng.net.profile(False)
+    assert all(600 <= codes[i] < 700 for i in c8_convs), codes
+    eng.net.set_graph(True)
+    b = eng.embed(chips, flip=True)
+    c = eng.embed(chips, flip=True)
+    ref = _oracle_embed(r100, chips, flip=True)
+    err = float(np.abs(a - ref).max())
+    print(f"f16c8 IResNet-100: max |de| {err:.2e}")
+    assert err < 1e-4 and np.array_equal(b, c) and float(np.abs(b - ref).max()) < 1e-4

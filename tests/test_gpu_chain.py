@@ -65,3 +65,31 @@ def test_chain_equals_per_conv_launches(gpu_ctx, depth, batches):
         assert bad.size == 0, f"N={N}: {len(bad)} differing outputs, max |d| {np.abs(a - b).max()}"
     on.close()
     off.close()
+
+
+def test_teardown_after_failed_assertion():
+    """r04n: after this file's chain test failed, the pytest process dumped core at exit - the
+    failed test's nets (never closed) were garbage-collected after the session fixture had closed
+    their context, and pc_net_destroy ran on the destroyed context. Contexts now close their nets
+    first and close themselves at interpreter exit. A child process leaves a net alive past its
+    context's close and another alive at exit after an exception: it must exit with the
+    exception's status, not a signal."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = (
+        "import sys; sys.path.insert(0, %r)\n"
+        "from person_capture_amd import models\n"
+        "from person_capture_amd.runtime import GpuContext, Net\n"
+        "from person_capture_amd._lib import PC_PREC_F16\n"
+        "import numpy as np\n"
+        "P = models.compile_iresnet(models.synth_iresnet(18, seed=1, calibrate=False), 18).serialize()\n"
+        "c1 = GpuContext(0); a = Net(c1, P, PC_PREC_F16, max_batch=2)\n"
+        "d = c1.upload(np.zeros((2, 112, 112, 4), np.float16)); a.run(d.ptr, 2); c1.sync()\n"
+        "c1.close()\n"
+        "del a\n"
+        "c2 = GpuContext(0); b = Net(c2, P, PC_PREC_F16, max_batch=2)\n"
+        "assert False, 'a failed test leaves its net and context alive'\n" % root)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 1, (r.returncode, r.stderr[-2000:])
+    assert "AssertionError" in r.stderr

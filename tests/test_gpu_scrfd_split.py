@@ -127,3 +127,25 @@ def test_split_detections_match_f32(gpu_ctx, s10g, seed):
     dk = np.abs(a_kps[ka] - b_kps[kb]).max()
     print(f"f16x3 vs f32 detections: {int(ka.sum())} faces, max |dbox| {db:.2e} px, max |dkps| {dk:.2e} px")
     assert db < 1e-3 and dk < 1e-3
+
+
+@pytest.mark.parametrize("hx", ["default", "off"])
+def test_split_hx_ran(gpu_ctx, s10g, hx, monkeypatch):
+    """The planner sends the f16x3 64 -> 64 channel 3x3 layers to the halo-staged kernel (profile
+    code 500): at D=640 the 160x160, 80x80 and 40x40 ones (40 is not a multiple of its 16-pixel
+    blocks: partial blocks), and never under PC_CONV_HX=0."""
+    if hx == "off":
+        monkeypatch.setenv("PC_CONV_HX", "0")
+    eng = ScrfdEngine(gpu_ctx, s10g, "10g", D=640, precision=PC_PREC_F16X3, max_batch=1)
+    f = _frame(7)
+    d = gpu_ctx.upload(f)
+    eng.net.profile(True)
+    eng.detect_frames([(d.ptr, f.shape[0], f.shape[1], f.strides[0])], thresh=0.5)
+    recs = eng.net.profile_ops()
+    eng.net.profile(False)
+    hx_ops = [int(r[0]) for r in recs if int(r[4]) == 500]
+    if hx == "off":
+        assert not hx_ops
+        return
+    sizes = {eng.program.tensors[eng.program.ops[o][1]][1] for o in hx_ops}
+    assert {160, 80, 40} <= sizes, sorted(sizes)

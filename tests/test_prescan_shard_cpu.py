@@ -8,7 +8,9 @@ a face only a 90-degree probe finds (so the round-robin phase decides the result
 speculation can miss). Its embeddings depend on the regime (escalation = flip-TTA). The
 sharded run - speculation per shard, gather, rank-0 replay with re-extraction of misses -
 must give the sequential loop's spans, per-sample records, bank and final policy state: in
-process for 1-4 shards, and over a gloo world of 2 processes.
+process for 1-7 shards, and over gloo worlds of 2 and 8 processes (the 8-GPU C5 layout). A miss
+is served by a batched speculative chunk on rank 0 from the true state, whose records serve the
+samples after it as well.
 """
 import os
 import socket
@@ -199,15 +201,37 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_sharded_prescan_gloo_world2():
+@pytest.mark.parametrize("world", [2, 8])
+def test_sharded_prescan_gloo(world):
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    mp.spawn(_worker, args=(2, port, q), nprocs=2, join=True)
-    spans, b, recs, reused, reex, per_rank = q.get(timeout=60)
+    mp.spawn(_worker, args=(world, port, q), nprocs=world, join=True)
+    spans, b, recs, reused, reex, per_rank = q.get(timeout=120)
     seq = _sequential()
     assert spans == seq[0] and recs == seq[2] and np.array_equal(b, seq[1])
-    assert len(per_rank) == 2 and all(n > 0 for n in per_rank) and reused > 0
+    assert len(per_rank) == world and all(n > 0 for n in per_rank) and reused > 0
+
+
+def test_misses_run_as_batched_chunks():
+    """Every miss starts one rank-0 chunk, and a chunk's later records serve later samples: at 7
+    shards of batch 4 the rank-0 chunks extract more samples than there were miss events, and the
+    merge's extract_batch calls number the chunks, not the re-extracted samples."""
+    cfg, bank = _cfg()
+    from person_capture_amd.shard import shard_bounds
+    specs, runners = [], []
+    for rank in range(7):
+        r = PrescanRunner(FakeFace(), cfg, FPS, TOTAL, ref_feat=bank, batch=4)
+        r.run(frame_at, positions=shard_bounds(len(r.samples()), rank, 7), speculate=True)
+        specs.append(list(r.spec))
+        runners.append(r)
+    r0 = runners[0]
+    chunks_before = r0.chunks
+    spans, b, recs, st = merge(r0, frame_at, [x for sp in specs for x in sp], r0.initial_state)
+    _same((spans, b, [vars(x) for x in recs], r0.face.policy_state()), _sequential())
+    assert st.misses > 0 and st.rechunks == st.misses == r0.chunks - chunks_before
+    assert st.reextracted >= st.from_rechunks >= st.misses
+    assert st.reused + st.from_rechunks + st.skipped == st.samples and st.merge_s > 0
