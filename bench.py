@@ -252,8 +252,17 @@ def hbm_kernels(fe, devs, H: int, W: int, reps: int = 20, kinds=("letterbox", "w
     descs = (LetterboxDesc * n)(*[make_letterbox_desc(d.ptr, d.H, d.W, d.stride, D)[0] for d in devs[:n]])
     blob = ctx.scratch("hbm_letterbox", n * D * D * 4 * 2)
     sec = timed(lambda: check(lib.pc_letterbox(h, PC_PREC_F16, descs, n, D, C.c_void_p(blob.ptr)), h, "letterbox"))
+    # the INTER_LINEAR resampler reads two source rows per output row: at 1080p -> 640 (scale 3) 720 of the
+    # 1080 rows, whole (2 of every 3 pixels: every 64-byte line); the blob is written whole (canvas padding
+    # included). r04 counted whole frames (303.9 MB per 32 frames against 237.6 MB of PMC fetch + write).
+    d0 = descs[0]
+    rows = set()
+    for y in range(d0.new_h):
+        sy = int(np.floor((y + 0.5) * d0.scale_y - 0.5))
+        rows.update((min(max(sy, 0), H - 1), min(max(sy + 1, 0), H - 1)))
     out["letterbox_blob"] = entry("letterbox_blob (pc_image.hip)", f"{n} frames {H}x{W} -> {D}x{D}x4 f16",
-                                  n * (H * W * 3 + D * D * 4 * 2), sec, "source frame + blob", "letterbox")
+                                  n * (len(rows) * W * 3 + D * D * 4 * 2), sec,
+                                  f"the {len(rows)} source rows the bilinear taps read + the whole blob", "letterbox")
     # warp_affine_u8: one ArcFace quantum of chips (146 faces) from the 1080p frames, ~100 px faces -> 112x112
     m = 146
     chips = ctx.scratch("hbm_chips", m * 112 * 112 * 3)
@@ -265,8 +274,15 @@ def hbm_kernels(fe, devs, H: int, W: int, reps: int = 20, kinds=("letterbox", "w
         ws.append(imageops.warp_desc(d.ptr, d.stride, W, H, M.reshape(-1), chips.ptr + i * 112 * 112 * 3))
     warr = (WarpDesc * m)(*ws)
     sec = timed(lambda: check(lib.pc_warp_affine(h, warr, m), h, "warp_affine"))
+    # source bytes: the 64-byte lines of the rows each chip's taps touch (scale 1/1.12: a ~101 x 101 px region)
+    Minv = np.linalg.inv(np.vstack([M, [0, 0, 1]]))
+    corners = Minv @ np.array([[0, 111, 0, 111], [0, 0, 111, 111], [1, 1, 1, 1]], np.float64)
+    span_x = corners[0].max() - corners[0].min() + 2
+    span_y = corners[1].max() - corners[1].min() + 2
+    src_bytes = int(np.ceil(span_y)) * int(np.ceil(span_x * 3 / 64.0 + 1)) * 64
     out["warp_affine_u8"] = entry("warp_affine_u8 (pc_image.hip)", f"{m} chips 112x112 from 1080p frames",
-                                  m * 2 * 112 * 112 * 3, sec, "chip written + ~the same source pixels read",
+                                  m * (112 * 112 * 3 + src_bytes), sec,
+                                  "chip written + the 64-byte lines of the source region its taps touch",
                                   "warp_affine")
     # the SCRFD stem max pool (3x3/s2 over the split stem output) inside a 32-frame detection chunk:
     # its HIP-event time from the net profile, bytes from the program's tensors
@@ -451,13 +467,38 @@ def _net_roof(name, p_, steps, fe):
     return r
 
 
-def dominant_conv(nets, names) -> dict:
+def _op_shape(P, op: int) -> str:
+    """'14x14x256 <- 14x14x256 3x3/s1' of conv op `op` of program P (logical channels)."""
+    w = P.ops[op]
+    H, W, C = P.dims(w[1])
+    segs = []
+    for i in range(w[2]):
+        t = w[3 + 5 * i]
+        h, ww, c = P.dims(t)
+        segs.append(f"{h}x{ww}x{c} {w[4 + 5 * i]}x{w[5 + 5 * i]}/s{w[6 + 5 * i]}")
+    return f"{H}x{W}x{C} <- " + " + ".join(segs)
+
+
+def _op_flops(P, op: int) -> float:
+    """Algorithmic FLOPs per image of conv op `op` (the pc_net_create count: true channels)."""
+    w = P.ops[op]
+    H, W, _ = P.dims(w[1])
+    cout = w[27] or w[16]
+    return sum(2.0 * H * W * cout * w[4 + 5 * i] * w[5 + 5 * i] * (w[25 + i] or P.dims(w[3 + 5 * i])[2])
+               for i in range(w[2]))
+
+
+def dominant_conv(nets, names, programs=None) -> dict:
     """The conv kernel instantiation with the largest total HIP-event time over the timed
     region (per-launch records of every profiled net), with its algorithmic FLOPs per launch
-    and average launch duration: the roofline line is this kernel's."""
+    and average launch duration: the roofline line is this kernel's. With the nets' programs,
+    `layers` names every layer that ran on it - shape, launches and rows (images) per launch,
+    FLOPs per launch - so launches x FLOPs per launch reproduce the kernel's FLOPs from the
+    program alone."""
     agg = {}
+    ops = {}
     total = 0.0
-    for n, name in zip(nets, names):
+    for j, (n, name) in enumerate(zip(nets, names)):
         for op, kind, ms, fl, code, cfg in n.profile_ops():
             if fl <= 0:
                 continue
@@ -467,14 +508,35 @@ def dominant_conv(nets, names) -> dict:
             a[1] += ms
             a[2] += fl
             total += ms
+            o = ops.setdefault(k, {}).setdefault((j, int(op)), [0, 0.0, 0.0])
+            o[0] += 1
+            o[1] += fl
+            o[2] += ms
     if not agg:
         return {"kernel": None, "code": None, "launches": 0, "avg_us": None, "flops_per_launch": None,
                 "achieved_tflops": 0.0, "share": None}
     (name, code, cfg), (cnt, ms, fl) = max(agg.items(), key=lambda kv: kv[1][1])
-    return {"kernel": f"{_kernel_of(code, cfg)} in {name}" + (
+    out = {"kernel": f"{_kernel_of(code, cfg)} in {name}" + (
                 " = conv_fast<f16,256,224,128,4,2,2,1> (ArcFace 14x14x256 layers)" if code == 113 else ""),
-            "code": code, "launches": cnt, "avg_us": round(ms * 1e3 / cnt, 2), "flops_per_launch": round(fl / cnt),
-            "achieved_tflops": round(fl / (ms * 1e-3) / 1e12, 2), "share": round(ms / total, 4)}
+           "code": code, "launches": cnt, "avg_us": round(ms * 1e3 / cnt, 2), "flops_per_launch": round(fl / cnt),
+           "achieved_tflops": round(fl / (ms * 1e-3) / 1e12, 2), "share": round(ms / total, 4)}
+    if programs is not None:
+        by_shape = {}
+        for (j, op), (c, f, t) in ops[(name, code, cfg)].items():
+            P = programs[j]
+            if P is None:
+                continue
+            shp = _op_shape(P, op)
+            e = by_shape.setdefault(shp, [0, 0.0, 0.0, set(), _op_flops(P, op)])
+            e[0] += c
+            e[1] += f
+            e[2] += t
+            e[3].add(op)
+        out["layers"] = [{"shape": shp, "ops": len(e[3]), "launches": e[0],
+                          "rows_per_launch": round(e[1] / e[0] / e[4], 2),
+                          "flops_per_launch": round(e[1] / e[0]), "ms": round(e[2], 3)}
+                         for shp, e in sorted(by_shape.items(), key=lambda kv: -kv[1][2])]
+    return out
 
 
 def load_traffic():
@@ -617,7 +679,12 @@ def main():
     _barrier(world)
     elapsed = _max_over_ranks(world, t1 - t0)
     prof = [n.profile_read() for n in nets]
-    dom = dominant_conv(nets, net_names)
+    if fe.detector_backend == "yolo":
+        progs = [getattr(e, "program", None) for e in fe._yf_engines.values()] + [fe._arc.program]
+    else:
+        progs = ([e.program for e in fe._scrfd_engines.values()] if args.frames == "per-frame"
+                 else [fe._engine(640).program]) + [fe._arc.program]
+    dom = dominant_conv(nets, net_names, progs)
     for n in nets:
         n.profile(False)
     if fe.host_times is not None:
@@ -663,6 +730,7 @@ def main():
                      "kernel": dom["kernel"], "kernel_launches": dom["launches"],
                      "kernel_avg_launch_us": dom["avg_us"], "kernel_flops_per_launch": dom["flops_per_launch"],
                      "kernel_share_of_conv_time": dom["share"],
+                     "kernel_layers": dom.get("layers"),
                      "conv_family": {"achieved": round(achieved, 2), "frac": round(achieved / peak, 4),
                                      "traffic_mean_per_launch": traffic},
                      "launches": conv_launches, "avg_launch_us": round(conv_ms * 1e3 / max(1, conv_launches), 2),
@@ -794,7 +862,7 @@ def main_c2(args):
     # per-launch split of one profiled step (HIP events on the net's stream)
     eng.net.profile(True)
     eng.embed_device(d_chips.ptr, B, False, d_out.ptr)
-    dom = dominant_conv([eng.net], ("arcface",))
+    dom = dominant_conv([eng.net], ("arcface",), [eng.program])
     recs = eng.net.profile_ops()
     eng.net.profile(False)
     # f16x3 issues 3 f16 MFMAs per algorithmic product: its roofline is a third of dense f16

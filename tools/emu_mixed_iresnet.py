@@ -7,7 +7,8 @@ read), conv1's operand read of the stream (`in1`: hi only, or hi + lo = one extr
 conv1's weights (`w1`), the intermediate (`y1`), conv2's weights (`w2`), the shortcut weights
 (`wd`); net sites: stem weights / output, FC input / weights. Stages 1-4 = the 56/28/14/7 maps.
 Metric: flip-TTA embeddings vs the fp32 oracle (1-cos, max |component|) and fd against a
-planted bank like bench.plant_bank. usage: python tools/emu_mixed_iresnet.py [n_chips]"""
+planted bank like bench.plant_bank; plus the f16c8 program (emu_c8). usage:
+python tools/emu_mixed_iresnet.py [n_chips] ["variant;variant"]"""
 import sys
 
 sys.dont_write_bytecode = True
@@ -76,6 +77,56 @@ def emu_forward(p, depth, x, split):
     return e
 
 
+def q8(t):
+    """e4m3 (OCP e4m3fn) with one power-of-two scale per tensor putting its max in [224, 448)."""
+    m = t.abs().max().clamp_min(1e-30)
+    e = torch.floor(torch.log2(448.0 / m))
+    return (t * 2 ** e).to(torch.float8_e4m3fn).float() * 2 ** (-e)
+
+
+def emu_c8(p, depth, x):
+    """The f16c8 program: every activation stored as f16 hi + e4m3 lo, every conv
+    x_hi*W_hi (f16 operands, f32 accumulate) + q8(x_lo)*q8(W_hi) + q8(x_hi)*q8(W_lo); exact
+    centred input; FC input kept split (f32 class)."""
+    def conv(t, w, **kw):
+        th = t.half().float()
+        wh = w.half().float()
+        return F.conv2d(th, wh, **kw) + F.conv2d(q8(t - th), q8(wh), **kw) + F.conv2d(q8(th), q8(w - wh), **kw)
+
+    def store(t):
+        h = t.half().float()
+        return h + q8(t - h)
+    T = lambda k: torch.from_numpy(p[k].astype(np.float32))
+    c = lambda a: torch.from_numpy(np.asarray(a, np.float32))[None, :, None, None]
+    W = lambda a: torch.from_numpy(a.astype(np.float32))
+    with torch.no_grad():
+        s, b = bnf(p, "bn1")
+        t = store(F.prelu(F.conv2d(x, W(p["conv1.weight"] * s[:, None, None, None]), padding=1) + c(b),
+                          T("prelu.weight")))
+        for pre, inp, pl, stride, ds in models.iresnet_blocks(depth):
+            s1, b1 = bnf(p, pre + ".bn1")
+            s2, b2 = bnf(p, pre + ".bn2")
+            W1 = p[pre + ".conv1.weight"]
+            ones = torch.ones((1, inp) + tuple(t.shape[2:]))
+            tab = F.conv2d(ones * c(b1), W(W1), padding=1) * c(s2) + c(b2)
+            y1 = store(F.prelu(conv(t, W(W1 * s1[None, :, None, None] * s2[:, None, None, None]), padding=1) + tab,
+                               T(pre + ".prelu.weight")))
+            s3, b3 = bnf(p, pre + ".bn3")
+            o = conv(y1, W(p[pre + ".conv2.weight"] * s3[:, None, None, None]), stride=stride, padding=1) + c(b3)
+            if ds:
+                sd, bd = bnf(p, pre + ".downsample.1")
+                o = o + conv(t, W(p[pre + ".downsample.0.weight"] * sd[:, None, None, None]), stride=stride) + c(bd)
+            else:
+                o = o + t
+            t = store(o)
+        s2, b2 = bnf(p, "bn2")
+        sf, bf = bnf(p, "features")
+        Wfc = p["fc.weight"].reshape(-1, 512, 7, 7)
+        wf = Wfc * s2[None, :, None, None] * sf[:, None, None, None]
+        bias = sf * (np.einsum("ochw,c->o", Wfc, b2) + p["fc.bias"]) + bf
+        return F.conv2d(t, W(wf)).flatten(1) + torch.from_numpy(bias.astype(np.float32))
+
+
 def tta(fwd, chips):
     x = arcface_input_from_chips(chips)
     e = fwd(x) + fwd(torch.flip(x, dims=[3]))
@@ -138,10 +189,12 @@ def main():
     bank = np.array(bank, np.float32)
     fd = lambda e: (1.0 - e @ bank.T).min(1)
     fd_ref = fd(ref)
-    for name, fn in VARIANTS.items():
+    runs = [(k, (lambda x, fn=fn: emu_forward(p, depth, x, fn))) for k, fn in VARIANTS.items()]
+    runs.append(("f16c8 (e4m3 corrections, lo stored e4m3)", lambda x: emu_c8(p, depth, x)))
+    for name, fwd in runs:
         if only and not any(o == name for o in only):
             continue
-        e = tta(lambda x: emu_forward(p, depth, x, fn), chips)
+        e = tta(fwd, chips)
         d = np.abs(fd(e) - fd_ref)
         nd = np.linalg.norm(e.astype(np.float64) - ref, axis=1)
         print(f"{name:34s}: |dfd| med {np.median(d):.2e} max {d.max():.2e}; |de|max "
