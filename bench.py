@@ -539,6 +539,25 @@ def dominant_conv(nets, names, programs=None) -> dict:
     return out
 
 
+# conv_fast tile table (pc_conv_fast.hip kFastCfgs): cfg -> (channel tile, pixel tile)
+FAST_TILES = {0: (256, 256), 1: (128, 256), 2: (256, 128), 3: (128, 128), 4: (64, 256), 5: (96, 256), 6: (64, 512),
+              7: (32, 256), 8: (224, 128), 9: (128, 512), 10: (128, 256), 11: (96, 384), 12: (32, 256),
+              13: (256, 224), 14: (128, 224), 15: (64, 64), 16: (64, 128), 17: (128, 64), 18: (32, 64), 19: (96, 64),
+              20: (224, 64), 21: (96, 128)}
+
+
+def _traffic_for(dominant, code):
+    """HBM bytes per launch of the rocprofv3 dominant kernel when it is the bench's dominant conv_fast
+    tile (same channel x pixel tile; the f16c8 form carries C8 = true as its last template flag)."""
+    if not dominant or code is None or not (100 <= code < 200 or 600 <= code < 700):
+        return None
+    bc, bp = FAST_TILES.get(code % 100, (0, 0))
+    name = dominant.get("kernel", "")
+    if f"Li{bc}ELi{bp}E" not in name or name.endswith("Lb1EEEvNS_10ConvParamsE") != (code >= 600):
+        return None
+    return dominant.get("hbm_bytes_per_launch")
+
+
 def load_traffic():
     """HBM bytes per conv launch from the round's rocprofv3 FETCH_SIZE / WRITE_SIZE passes
     (tools/pmc_traffic.py writes bench_traffic.json at the repo root, next to this file, so
@@ -726,7 +745,7 @@ def main():
                    "parallelism": f"frame-shard x{world} (no collective)"},
         "roofline": {"bound": "mfma", "achieved": dom["achieved_tflops"], "peak": peak, "unit": "TFLOP/s",
                      "frac": round(dom["achieved_tflops"] / peak, 4),
-                     "traffic": (dominant or {}).get("hbm_bytes_per_launch") if dom["code"] == 113 else None,
+                     "traffic": _traffic_for(dominant, dom["code"]),
                      "kernel": dom["kernel"], "kernel_launches": dom["launches"],
                      "kernel_avg_launch_us": dom["avg_us"], "kernel_flops_per_launch": dom["flops_per_launch"],
                      "kernel_share_of_conv_time": dom["share"],

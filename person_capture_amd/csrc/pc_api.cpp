@@ -667,6 +667,13 @@ static unsigned tensor_zero_off(const pc_net* n, int t) {
 
 static const int kNumConvCfgs = 14;   // pc_conv.hip launch_rowb
 
+// K-row width of every f16c8 conv plan (64: a 32-channel K tile and a half-zero block-scaled MFMA;
+// 128: 64 channels and a full one)
+static int c8_rowb() {
+  const char* e = getenv("PC_C8_ROWB");
+  return e && atoi(e) == 128 ? 128 : 64;
+}
+
 static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_batch, bool small = false) {
   const int* w = op.w;
   const int out = w[1], nseg = w[2], npad = w[14];
@@ -818,9 +825,10 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
           if (npad % bc || (force > 0 && k != force - 1)) continue;
           if (k >= kFastSmallCfg0 && k <= kFastSmallCfg1 && (!small || no_small_tiles) && force <= 0) continue;
           for (int rb : {rowb, 64}) {
-            // f16c8 inputs: tiles with the LDS epilogue (PC_C8_ROWB pins the K row width: tuning)
-            if (in_c8 && (!conv_fast_valid_c8(k, rb) ||
-                          (getenv("PC_C8_ROWB") && atoi(getenv("PC_C8_ROWB")) != rb))) continue;
+            // f16c8 inputs: tiles with the LDS epilogue, at ONE K-row width for every plan of the
+            // net (kC8Rowb; PC_C8_ROWB for tuning): the row width orders the f16 and block-scaled
+            // MFMAs of a K tile, so a conv's output would otherwise depend on its batch class
+            if (in_c8 && (!conv_fast_valid_c8(k, rb) || rb != c8_rowb())) continue;
             if (!conv_fast_valid_sx(k, rb)) continue;
             const long long t = (M + bp - 1) / bp * (npad / bc);
             const double est = (double)((t + 255) / 256) * bc * bp * cost[k];

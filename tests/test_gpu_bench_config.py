@@ -284,10 +284,12 @@ def test_c3_plain_f16_detector_mismatches(gpu_ctx, monkeypatch, c3_frames, c3_or
     # (max_fd_diff is not bounded here: a shifted box pairs the nearest other face, measured 0.26)
 
 
-@pytest.mark.parametrize("prec,tol", [(PC_PREC_F32, 1e-4), (PC_PREC_F16X3, 1e-4), (PC_PREC_F16C8, 1e-4),
-                                      (PC_PREC_F16, 1e-2)])
+# measured r05 (gpurun_out/parity/c2_prec*.json): f32 6.7e-7, f16x3 2.7e-6, f16c8 1.5e-5, f16 5.4e-4
+@pytest.mark.parametrize("prec,tol", [(PC_PREC_F32, 1e-5), (PC_PREC_F16X3, 1e-5), (PC_PREC_F16C8, 5e-5),
+                                      (PC_PREC_F16, 1e-3)])
 def test_c2_arcface_batch256(gpu_ctx, prec, tol):
-    """BASELINE C2: 256 chips -> 512 rows with flip in one ArcFaceEngine(max_batch=512) launch."""
+    """BASELINE C2: 256 chips -> 512 rows with flip in one ArcFaceEngine(max_batch=512) launch,
+    max |embedding - oracle| on 32 chips, bounded ~2-3x above the measured error of each mode."""
     p = models.synth_iresnet(100, seed=0)
     chips = np.random.default_rng(256).integers(0, 256, (256, 112, 112, 3), dtype=np.uint8)
     eng = ArcFaceEngine(gpu_ctx, p, 100, precision=prec, max_batch=512)

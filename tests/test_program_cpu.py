@@ -87,3 +87,35 @@ def test_scrfd_split_program_is_f32_class(variant):
         worst = max(worst, np.abs(got - r).max() / max(1.0, np.abs(r).max()))
     # (the plain program in fp32 emulation, i.e. only the folding algebra, is at ~3e-6 here)
     assert worst < 1e-5, worst
+
+
+@pytest.mark.parametrize("mode", ["split", "c8"])
+def test_iresnet_f32_class_program_flags(r18, mode):
+    """The f16x3 / f16c8 IResNet programs: centred input (split-word bit 1 of the
+    input tensor), 1/127.5 folded into the stem weights, every trunk activation split - f16c8
+    (bit 2) in the c8 form except the FC's input, which stays [hi | lo] for split-K - and the
+    split weight columns [W_hi, W_hi, W_lo] that reproduce the f32 weights to f32 precision."""
+    P = models.compile_iresnet(r18, 18, split=mode == "split", c8=mode == "c8")
+    assert P.input_centered and P.split and P.c8 == (mode == "c8")
+    fc = P.ops[-1]
+    assert fc[24] > 1 and not P.tc8[fc[3]] and P.tsplit[fc[3]]
+    convs = [w for w in P.ops if w[0] == 1]
+    assert all(P.tsplit[w[3]] for w in convs)
+    if mode == "c8":
+        assert all(P.tc8[w[3]] for w in convs[:-1])
+    plain = models.compile_iresnet(r18, 18)
+    st, st0 = P.ops[0], plain.ops[0]
+    assert np.allclose(P.arrays[st[7]] * 127.5, plain.arrays[st0[7]], rtol=1e-6, atol=1e-9)
+    # serialized split words: input bit 1, f16c8 bit 2
+    blob = P.serialize()
+    head = np.frombuffer(blob[:32], dtype="<i4")
+    nbuf, nten = head[2], head[3]
+    words = np.frombuffer(blob[32 + nbuf * 16: 32 + nbuf * 16 + nten * 32], dtype="<i4").reshape(nten, 8)
+    assert words[P.input, 7] & 2
+    assert all(bool(words[t, 7] & 4) == bool(P.tc8[t]) for t in range(nten))
+    # split weight columns sum back to the plain program's weights (f32 products of f16 halves)
+    w1 = convs[0]   # layer1.0.conv1: one 3x3 segment
+    a, b = P.arrays[w1[13]].reshape(w1[14], -1), plain.arrays[plain.ops[1][13]].reshape(w1[14], -1)
+    cp = P.dims(w1[3])[2]
+    taps = a.reshape(w1[14], 9, 3, cp)
+    assert np.allclose(taps[:, :, 0] + taps[:, :, 2], b.reshape(w1[14], 9, cp), rtol=0, atol=1e-7)
