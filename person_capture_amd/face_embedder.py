@@ -109,16 +109,17 @@ def _det_precision() -> int:
 
 
 def _arc_precision() -> int:
-    """ArcFace precision. Default f16c8: f16 hi with e4m3 lo / hi bytes, x_hi*W_hi on
-    the f16 MFMA and x_lo*W_hi + x_hi*W_lo on the block-scaled e4m3 MFMA - embeddings and cosine
-    distances within 1e-4 of the fp32 path (measured ~1e-5), where plain f16 (the reference's TensorRT
-    precision, face_embedder.py:445) moved fd by up to 2.2e-4 on identical chips. f16x3 (the split
-    program, 3 f16 MFMAs per product) is the same class at twice the MFMA issues.
-    PERSON_CAPTURE_AMD_ARC_PRECISION=f16c8 / f16x3 / f16 / f32 select; with
+    """ArcFace precision. Default f16x3: the split IResNet program (every activation
+    and weight f16 hi + f16 lo, 3 f16 MFMAs per product, exact centred input) - embeddings within
+    2.7e-6 and cosine distances within 1e-4 of the fp32 path, where plain f16 (the reference's
+    TensorRT precision, face_embedder.py:445) moved fd by up to 2.2e-4 on identical chips. f16c8 (e4m3
+    lo / hi bytes, the corrections on the block-scaled e4m3 MFMA: half the MFMA issues, 1.5e-5) ran
+    no faster on the same staging-bound tiles (r05d: C2 22.5 vs 22.3 ms) and is opt-in.
+    PERSON_CAPTURE_AMD_ARC_PRECISION=f16x3 / f16c8 / f16 / f32 select; with
     PERSON_CAPTURE_AMD_PRECISION=f32 (the parity mode) ArcFace is f32 too."""
     v = os.getenv("PERSON_CAPTURE_AMD_ARC_PRECISION", "").strip().lower()
     if not v:
-        return PC_PREC_F32 if _precision() == PC_PREC_F32 else PC_PREC_F16C8
+        return PC_PREC_F32 if _precision() == PC_PREC_F32 else PC_PREC_F16X3
     if v in ("f32", "fp32", "float32"):
         return PC_PREC_F32
     if v in ("f16x3", "x3", "split"):

@@ -205,15 +205,16 @@ def test_c3_detector_f32_mode_decisions(gpu_ctx, monkeypatch, c3_frames, c3_orac
 
 
 def test_c3_timed_mode_decisions(gpu_ctx, monkeypatch, c3_frames, c3_oracle):
-    """The timed mode (bench.py C3: f16x3 SCRFD + f16 ArcFace) vs the fp32 oracle, counted as the
+    """The timed mode (bench.py C3: f16x3 SCRFD + f16x3 ArcFace) vs the fp32 oracle, counted as the
     bench's parity block counts (nearest box): identical face counts and boxes, no accept flip at
     0.32 or 0.45 outside a 1e-3 band of the threshold (a face within the band flips under any
     path that is not bitwise the oracle's: the f32 device mode's own chips differ from the
     oracle's by up to 7e-4 in fd), at most 1 % of the faces flipping inside it."""
     ores, bank = c3_oracle
     monkeypatch.delenv("PERSON_CAPTURE_AMD_DET_PRECISION", raising=False)
+    monkeypatch.delenv("PERSON_CAPTURE_AMD_ARC_PRECISION", raising=False)
     fe, got = _run_bench_config(monkeypatch, c3_frames, bank, "f16")
-    assert fe.det_precision == 2   # PC_PREC_F16X3, the default
+    assert fe.det_precision == 2 and fe.arc_precision == 2   # PC_PREC_F16X3, the defaults
     report = _vs_oracle(got, ores)
     print("C3 timed mode (f16x3 SCRFD) vs fp32 oracle: " + json.dumps(report))
     _persist("c3_timed", report)
