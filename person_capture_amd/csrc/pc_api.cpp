@@ -819,6 +819,15 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
       if (try_sx) {   // the same choice among the tiles that can stage fused split tiles
         int bsx = -1, bsx_rowb = rowb;
         double bsx_t = 0;
+        // fused tiles walk K channel-block-major (each block through every tap, pc_conv_fast.hip
+        // advance), so the K-row width orders the accumulation: ONE width per conv for every
+        // plan class - the input's width when a full-batch tile runs at it, 64 bytes otherwise
+        int sx_rb = 64;
+        for (int k = 0; k < conv_fast_num_cfgs() && sx_rb != rowb; ++k) {
+          int bc = 0, bp = 0;
+          conv_fast_tile(k, &bc, &bp);
+          if (!(k >= kFastSmallCfg0 && k <= kFastSmallCfg1) && npad % bc == 0 && conv_fast_valid_sx(k, rowb)) sx_rb = rowb;
+        }
         for (int k = 0; k < conv_fast_num_cfgs(); ++k) {
           int bc = 0, bp = 0;
           conv_fast_tile(k, &bc, &bp);
@@ -829,6 +838,7 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
             // net (kC8Rowb; PC_C8_ROWB for tuning): the row width orders the f16 and block-scaled
             // MFMAs of a K tile, so a conv's output would otherwise depend on its batch class
             if (in_c8 && (!conv_fast_valid_c8(k, rb) || rb != c8_rowb())) continue;
+            if (!in_c8 && rb != sx_rb && force <= 0) continue;
             if (!conv_fast_valid_sx(k, rb)) continue;
             const long long t = (M + bp - 1) / bp * (npad / bc);
             const double est = (double)((t + 255) / 256) * bc * bp * cost[k];

@@ -134,6 +134,8 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
   load_seg(p.seg[0]);
   int iseg = 0, ith = 0, itw = 0, icb = 0;
   const int seg0_kh = p.seg[0].KH;
+  const int seg0_cb = p.seg[0].cblk;
+  int sKH = p.seg[0].KH;
   // SX: weight K byte base of the current segment (segment 1 starts after segment 0's
   // KH*KW taps of 3 x cblk virtual blocks)
   int swk = 0;
@@ -178,21 +180,43 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
       });
     });
   };
-  // advance the issue iterator by one K-tile (no-op once the last tile was issued)
+  // advance the issue iterator by one K-tile (no-op once the last tile was issued).
+  // Plain tiles walk K tap-major (channel block fastest: the K order the chain / t2d kernels share
+  // bit for bit). Fused split tiles walk it channel-block-major (the 9 taps of one [hi | lo] block,
+  // then the next block): a tap-major pass re-reads the tile's whole split pixel rows per tap, which
+  // at 256x224 and 512 split channels (229 KB per workgroup, 7 MB per XCD) no longer fits the L2 -
+  // every tap went back to HBM (r05 profile: 650 MB fetched per 14x14x256 launch, 2.8x the tensor)
   auto advance = [&](bool more) __attribute__((always_inline)) {
     if (!more) return;
-    const int cb1 = icb + 1;
-    const bool w1 = cb1 == scblk;
-    icb = w1 ? 0 : cb1;
-    const int tw1 = itw + (w1 ? 1 : 0);
-    const bool w2 = tw1 == sKW;
-    itw = w2 ? 0 : tw1;
-    ith += w2 ? 1 : 0;
-    if (iseg == 0 && ith == seg0_kh) {   // once per launch, 2-segment convs only
-      iseg = 1;
-      ith = 0;
-      swk = swk1;
-      load_seg(p.seg[1]);
+    if constexpr (SX) {
+      const int tw1 = itw + 1;
+      const bool w1 = tw1 == sKW;
+      itw = w1 ? 0 : tw1;
+      const int th1 = ith + (w1 ? 1 : 0);
+      const bool w2 = th1 == sKH;
+      ith = w2 ? 0 : th1;
+      icb += w2 ? 1 : 0;
+      if (iseg == 0 && icb == seg0_cb) {   // once per launch, 2-segment convs only
+        iseg = 1;
+        icb = 0;
+        swk = swk1;
+        sKH = p.seg[1].KH;
+        load_seg(p.seg[1]);
+      }
+    } else {
+      const int cb1 = icb + 1;
+      const bool w1 = cb1 == scblk;
+      icb = w1 ? 0 : cb1;
+      const int tw1 = itw + (w1 ? 1 : 0);
+      const bool w2 = tw1 == sKW;
+      itw = w2 ? 0 : tw1;
+      ith += w2 ? 1 : 0;
+      if (iseg == 0 && ith == seg0_kh) {   // once per launch, 2-segment convs only
+        iseg = 1;
+        ith = 0;
+        swk = swk1;
+        load_seg(p.seg[1]);
+      }
     }
   };
 

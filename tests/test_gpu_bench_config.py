@@ -219,9 +219,10 @@ def test_c3_timed_mode_decisions(gpu_ctx, monkeypatch, c3_frames, c3_oracle):
     print("C3 timed mode (f16x3 SCRFD) vs fp32 oracle: " + json.dumps(report))
     _persist("c3_timed", report)
     assert report["face_count_mismatch"] == 0 and report["box_mismatch"] == 0
-    assert report["accept_mismatch_outside_0.001_band"] == 0
-    assert report["accept_mismatch_0.32"] + report["accept_mismatch_0.45"] <= max(1, report["faces"] // 100)
-    assert report["max_fd_diff"] < 2e-3
+    # r05 (f16x3 ArcFace, gpurun_out/parity/c3_timed.json): no accept flip at either threshold; max |dfd|
+    # 1.02e-3, all of it the noise chips' few differing pixels (the device f32 mode: 6.6e-4)
+    assert report["accept_mismatch_0.32"] == 0 and report["accept_mismatch_0.45"] == 0
+    assert report["max_fd_diff"] < 1.5e-3
 
 
 SMOOTH_N = 8
@@ -250,8 +251,8 @@ def test_c3_smooth_frames_timed_mode(gpu_ctx, monkeypatch, smooth_c3):
     (face_embedder.py:2214-2239) on the other side of it, which any path not bitwise the oracle's can
     meet (the f16x3 boxes are within 1e-3 px of the f32 path's, test_gpu_scrfd_split.py) - and such a
     face's keypoints then sit one pixel over in crop coordinates, so its chip's border reflection
-    differs; faces with equal boxes keep fd within 1e-3 and no accept decision flips outside the 1e-3
-    band (r04's smooth-frame report had one such box, no test)."""
+    differs; faces with equal boxes keep fd within 3e-4 and no accept decision flips (r04's smooth-frame
+    report had one such box against the device f32 mode, and no test)."""
     sm, ores, bank = smooth_c3
     monkeypatch.delenv("PERSON_CAPTURE_AMD_DET_PRECISION", raising=False)
     monkeypatch.delenv("PERSON_CAPTURE_AMD_ARC_PRECISION", raising=False)
@@ -263,8 +264,9 @@ def test_c3_smooth_frames_timed_mode(gpu_ctx, monkeypatch, smooth_c3):
     assert report["face_count_mismatch"] == 0
     assert report["box_mismatch"] == report.get("box_mismatch_int_boundary", 0)
     assert report.get("box_mismatch_int_margin_px", 0.0) < 2e-3
-    assert report["accept_mismatch_outside_0.001_band"] == 0
-    assert report["max_fd_diff_same_box"] < 1e-3
+    assert report["accept_mismatch_0.32"] == 0 and report["accept_mismatch_0.45"] == 0
+    # r05: 42 faces, max |dfd| 1.08e-4 (smooth chips barely change under last-bit landmark shifts)
+    assert report["max_fd_diff_same_box"] < 3e-4
 
 
 def test_c3_plain_f16_detector_mismatches(gpu_ctx, monkeypatch, c3_frames, c3_oracle):
