@@ -458,11 +458,12 @@ def _kernel_of(code: float, cfg: float) -> str:
 
 
 def _net_roof(name, p_, steps, fe):
-    """C3 per-net conv time and algorithmic TF/s; the f16x3 SCRFD also with the MFMA work it
-    issues (3 MFMAs per product)."""
+    """C3 per-net conv time and algorithmic TF/s; the f16x3 nets also with the MFMA work they
+    issue (3 MFMAs per product)."""
     tf = p_["conv_flops"] / (p_["conv_ms"] * 1e-3) / 1e12 if p_["conv_ms"] > 0 else None
     r = {"conv_ms_per_step": round(p_["conv_ms"] / steps, 3), "tflops": round(tf, 1) if tf else None}
-    if name.startswith("scrfd") and getattr(fe, "det_precision", None) == 2 and tf:   # PC_PREC_F16X3
+    prec = getattr(fe, "arc_precision", None) if name == "arcface" else getattr(fe, "det_precision", None)
+    if prec == 2 and tf:   # PC_PREC_F16X3
         r.update(dtype="f16x3", mfma_tflops=round(3 * tf, 1), mfma_frac=round(3 * tf / PEAK_F16_TFLOPS, 4))
     return r
 
@@ -488,7 +489,20 @@ def _op_flops(P, op: int) -> float:
                for i in range(w[2]))
 
 
-def dominant_conv(nets, names, programs=None) -> dict:
+def _prec_name(prec) -> str:
+    from person_capture_amd._lib import PC_PREC_F16C8, PC_PREC_F16X3, PC_PREC_F32
+    return {PC_PREC_F32: "f32", PC_PREC_F16X3: "f16x3", PC_PREC_F16C8: "f16c8"}.get(prec, "f16")
+
+
+def _peak_for(prec_name: str) -> float:
+    """Dense MFMA roofline of a conv kernel in algorithmic FLOPs: f16x3 issues 3 f16 MFMAs per
+    product (a third of dense f16); f16c8 2 f16 + 1 block-scaled e4m3 MFMA per 64-channel K tile
+    where f16 takes 2 (x 2/3, at the e4m3 instruction's measured equal issue time)."""
+    return {"f16": PEAK_F16_TFLOPS, "f16x3": PEAK_F16_TFLOPS / 3,
+            "f16c8": PEAK_F16_TFLOPS * 2 / 3}.get(prec_name, PEAK_F32_TFLOPS)
+
+
+def dominant_conv(nets, names, programs=None, precisions=None) -> dict:
     """The conv kernel instantiation with the largest total HIP-event time over the timed
     region (per-launch records of every profiled net), with its algorithmic FLOPs per launch
     and average launch duration: the roofline line is this kernel's. With the nets' programs,
@@ -516,8 +530,13 @@ def dominant_conv(nets, names, programs=None) -> dict:
         return {"kernel": None, "code": None, "launches": 0, "avg_us": None, "flops_per_launch": None,
                 "achieved_tflops": 0.0, "share": None}
     (name, code, cfg), (cnt, ms, fl) = max(agg.items(), key=lambda kv: kv[1][1])
-    out = {"kernel": f"{_kernel_of(code, cfg)} in {name}" + (
-                " = conv_fast<f16,256,224,128,4,2,2,1> (ArcFace 14x14x256 layers)" if code == 113 else ""),
+    prec = (precisions or {}).get(name, "f16")
+    label = ""
+    if code == 113:
+        label = (" = conv_fast<f16,256,224,64,4,2,2,1,SPLIT,SX> (fused f16x3 split tile, 64-byte K rows; "
+                 "ArcFace 14x14x256 layers)" if prec == "f16x3" else
+                 " = conv_fast<f16,256,224,128,4,2,2,1> (ArcFace 14x14x256 layers)" if prec == "f16" else "")
+    out = {"kernel": f"{_kernel_of(code, cfg)} in {name}" + label, "precision": prec, "peak_tflops": _peak_for(prec),
            "code": code, "launches": cnt, "avg_us": round(ms * 1e3 / cnt, 2), "flops_per_launch": round(fl / cnt),
            "achieved_tflops": round(fl / (ms * 1e-3) / 1e12, 2), "share": round(ms / total, 4)}
     if programs is not None:
@@ -546,14 +565,16 @@ FAST_TILES = {0: (256, 256), 1: (128, 256), 2: (256, 128), 3: (128, 128), 4: (64
               20: (224, 64), 21: (96, 128)}
 
 
-def _traffic_for(dominant, code):
+def _traffic_for(dominant, code, prec="f16"):
     """HBM bytes per launch of the rocprofv3 dominant kernel when it is the bench's dominant conv_fast
-    tile (same channel x pixel tile; the f16c8 form carries C8 = true as its last template flag)."""
+    tile: same channel x pixel tile and the same form - the template's last three flags (SPLIT, SX,
+    C8) are false for f16, SX for the fused f16x3 tiles, all three for f16c8."""
     if not dominant or code is None or not (100 <= code < 200 or 600 <= code < 700):
         return None
     bc, bp = FAST_TILES.get(code % 100, (0, 0))
     name = dominant.get("kernel", "")
-    if f"Li{bc}ELi{bp}E" not in name or name.endswith("Lb1EEEvNS_10ConvParamsE") != (code >= 600):
+    flags = "Lb1ELb1ELb1E" if code >= 600 else "Lb1ELb1ELb0E" if prec == "f16x3" else "ELb0ELb0E"
+    if f"Li{bc}ELi{bp}E" not in name or not name.endswith(flags + "EEvNS_10ConvParamsE"):
         return None
     return dominant.get("hbm_bytes_per_launch")
 
@@ -703,7 +724,8 @@ def main():
     else:
         progs = ([e.program for e in fe._scrfd_engines.values()] if args.frames == "per-frame"
                  else [fe._engine(640).program]) + [fe._arc.program]
-    dom = dominant_conv(nets, net_names, progs)
+    precs = {name: _prec_name(fe.arc_precision if name == "arcface" else fe.det_precision) for name in net_names}
+    dom = dominant_conv(nets, net_names, progs, precs)
     for n in nets:
         n.profile(False)
     if fe.host_times is not None:
@@ -715,7 +737,7 @@ def main():
     total_frames = _sum_over_ranks(world, args.batch * args.steps)
     value = total_frames / elapsed
     achieved = conv_flops / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
-    peak = PEAK_F16_TFLOPS if args.precision == "f16" else PEAK_F32_TFLOPS
+    peak = dom.get("peak_tflops") or (PEAK_F16_TFLOPS if args.precision == "f16" else PEAK_F32_TFLOPS)
     traffic, dominant = load_traffic()
     out = {
         "metric": "frames/sec detect+embed+match @1080p, 1/2/4/8 GPU; MFMA util %",
@@ -745,7 +767,7 @@ def main():
                    "parallelism": f"frame-shard x{world} (no collective)"},
         "roofline": {"bound": "mfma", "achieved": dom["achieved_tflops"], "peak": peak, "unit": "TFLOP/s",
                      "frac": round(dom["achieved_tflops"] / peak, 4),
-                     "traffic": _traffic_for(dominant, dom["code"]),
+                     "traffic": _traffic_for(dominant, dom["code"], dom.get("precision", "f16")),
                      "kernel": dom["kernel"], "kernel_launches": dom["launches"],
                      "kernel_avg_launch_us": dom["avg_us"], "kernel_flops_per_launch": dom["flops_per_launch"],
                      "kernel_share_of_conv_time": dom["share"],
@@ -881,14 +903,13 @@ def main_c2(args):
     # per-launch split of one profiled step (HIP events on the net's stream)
     eng.net.profile(True)
     eng.embed_device(d_chips.ptr, B, False, d_out.ptr)
-    dom = dominant_conv([eng.net], ("arcface",), [eng.program])
+    dom = dominant_conv([eng.net], ("arcface",), [eng.program], {"arcface": args.precision})
     recs = eng.net.profile_ops()
     eng.net.profile(False)
     # f16x3 issues 3 f16 MFMAs per algorithmic product: its roofline is a third of dense f16
     # (f16c8: 2 f16 MFMAs + 1 block-scaled e4m3 MFMA per 64-channel K tile where f16 takes 2; its
     # roofline is the f16 peak x 2 / 3 at the e4m3 instruction's measured equal issue time)
-    peak = {"f16": PEAK_F16_TFLOPS, "f16x3": PEAK_F16_TFLOPS / 3,
-            "f16c8": PEAK_F16_TFLOPS * 2 / 3}.get(args.precision, PEAK_F32_TFLOPS)
+    peak = _peak_for(args.precision)
     fl = eng.flops_per_forward * B
     ms = elapsed / args.steps * 1e3
     net_tf = fl / (ms * 1e-3) / 1e12
@@ -1129,12 +1150,13 @@ def main_other(args):
             continue
         f32 = n.precision == 1
         tf = p_["conv_flops"] / (p_["conv_ms"] * 1e-3) / 1e12
-        pk = PEAK_F32_TFLOPS if f32 else PEAK_F16_TFLOPS
-        per_net[nm] = {"dtype": "f32" if f32 else "f16", "conv_ms_per_step": round(p_["conv_ms"] / args.steps, 3),
-                       "achieved_tflops": round(tf, 1), "peak": pk, "frac": round(tf / pk, 4)}
-        if nm.startswith("scrfd") and not f32 and getattr(fe, "det_precision", None) == 2:   # PC_PREC_F16X3
-            # algorithmic FLOPs above; the f16x3 program issues 3 MFMAs per product
-            per_net[nm].update(dtype="f16x3", mfma_tflops=round(3 * tf, 1), mfma_frac=round(3 * tf / pk, 4))
+        pn = "f32" if f32 else _prec_name(fe.arc_precision if nm == "arcface" else
+                                           getattr(fe, "det_precision", None) if nm.startswith("scrfd") else None)
+        pk = _peak_for(pn)
+        per_net[nm] = {"dtype": pn, "conv_ms_per_step": round(p_["conv_ms"] / args.steps, 3),
+                       "achieved_tflops": round(tf, 1), "peak": round(pk, 1), "frac": round(tf / pk, 4)}
+        if pn == "f16x3":   # algorithmic FLOPs above; 3 MFMAs issued per product
+            per_net[nm].update(mfma_tflops=round(3 * tf, 1), mfma_frac=round(3 * tf / PEAK_F16_TFLOPS, 4))
     peak = PEAK_F16_TFLOPS if args.precision == "f16" else PEAK_F32_TFLOPS
     total_units = units_per_step * args.steps if scaling == "strong" else _sum_over_ranks(world, units_per_step *
                                                                                            args.steps)

@@ -36,6 +36,7 @@ int conv_fast_tile(int cfg, int* bc, int* bp);
 int conv_fast_valid(int cfg, int rowb);
 int conv_fast_valid_sx(int cfg, int rowb);
 int conv_fast_valid_c8(int cfg, int rowb);
+int conv_fast_valid_wg(int cfg);
 int conv_halo_num_cfgs();
 int conv_halo_tile(int cfg, int* bc, int* bp);
 int conv_halo_fits(int cfg, int KH, int KW, int W);
@@ -566,7 +567,8 @@ struct NetTensor { int buf, H, W, C, cs, coff, is_f32, split; int c8 = 0, e_lo =
 struct NetOp { int w[32]; };
 // sx: fused f16x3 split tiles on conv_fast (pc_conv_fast.hip SX); c8: its f16c8 form (C8);
 // wf8s: E8M0 exponents of the conv's W_hi8 | W_lo8 << 8 bytes (c8 weights)
-struct ConvPlan { int rowb, cfg, splitk, halo = -1, fast = -1, t2d = -1, sx = 0, hx = 0, c8 = 0, wf8s = 0; long long M_per_image; double flops_per_image; };
+// wg: the fused f16x3 tile takes its weight fragments from the fragment-ordered copy (pc_net::wfrag)
+struct ConvPlan { int rowb, cfg, splitk, halo = -1, fast = -1, t2d = -1, sx = 0, hx = 0, c8 = 0, wf8s = 0, wg = 0; long long M_per_image; double flops_per_image; };
 // A stem (tiny Cin) runs as im2col + a 1x1 MFMA conv over 32-element K rows.
 struct StemPlan {
   int use_mfma = 0, npad = 0, cfg = 0, rowb = 0, cin_true = 0;
@@ -633,6 +635,7 @@ struct pc_net {
   std::map<std::pair<int, const void*>, hipGraphExec_t> graphs;
   // f16c8 convs: per op, E8M0 exponents of the weight bytes' scales (W_hi8 | W_lo8 << 8), 0 elsewhere
   std::vector<int> wf8s;
+  std::vector<void*> wfrag;   // per conv op: fragment-ordered f16x3 weights (ConvParams::wfrag), or null
   // absmax calibration of the f16c8 tensors (pc_net_calibrate): per tensor max |x| slots
   int calib = 0;
   float* d_absmax = nullptr;
@@ -821,12 +824,24 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
         double bsx_t = 0;
         // fused tiles walk K channel-block-major (each block through every tap, pc_conv_fast.hip
         // advance), so the K-row width orders the accumulation: ONE width per conv for every
-        // plan class - the input's width when a full-batch tile runs at it, 64 bytes otherwise
+        // plan class - the width of the tile the full-batch plan picks
         int sx_rb = 64;
-        for (int k = 0; k < conv_fast_num_cfgs() && sx_rb != rowb; ++k) {
-          int bc = 0, bp = 0;
-          conv_fast_tile(k, &bc, &bp);
-          if (!(k >= kFastSmallCfg0 && k <= kFastSmallCfg1) && npad % bc == 0 && conv_fast_valid_sx(k, rowb)) sx_rb = rowb;
+        {
+          const long long Mfull = Mimg * n->max_batch;
+          double bt = 0;
+          bool found = false;
+          for (int k = 0; k < conv_fast_num_cfgs(); ++k) {
+            int bc = 0, bp = 0;
+            conv_fast_tile(k, &bc, &bp);
+            if ((k >= kFastSmallCfg0 && k <= kFastSmallCfg1) || npad % bc) continue;
+            for (int rb : {rowb, 64}) {
+              if (!conv_fast_valid_sx(k, rb)) continue;
+              const long long t = (Mfull + bp - 1) / bp * (npad / bc);
+              const double est = (double)((t + 255) / 256) * bc * bp * cost[k];
+              if (!found || est < bt) { found = true; bt = est; sx_rb = rb; }
+              break;
+            }
+          }
         }
         for (int k = 0; k < conv_fast_num_cfgs(); ++k) {
           int bc = 0, bp = 0;
@@ -929,6 +944,12 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
   }
   if ((Y.c8 || (w[21] >= 0 && n->tens[w[21]].c8)) && (pl.fast < 0 || !pl.sx || pl.t2d >= 0 || pl.hx || pl.halo >= 0))
     return fail(n->ctx, PC_ERR_FORMAT, "f16c8 outputs and residuals are written / read by conv_fast's fused tiles only");
+  // fused f16x3 tiles of 64-byte K rows on the WG form where it is instantiated (PC_SX_WG=0: staged
+  // weights, for A/B). Same K order and pass order as the staged form: bit-identical outputs.
+  pl.wg = 0;
+  if (pl.fast >= 0 && pl.sx && !pl.c8 && pl.rowb == 64 && pl.splitk == 1 && pl.t2d < 0 && !pl.hx && pl.halo < 0 &&
+      conv_fast_valid_wg(pl.fast) && !(getenv("PC_SX_WG") && atoi(getenv("PC_SX_WG")) == 0))
+    pl.wg = 1;
   if ((Y.split ? Y.C / 2 : Y.C) > npad) return fail(n->ctx, PC_ERR_FORMAT, "conv output tensor wider than npad");
   if (Y.split && (Y.is_f32 || Y.cs != Y.C || (Y.C / 2) % 8))
     return fail(n->ctx, PC_ERR_FORMAT, "split conv output must be a dense f16 [hi | lo] tensor");
@@ -1130,6 +1151,49 @@ static uint8_t e4m3_encode(float v) {
   if (q == 16) { q = 8; ++E; }
   if (E > 8 || (E == 8 && q > 14)) return sgn | 0x7e;
   return sgn | (uint8_t)(((E + 7) << 3) | (q - 8));
+}
+
+// Fragment-ordered copy of a fused f16x3 conv's weights (conv_fast WG): K tiles of 32 channels in the
+// fused tiles' channel-block-major order (segment, hi channel block, tap row, tap column); per tile
+// npad / 16 row blocks of [W_hi, W_lo] fragments, each 64 lanes x 8 f16 (lane l: row l & 15,
+// channels 8 (l >> 4) .. +8), so a wave's fragment read is one contiguous KiB.
+static int pack_wfrag(pc_net* n, const NetOp& op, const float* wf, void** out) {
+  const int* w = op.w;
+  const int npad = w[14];
+  const long long ktot = w[15];
+  long long nkt = 0, k0 = 0;
+  for (int sg = 0; sg < w[2]; ++sg) {
+    const NetTensor& X = n->tens[w[3 + 5 * sg]];
+    if (!X.split || (X.C / 2) % 32) return fail(n->ctx, PC_ERR_FORMAT, "wfrag: split inputs of 32-channel blocks");
+    nkt += (long long)w[4 + 5 * sg] * w[5 + 5 * sg] * (X.C / 2 / 32);
+    k0 += (long long)w[4 + 5 * sg] * w[5 + 5 * sg] * 3 * (X.C / 2);
+  }
+  if (k0 != ktot || npad % 16) return fail(n->ctx, PC_ERR_FORMAT, "wfrag: K layout");
+  const long long tile_elems = (long long)(npad / 16) * 2 * 512;
+  std::vector<_Float16> h((size_t)(nkt * tile_elems));
+  long long kt = 0;
+  k0 = 0;
+  for (int sg = 0; sg < w[2]; ++sg) {
+    const int cp = n->tens[w[3 + 5 * sg]].C / 2, KH = w[4 + 5 * sg], KW = w[5 + 5 * sg];
+    for (int cb = 0; cb < cp / 32; ++cb)
+      for (int th = 0; th < KH; ++th)
+        for (int tw = 0; tw < KW; ++tw, ++kt) {
+          const long long kbase = k0 + (long long)(th * KW + tw) * 3 * cp + cb * 32;
+          for (int rb = 0; rb < npad / 16; ++rb)
+            for (int hf = 0; hf < 2; ++hf)
+              for (int l = 0; l < 64; ++l)
+                for (int j = 0; j < 8; ++j) {
+                  const long long row = rb * 16 + (l & 15);
+                  const long long k = kbase + (hf ? 2 * cp : 0) + (l >> 4) * 8 + j;
+                  h[(size_t)(kt * tile_elems + ((long long)(rb * 2 + hf) * 64 + l) * 8 + j)] = (_Float16)wf[row * ktot + k];
+                }
+        }
+    k0 += (long long)KH * KW * 3 * cp;
+  }
+  if (hipMalloc(out, h.size() * 2) != hipSuccess ||
+      hipMemcpy(*out, h.data(), h.size() * 2, hipMemcpyHostToDevice) != hipSuccess)
+    return fail(n->ctx, PC_ERR_HIP, "wfrag upload failed");
+  return PC_OK;
 }
 
 // f16c8 conv weights: the program holds the split form [W_hi, W_hi, W_lo] per tap and
@@ -1376,6 +1440,14 @@ extern "C" int pc_net_create(pc_ctx* c, const void* prog, size_t nbytes, int pre
       rc = fail(c, PC_ERR_FORMAT, "unknown op type");
     }
   }
+  // fragment-ordered weights for the convs any plan runs on the WG form
+  n->wfrag.assign(n->ops.size(), nullptr);
+  for (size_t i = 0; i < n->ops.size() && rc == PC_OK; ++i) {
+    if (n->ops[i].w[0] != OP_CONV) continue;
+    bool wg = n->plans[i].wg;
+    for (auto& pc : n->plans_cls) wg = wg || pc[i].wg;
+    if (wg) rc = pack_wfrag(n, n->ops[i], reinterpret_cast<const float*>(n->host_arrays[n->ops[i].w[13]]), &n->wfrag[i]);
+  }
   n->host_arrays.clear();
   if (rc == PC_OK) rc = plan_chains(n);
   if (rc == PC_OK && stem_col_bytes) {
@@ -1402,6 +1474,7 @@ extern "C" int pc_net_destroy(pc_net* n) {
   if (n->cap_stream) hipStreamDestroy(n->cap_stream);
   if (n->d_absmax) hipFree(n->d_absmax);
   for (void* a : n->arrays) if (a) hipFree(a);
+  for (void* a : n->wfrag) if (a) hipFree(a);
   for (auto& b : n->bufs) if (b.d) hipFree(b.d);
   if (n->partial) hipFree(n->partial);
   if (n->prep) hipFree(n->prep);
@@ -1541,6 +1614,7 @@ static int run_ops(pc_net* n, int N, hipStream_t s) {
       p.sx = pl.sx;
       p.c8 = pl.c8;
       p.wf8s = n->wf8s[i];
+      p.wfrag = pl.wg ? n->wfrag[i] : nullptr;
       if (Y.c8) {
         p.yc8 = 1;
         p.ylo_mul = std::ldexp(1.f, Y.e_lo);
@@ -1751,7 +1825,7 @@ extern "C" int pc_net_profile_read(pc_net* n, double* out) {
 }
 
 // Per-record detail of the profiled runs: 6 doubles per record
-// [op index, kind, ms, flops, kernel (100+k fast tile k, 200+v t2d variant v, 300 resident chain, 500 halo-staged f16x3, k halo tile k, -1 igemm), igemm cfg]; returns the count.
+// [op index, kind, ms, flops, kernel (100+k fast tile k, 200+v t2d variant v, 300 resident chain, 500 halo-staged f16x3, k halo tile k, -1 igemm), igemm cfg or the conv_fast form: 0 plain, 1 fused split, 3 fused split with register weight fragments]; returns the count.
 extern "C" int pc_net_profile_ops(pc_net* n, double* out, int max_recs) {
   if (!n || !out) return -PC_ERR_ARG;
   HIPCHK(n->ctx, hipStreamSynchronize(n->ctx->stream));
@@ -1771,7 +1845,10 @@ extern "C" int pc_net_profile_ops(pc_net* n, double* out, int max_recs) {
                                  : pl->fast >= 0   ? 100 + pl->fast
                                                    : pl->halo)
                               : -1;
-    o[5] = conv ? pl->cfg : -1;
+    // [5]: the generic kernel's tile cfg; for conv_fast launches its form: 1 fused split (SX), 3 SX
+    // with register weight fragments (WG), 0 plain
+    const bool fastk = conv && r.code < 0 && !pl->hx && pl->t2d < 0 && pl->fast >= 0;
+    o[5] = !conv ? -1 : fastk ? (pl->sx ? 1 : 0) + (pl->wg ? 2 : 0) : pl->cfg;
   }
   return k;
 }

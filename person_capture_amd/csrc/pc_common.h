@@ -79,6 +79,10 @@ struct ConvParams {
   // hi8 = e4m3(hi * yhi_mul); residual: hi + lo8 * rlo_inv
   int yc8, rc8;
   float ylo_mul, yhi_mul, rlo_inv;
+  // fused f16x3 tiles, WG form (conv_fast): the weights in fragment order, per K tile (the SX
+  // channel-block-major order) x 16-row block x [W_hi, W_lo] x 64 lanes x 8 f16 (lane l: row l & 15,
+  // channels 8 (l >> 4) .. +8 of the tile's 32); null: the weights are staged from w
+  const void* wfrag;
 };
 
 // Direct convolution for tiny input channel counts (network stems, Cin <= 4).

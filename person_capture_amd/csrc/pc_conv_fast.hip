@@ -45,8 +45,11 @@ __host__ __device__ constexpr int fast_epi_bytes() {
 // C8 (with SX staging): f16c8 inputs - per K tile (32 or 64 channels) the f16 MFMAs for
 // x_hi*W_hi, then one block-scaled e4m3 MFMA (v_mfma_scale_f32_16x16x128_f8f6f4) over the f8 rows
 // [lo8 | hi8] x [W_hi8 | W_lo8] for x_lo*W_hi + x_hi*W_lo: 3 MFMA issues per tile where SX takes 6.
+// WG (with SX, 64-byte K rows): the weight fragments come straight from global memory (L2) into
+// registers, from the fragment-ordered copy p.wfrag (pc_api.cpp pack_wfrag), one K tile ahead; only the
+// split pixel rows are staged, so the ring holds 4 stages and the LDS carries ~40 % fewer bytes per MFMA.
 template <typename T, int BC, int BP, int ROWB, int WC, int WP, int NSTAGE, int OCC = 1, bool SPLIT = false,
-          bool SX = false, bool C8 = false>
+          bool SX = false, bool C8 = false, bool WG = false>
 __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fast(ConvParams p) {
   constexpr int NW = WC * WP;
   constexpr int NH = SX ? 2 : 1;              // staged halves per tile
@@ -58,12 +61,14 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
   static_assert(NA % NW == 0, "every wave must issue the same weight DMA count");
   // im2col rows: when NB is not a multiple of the wave count, the last round of DMAs of
   // the waves past NB goes to a trash area, so every wave still issues NIB (static vmcnt)
-  constexpr int NIA = NA / NW, NIB = (NB + NW - 1) / NW, NI = NH * (NIA + NIB);
+  constexpr int NIA = WG ? 0 : NA / NW, NIB = (NB + NW - 1) / NW, NI = NH * (NIA + NIB);
+  static_assert(!WG || (SX && !C8 && ROWB == 64), "global weight fragments: fused f16x3 tiles, 64-byte K rows");
+  constexpr int BCL = WG ? 0 : BC;            // weight rows staged per tile half
   static_assert(!SX || sizeof(T) == 2, "fused split tiles: f16 only");
   static_assert(!C8 || (SX && (ROWB == 128 || ROWB == 64)), "f16c8 tiles: fused split staging");
   constexpr int WTC = BC / WC, WTP = BP / WP;
   constexpr int TC = WTC / 16, TP = WTP / 16;
-  constexpr int BUF = NH * (BC + BP) * ROWB;
+  constexpr int BUF = NH * (BCL + BP) * ROWB;
   constexpr int RING = NSTAGE * BUF;
   constexpr int EPI_MAX = OCC == 1 ? 131072 : 65536;
   constexpr int EPI = fast_epi_bytes<BC, BP, WC, WP, EPI_MAX>();
@@ -92,7 +97,7 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
 
   // ---- staging geometry ----
   const int lrow = lane / CHUNKS, pchunk = lane % CHUNKS;
-  unsigned woff[NIA];
+  unsigned woff[NIA > 0 ? NIA : 1];
   static_for<NIA>([&](auto ic) __attribute__((always_inline)) {
     constexpr int i = decltype(ic)::value;
     const int r = (i * NW + wave) * RPI + lrow;
@@ -174,7 +179,7 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
         unsigned off = ok ? b_base[i] + tapoff : b_zero;
         asm volatile("" : "+v"(off));
         const int dst = (NB % NW == 0 || i * NW + wave < NB)
-                            ? slot * BUF + (NH * BC + h * BP) * ROWB + (i * NW + wave) * 1024
+                            ? slot * BUF + (NH * BCL + h * BP) * ROWB + (i * NW + wave) * 1024
                             : RING + wave * 1024;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)(smem + dst), 16, off, xso + h * svwrap * ROWB, 0, 0);
       });
@@ -230,7 +235,7 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
   const int fr = lane & 15;
   const int sw = swz(fr);
   const unsigned a_row = (wr * WTC + fr) * ROWB;
-  const unsigned b_row = (NH * BC + wc * WTP + fr) * ROWB;
+  const unsigned b_row = (NH * BCL + wc * WTP + fr) * ROWB;
   // Pinned two-k-substep schedule (f16, 128-byte K rows, two register sets fit beside the
   // accumulators): the 11 fragment reads of k-substep 0 go out first, the reads of k-substep 1
   // are interleaved one per MFMA with k-substep 0's MFMAs, and every MFMA waits (counted
@@ -269,6 +274,21 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
   const int xsc0 = klo ? (p.seg[0].f8s & 0xff) : ((p.seg[0].f8s >> 8) & 0xff);
   const int xsc1 = klo ? (p.seg[1].f8s & 0xff) : ((p.seg[1].f8s >> 8) & 0xff);
   const int kt0 = p.seg[0].kt;
+  // WG: this wave's W_hi / W_lo fragments of the current K tile (the next tile's W_lo is loaded once
+  // the first pass has consumed it, its W_hi after the last pass)
+  // (MUBUF loads: tile offset in an SGPR, two lane offsets, fragment offsets as immediates)
+  f16x8 wgh[WG ? TC : 1], wgl[WG ? TC : 1];
+  const __amdgpu_buffer_rsrc_t wgrs = rsrc(WG ? p.wfrag : p.w);
+  const int wgoff0 = ((c0 + wr * WTC) / 16) * 2048 + lane * 16, wgoff1 = wgoff0 + 4096;
+  const int wgstride = (p.npad / 16) * 2048;   // bytes per K tile
+  auto wg_load = [&](f16x8* dst, int kt, auto hc) __attribute__((always_inline)) {
+    constexpr int h = decltype(hc)::value;
+    static_for<TC>([&](auto tc) __attribute__((always_inline)) {
+      constexpr int t = decltype(tc)::value, o = t * 2048 + h * 1024;
+      dst[t] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(wgrs, o < 4096 ? wgoff0 + o : wgoff1 + (o - 4096),
+                                                                              kt * wgstride, 0));
+    });
+  };
   auto compute = [&](auto slotc, int tix) __attribute__((always_inline)) {
     constexpr int slot = decltype(slotc)::value;
     const char* base = smem + slot * BUF;
@@ -319,6 +339,43 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
       if constexpr (TC * TP >= 16) __builtin_amdgcn_sched_barrier(0);
       return;
     }
+    // fused split tiles: per k-substep three passes over the fragment grid (a dependent MFMA is
+    // TC*TP issues away), W_lo*x_hi, W_hi*x_hi, W_hi*x_lo - the same order in every SX form
+    if constexpr (WG) {
+      // x_hi fragments, W_lo*x_hi; x_lo reads behind W_hi*x_hi; the next tile's W_lo after it,
+      // W_hi*x_lo, the next tile's W_hi (at most 2 TP + 2 TC fragments live beside the accumulators)
+      const unsigned ko = ((lane >> 4) ^ sw) << 4;
+      f16x8 fbh[TP], fbl[TP];
+      const int tn = tix + 1 < nk ? tix + 1 : nk - 1;
+#pragma unroll
+      for (int t = 0; t < TP; ++t) fbh[t] = *reinterpret_cast<const f16x8*>(base + b_row + ko + t * 16 * ROWB);
+#pragma unroll
+      for (int a = 0; a < TC; ++a)
+#pragma unroll
+        for (int b = 0; b < TP; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wgl[a], fbh[b], acc[a][b], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < TP; ++t) fbl[t] = *reinterpret_cast<const f16x8*>(base + b_row + BP * ROWB + ko + t * 16 * ROWB);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int a = 0; a < TC; ++a)
+#pragma unroll
+        for (int b = 0; b < TP; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wgh[a], fbh[b], acc[a][b], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      wg_load(wgl, tn, std::integral_constant<int, 1>{});
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int a = 0; a < TC; ++a)
+#pragma unroll
+        for (int b = 0; b < TP; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wgh[a], fbl[b], acc[a][b], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      wg_load(wgh, tn, std::integral_constant<int, 0>{});
+      __builtin_amdgcn_sched_barrier(0);
+      return;
+    }
     if constexpr (SX) {
 #pragma unroll
       for (int ks = 0; ks < KSTEPS; ++ks) {
@@ -334,17 +391,16 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
           fbh[t] = *reinterpret_cast<const f16x8*>(base + b_row + ko + t * 16 * ROWB);
           fbl[t] = *reinterpret_cast<const f16x8*>(base + b_row + BP * ROWB + ko + t * 16 * ROWB);
         }
-        // three passes over the fragment grid (a dependent MFMA is TC*TP issues away)
-#pragma unroll
-        for (int a = 0; a < TC; ++a)
-#pragma unroll
-          for (int b = 0; b < TP; ++b)
-            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fah[a], fbh[b], acc[a][b], 0, 0, 0);
 #pragma unroll
         for (int a = 0; a < TC; ++a)
 #pragma unroll
           for (int b = 0; b < TP; ++b)
             acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fal[a], fbh[b], acc[a][b], 0, 0, 0);
+#pragma unroll
+        for (int a = 0; a < TC; ++a)
+#pragma unroll
+          for (int b = 0; b < TP; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fah[a], fbh[b], acc[a][b], 0, 0, 0);
 #pragma unroll
         for (int a = 0; a < TC; ++a)
 #pragma unroll
@@ -402,11 +458,25 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
     advance(more);
     kiss += more ? 1 : 0;
   });
+  if constexpr (WG) {   // tile 0's weight fragments, behind the prologue's DMAs
+    wg_load(wgl, 0, std::integral_constant<int, 1>{});
+    wg_load(wgh, 0, std::integral_constant<int, 0>{});
+  }
   int it = 0;
-  // one step: retire tile `it`, refill the slot of tile it-1 with tile it+NSTAGE-1
-  auto step = [&](auto jc) __attribute__((always_inline)) {
+  // one step: retire tile `it`, refill the slot of tile it-1 with tile it+NSTAGE-1.
+  // WG: the 2 TC weight loads of step k follow its DMA, so NI + 2 TC loads per step are issued
+  // after tile it's DMAs (NI in the prologue, where tile 0's weights come once after all DMAs):
+  // step j of the first round waits for (NSTAGE-2) NI + 2 TC (j + 1) younger loads, later steps
+  // for (NSTAGE-2) (NI + 2 TC) + 2 TC
+  constexpr int WGL = WG ? 2 * TC : 0;
+  auto step = [&](auto jc, auto firstc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NSTAGE - 2) * NI) : "memory");
+    constexpr bool first = decltype(firstc)::value;
+    constexpr int steady = (NSTAGE - 2) * (NI + WGL) + WGL;
+    constexpr int early = (NSTAGE - 2) * NI + WGL * (j + 1);
+    constexpr int wcnt = first && early < steady ? early : steady;
+    static_assert(wcnt <= 63, "vmcnt range");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(wcnt) : "memory");
     bar();
     if (!(p.dbg & 1)) issue(std::integral_constant<int, (j + NSTAGE - 1) % NSTAGE>{}, kiss);   // dbg: tuning only
     const bool more = kiss + 1 < nk;
@@ -415,11 +485,21 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
     if (!(p.dbg & 2)) compute(std::integral_constant<int, j>{}, it + j);
   };
   if (p.dbg & 8) return;   // tuning only: prologue only
-  for (; it + NSTAGE <= nk; it += NSTAGE)
-    static_for<NSTAGE>([&](auto jc) __attribute__((always_inline)) { step(jc); });
-  static_for<NSTAGE - 1>([&](auto jc) __attribute__((always_inline)) {
-    if (it + decltype(jc)::value < nk) step(jc);
-  });
+  using first_t = std::integral_constant<bool, WG>;   // only WG's early waits differ
+  using later_t = std::integral_constant<bool, false>;
+  if (it + NSTAGE <= nk) {
+    static_for<NSTAGE>([&](auto jc) __attribute__((always_inline)) { step(jc, first_t{}); });
+    it += NSTAGE;
+    for (; it + NSTAGE <= nk; it += NSTAGE)
+      static_for<NSTAGE>([&](auto jc) __attribute__((always_inline)) { step(jc, later_t{}); });
+    static_for<NSTAGE - 1>([&](auto jc) __attribute__((always_inline)) {
+      if (it + decltype(jc)::value < nk) step(jc, later_t{});
+    });
+  } else {
+    static_for<NSTAGE - 1>([&](auto jc) __attribute__((always_inline)) {
+      if (it + decltype(jc)::value < nk) step(jc, first_t{});
+    });
+  }
 
   // drain the (dummy) tail DMAs and every wave's last reads before the LDS is reused
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -431,6 +511,7 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
     conv_epilogue<T, TC, TP, WTC, WTP>(p, acc, c0, p0, wr, wc, lane, 0);
 }
 
+#ifndef PC_FAST_KERNEL_ONLY   // (tools/kernel_regs.sh: the kernel template alone, for register checks)
 // tile shapes whose DMA count divides evenly over the waves at this row width
 template <int BC, int BP, int ROWB, int NW>
 constexpr bool fast_valid() {
@@ -502,6 +583,17 @@ constexpr int fast_sx_stages() {
   return ns;
 }
 
+// WG tiles (fused f16x3, weights from global memory): 4 stages of the split pixel rows (+ trash
+// rows) and the epilogue image fit the LDS, and the loads in flight stay in the vmcnt range
+template <int BC, int BP, int WC, int WP>
+constexpr bool fast_wg_fits() {
+  constexpr int NW = WC * WP, RPI = 16, NB = BP / RPI;
+  constexpr int ring = 4 * 2 * BP * 64 + (NB % NW ? NW * 1024 : 0);
+  constexpr int NI = 2 * ((NB + NW - 1) / NW), WGL = 2 * (BC / WC / 16);
+  return BP % RPI == 0 && (BC / WC) % 16 == 0 && ring <= 163840 && fast_epi_bytes<BC, BP, WC, WP>() <= 163840 &&
+         2 * (NI + WGL) + WGL <= 63;
+}
+
 // power-of-two channel tiles: the LDS epilogue (the only one that writes f16c8 outputs)
 template <int BC>
 constexpr bool LDS_EPI_OK() { return ((BC / 8) & (BC / 8 - 1)) == 0 && ((BC / 16) & (BC / 16 - 1)) == 0; }
@@ -513,6 +605,15 @@ static hipError_t launch_fast_cfg(const ConvParams& p, hipStream_t s) {
   } else {
     const int nwg = (p.M + BP - 1) / BP * (p.npad / BC);
     if (p.sx) {   // fused f16x3 / f16c8 tiles: always the split epilogue
+      if (p.wfrag && !p.c8) {   // weight fragments from global memory: 4 stages of pixel rows
+        if constexpr (sizeof(T) == 2 && ROWB == 64 && OCC == 1 && BC == 256 && BP == 224 && fast_wg_fits<BC, BP, WC, WP>()) {
+          hipLaunchKernelGGL((conv_fast<T, BC, BP, ROWB, WC, WP, 4, 1, true, true, false, true>), dim3(nwg),
+                             dim3(64 * WC * WP), 0, s, p);
+          return hipGetLastError();
+        } else {
+          return hipErrorInvalidValue;
+        }
+      }
       constexpr int NS = fast_sx_stages<BC, BP, ROWB, WC * WP, NSTAGE>();
       if constexpr (sizeof(T) == 2 && ROWB != 256 && fast_sx_fits<BC, BP, ROWB, WC * WP, OCC, NS>()) {
         if (p.c8) {
@@ -602,6 +703,15 @@ int conv_fast_valid_sx(int cfg, int rowb) {
   return ring <= 163840;
 }
 
+// can cfg run the WG form (fused f16x3 tiles with register weight fragments) at 64-byte K rows?
+int conv_fast_valid_wg(int cfg) {
+  if (cfg < 0 || cfg >= kNumFastCfgs || !conv_fast_valid_sx(cfg, 64)) return 0;
+  switch (cfg) {   // the instantiated WG tiles
+    case 13: return fast_wg_fits<256, 224, 4, 2>();
+    default: return 0;
+  }
+}
+
 // can cfg run f16c8 convs at K rows of rowb bytes (fused split staging, LDS epilogue)?
 int conv_fast_valid_c8(int cfg, int rowb) {
   if (!conv_fast_valid_sx(cfg, rowb)) return 0;
@@ -628,4 +738,5 @@ hipError_t conv_fast_launch(int f32, int rowb, int cfg, const ConvParams& p, hip
   return rowb == 128 ? launch_fast_t<f16, 128>(p, cfg, s) : launch_fast_t<f16, 64>(p, cfg, s);
 }
 
+#endif  // PC_FAST_KERNEL_ONLY
 }  // namespace pc

@@ -108,3 +108,34 @@ def test_arcface_f16c8_program(gpu_ctx, r100):
     err = float(np.abs(a - ref).max())
     print(f"f16c8 IResNet-100: max |de| {err:.2e}")
     assert err < 1e-4 and np.array_equal(b, c) and float(np.abs(b - ref).max()) < 1e-4
+
+
+def test_arcface_f16x3_wg_form_bit_identical(gpu_ctx, monkeypatch):
+    """The 256x224 fused split tile's WG form (weight fragments from global memory into registers,
+    only the split pixel rows staged: pc_conv_fast.hip WG, pc_api.cpp pack_wfrag) runs the b256
+    14x14x256 layers and gives the staged form's bits (PC_SX_WG=0): same K order, same passes."""
+    from person_capture_amd.runtime import Net
+    P = models.compile_iresnet(models.synth_iresnet(100, seed=4), 100, split=True)
+    x = np.zeros((256, 112, 112, 4), np.float16)
+    x[..., :3] = np.random.default_rng(5).uniform(-127.5, 127.5, (256, 112, 112, 3))
+    d = gpu_ctx.upload(x)
+    outs, forms = [], []
+    try:
+        for wg in ("1", "0"):
+            monkeypatch.setenv("PC_SX_WG", wg)
+            net = Net(gpu_ctx, P.serialize(), PC_PREC_F16, max_batch=256)
+            try:
+                net.profile(True)
+                net.run(d.ptr, 256)
+                forms.append([(int(r[4]), int(r[5])) for r in net.profile_ops()])
+                net.profile(False)
+                outs.append(net.read_output(0, 256).copy())
+            finally:
+                net.close()
+    finally:
+        d.free()
+    wg_launches = sum(1 for c, f in forms[0] if c == 113 and f == 3)
+    assert wg_launches >= 50, forms[0]
+    assert not any(f == 3 for c, f in forms[1] if 100 <= c < 200)
+    assert sum(1 for c, f in forms[1] if c == 113 and f == 1) == wg_launches
+    assert np.array_equal(outs[0].view(np.uint8), outs[1].view(np.uint8))

@@ -1,6 +1,6 @@
 """Per-layer profile of the two trunks (HIP events around every launch, pc_net_profile_ops).
-usage: python tools/probe_layers.py [arc|scrfd|scrfdx3] [batch]   -> table grouped by conv shape.
-scrfdx3: the f16x3 split SCRFD program.
+usage: python tools/probe_layers.py [arc|arcx3|scrfd|scrfdx3] [batch]   -> table grouped by conv shape.
+scrfdx3 / arcx3: the f16x3 split programs.
 PROBE_MAXB=N: create the net for N images (the small-batch plans then serve batch <= min(16, N/4))."""
 import sys
 from collections import defaultdict
@@ -30,10 +30,10 @@ def describe(P, w):
 
 def main():
     which = sys.argv[1] if len(sys.argv) > 1 else "arc"
-    B = int(sys.argv[2]) if len(sys.argv) > 2 else (256 if which == "arc" else 64)
+    B = int(sys.argv[2]) if len(sys.argv) > 2 else (256 if which.startswith("arc") else 64)
     ctx = GpuContext(0)
-    if which == "arc":
-        P = models.compile_iresnet(models.synth_iresnet(100, seed=0, calibrate=False), 100)
+    if which in ("arc", "arcx3"):
+        P = models.compile_iresnet(models.synth_iresnet(100, seed=0, calibrate=False), 100, split=which == "arcx3")
     else:
         P = models.compile_scrfd(models.synth_scrfd("10g", seed=0, calibrate=False), "10g", 640,
                                  split=which == "scrfdx3")
@@ -41,7 +41,7 @@ def main():
     net = Net(ctx, P.serialize(), prec, max_batch=int(os.environ.get('PROBE_MAXB', B)))   # FaceEmbedder: 512 for arc
     H, W, Cc = P.dims(P.input)
     x = np.zeros((B, H, W, Cc), np.float32 if prec == PC_PREC_F32 else np.float16)
-    x[..., :3] = np.random.default_rng(0).standard_normal((B, H, W, 3))
+    x[..., :3] = np.random.default_rng(0).standard_normal((B, H, W, 3)) * (127.5 if P.input_centered else 1.0)
     d = ctx.upload(x)
     for _ in range(3):
         net.run(d.ptr, B)
@@ -54,6 +54,8 @@ def main():
     agg = defaultdict(lambda: [0, 0.0, 0.0, ""])
     tot_ms = tot_fl = 0.0
     for op, kind, ms, fl, halo, cfg in recs:
+        if 100 <= halo < 200:
+            cfg = -1   # (the conv_fast form, not a generic tile)
         key = describe(P, P.ops[int(op)])
         a = agg[key]
         a[0] += 1; a[1] += ms; a[2] += fl
