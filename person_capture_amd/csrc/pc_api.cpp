@@ -800,6 +800,9 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
                                     1.9, 1.6, 1.6, 3.0, 1.9, 1.3, 1.55};
       static const int occ[] = {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 1, 1, 1, 2, 1, 1, 1, 1, 1, 1, 1};   // workgroups per CU
       static_assert(sizeof(cost) / sizeof(cost[0]) == sizeof(occ) / sizeof(occ[0]), "tile tables");
+      // fused split tiles: the 128x512 tile (8 waves of 64x128) ran ArcFace-x3's 28x28x128 at 464 us
+      // against 233 for the 128x256 tile at the same estimate (profiles/r05n_sx_tile_sweep.txt)
+      auto sxcost = [&](int k) { return k == 9 ? 2.2 : cost[k]; };
       int best = -1, best_rowb = rowb;
       double best_t = 0;
       bool rows256 = small && !n->f32 && !any_split && rowb == 128 && !getenv("PC_CONV_ROWB");
@@ -837,7 +840,7 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
             for (int rb : {rowb, 64}) {
               if (!conv_fast_valid_sx(k, rb)) continue;
               const long long t = (Mfull + bp - 1) / bp * (npad / bc);
-              const double est = (double)((t + 255) / 256) * bc * bp * cost[k];
+              const double est = (double)((t + 255) / 256) * bc * bp * sxcost(k);
               if (!found || est < bt) { found = true; bt = est; sx_rb = rb; }
               break;
             }
@@ -856,7 +859,7 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
             if (!in_c8 && rb != sx_rb && force <= 0) continue;
             if (!conv_fast_valid_sx(k, rb)) continue;
             const long long t = (M + bp - 1) / bp * (npad / bc);
-            const double est = (double)((t + 255) / 256) * bc * bp * cost[k];
+            const double est = (double)((t + 255) / 256) * bc * bp * sxcost(k);
             if (bsx < 0 || est < bsx_t) { bsx = k; bsx_t = est; bsx_rowb = rb; }
             break;
           }
@@ -1386,9 +1389,19 @@ extern "C" int pc_net_create(pc_ctx* c, const void* prog, size_t nbytes, int pre
   // (SCRFD) keeps 1 / 4 / 16, so its 32-frame C3 chunks stay on the max-batch tiles (r03:
   // the 16-image tiles at 32 images cost 0.4 ms per step).
   n->cls_batch.clear();
-  if (max_batch > 2 && !getenv("PC_NO_SMALL_PLANS"))
+  if (max_batch > 2 && !getenv("PC_NO_SMALL_PLANS")) {
     for (int b : {1, 4, 16, 32, 64})
       if (b <= std::max(1, max_batch / 4)) n->cls_batch.push_back(b);
+    // f16x3 nets (ArcFace-x3 runs 256-row calls on a 512-row net: C3's 128-face quantum with flips):
+    // plans for 128 rows and half the max batch too - a tile chosen for 512 rows runs 256 at half a
+    // round (7x7x512: 248 vs 185 us, profiles/r05n_sx_tile_sweep.txt). Their convs keep the one K
+    // order of every class (the fused tiles' K-row width is fixed per conv), so results stay bit-identical.
+    bool has_split = false;
+    for (auto& t : n->tens) has_split = has_split || t.split;
+    if (has_split && max_batch >= 256)
+      for (int b : {128, max_batch / 2})
+        if (b > n->cls_batch.back()) n->cls_batch.push_back(b);
+  }
   n->plans_cls.assign(n->cls_batch.size(), std::vector<ConvPlan>(n->ops.size()));
   n->stems.resize(n->ops.size());
   size_t part = 0, stem_col_bytes = 0;
@@ -1401,7 +1414,7 @@ extern "C" int pc_net_create(pc_ctx* c, const void* prog, size_t nbytes, int pre
       // tile choice: the max-batch tiles would leave most CUs idle
       for (size_t c = 0; c < n->cls_batch.size() && rc == PC_OK; ++c) {
         ConvPlan& sp = n->plans_cls[c][i];
-        rc = plan_conv(n, op, sp, n->cls_batch[c], true);
+        rc = plan_conv(n, op, sp, n->cls_batch[c], n->cls_batch[c] <= 64);
         if (rc == PC_OK && sp.splitk > 1)
           part = std::max(part, (size_t)((long long)sp.splitk * sp.M_per_image * n->cls_batch[c] * op.w[14] * 4));
       }
