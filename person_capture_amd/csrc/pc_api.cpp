@@ -1457,8 +1457,8 @@ extern "C" int pc_net_create(pc_ctx* c, const void* prog, size_t nbytes, int pre
   n->wfrag.assign(n->ops.size(), nullptr);
   for (size_t i = 0; i < n->ops.size() && rc == PC_OK; ++i) {
     if (n->ops[i].w[0] != OP_CONV) continue;
-    bool wg = n->plans[i].wg;
-    for (auto& pc : n->plans_cls) wg = wg || pc[i].wg;
+    bool wg = n->plans[i].wg || n->plans[i].hx;   // (the halo-staged kernel reads the same copy)
+    for (auto& pc : n->plans_cls) wg = wg || pc[i].wg || pc[i].hx;
     if (wg) rc = pack_wfrag(n, n->ops[i], reinterpret_cast<const float*>(n->host_arrays[n->ops[i].w[13]]), &n->wfrag[i]);
   }
   n->host_arrays.clear();
@@ -1627,7 +1627,7 @@ static int run_ops(pc_net* n, int N, hipStream_t s) {
       p.sx = pl.sx;
       p.c8 = pl.c8;
       p.wf8s = n->wf8s[i];
-      p.wfrag = pl.wg ? n->wfrag[i] : nullptr;
+      p.wfrag = pl.wg || pl.hx ? n->wfrag[i] : nullptr;
       if (Y.c8) {
         p.yc8 = 1;
         p.ylo_mul = std::ldexp(1.f, Y.e_lo);

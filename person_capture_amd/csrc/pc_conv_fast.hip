@@ -606,7 +606,8 @@ static hipError_t launch_fast_cfg(const ConvParams& p, hipStream_t s) {
     const int nwg = (p.M + BP - 1) / BP * (p.npad / BC);
     if (p.sx) {   // fused f16x3 / f16c8 tiles: always the split epilogue
       if (p.wfrag && !p.c8) {   // weight fragments from global memory: 4 stages of pixel rows
-        if constexpr (sizeof(T) == 2 && ROWB == 64 && OCC == 1 && BC == 256 && BP == 224 && fast_wg_fits<BC, BP, WC, WP>()) {
+        if constexpr (sizeof(T) == 2 && ROWB == 64 && OCC == 1 && ((BC == 256 && BP == 224) || (BC == 128 && BP == 256)) &&
+                      fast_wg_fits<BC, BP, WC, WP>()) {
           hipLaunchKernelGGL((conv_fast<T, BC, BP, ROWB, WC, WP, 4, 1, true, true, false, true>), dim3(nwg),
                              dim3(64 * WC * WP), 0, s, p);
           return hipGetLastError();
@@ -707,6 +708,7 @@ int conv_fast_valid_sx(int cfg, int rowb) {
 int conv_fast_valid_wg(int cfg) {
   if (cfg < 0 || cfg >= kNumFastCfgs || !conv_fast_valid_sx(cfg, 64)) return 0;
   switch (cfg) {   // the instantiated WG tiles
+    case 1: return fast_wg_fits<128, 256, 2, 4>();
     case 13: return fast_wg_fits<256, 224, 4, 2>();
     default: return 0;
   }

@@ -1,27 +1,30 @@
 // Halo-staged f16x3 3x3 convolution for 64 -> 64 channel split layers (gfx950): SCRFD's
-// 160x160x64 / 80x80x64 / 40x40x64 trunk in the f16x3 detector.
+// 160x160x64 / 80x80x64 / 40x40x64 trunk in the f16x3 detector and IResNet's 56x56x64 /
+// 112x112x64 stage in the f16x3 ArcFace.
 //
 // The fused split tiles of conv_fast stage, per K tile, the hi and lo pixel rows of one tap:
-// every input pixel moves L2 -> LDS nine times, 64 KB of the 80 KB a 64x256 tile stages per
-// tap, at the 15-30 B/clk per CU an L2 -> LDS fill sustains (round 4: 15-18 % MFMA busy).
-// Here a workgroup owns a 16x16 output block of one image: it stages the block's 18x18
-// input halo (hi and lo, 256 B per pixel, 83 KB) into LDS once, and each of its four waves
-// walks the 9 taps x 2 k-steps for 4 output rows x 16 pixels x 64 channels, reading pixel
-// fragments from the halo (tap shifts are slot offsets) and W_hi / W_lo fragments from a
-// 3-tap LDS ring filled by LDS-DMA two taps ahead. Per k-step and fragment the MFMAs are conv_fast SX's:
-// W_hi*x_hi, W_lo*x_hi, W_hi*x_lo, k-steps in (tap row, tap column, 32-channel block) order.
+// every input pixel moves L2 -> LDS nine times. Here a workgroup owns a 16x12 output block of one
+// image: it stages the block's 18x14 input halo (hi and lo, 256 B per pixel, 63 KB) into LDS once,
+// and each of its four waves walks the 9 taps x 2 k-steps for 3 output rows x 16 pixels x 64
+// channels, reading pixel fragments from the halo (tap shifts are slot offsets). The W_hi / W_lo
+// fragments come from the conv's fragment-ordered weight copy (pc_api.cpp pack_wfrag) straight into
+// registers, one k-step ahead: the K loop has no barrier, and two workgroups share a CU (round 4's
+// form staged 16x16 blocks and a 3-tap weight ring through the LDS, 131 KB: one workgroup per CU).
+// Per k-step and fragment the MFMAs are conv_fast SX's: W_hi*x_hi, W_lo*x_hi, W_hi*x_lo, k-steps
+// in (tap row, tap column, 32-channel block) order.
 #include "pc_conv_common.h"
 
 namespace pc {
 
-constexpr int HX_TW = 16, HX_TH = 16, HX_PW = HX_TW + 2, HX_SLOTS = (HX_TH + 2) * HX_PW;
+constexpr int HX_TW = 16, HX_TH = 12, HX_PW = HX_TW + 2, HX_SLOTS = (HX_TH + 2) * HX_PW;
 constexpr int HX_SB = 256;                        // slot bytes: 64 hi + 64 lo f16 channels
-constexpr int HX_BYTES = HX_SLOTS * HX_SB;        // 82944 = 81 x 1 KiB
+constexpr int HX_BYTES = HX_SLOTS * HX_SB;        // 64512 = 63 x 1 KiB
+static_assert(HX_BYTES % 1024 == 0, "halo DMA pieces");
+static_assert(HX_TH * HX_TW * 68 * 4 <= HX_BYTES, "epilogue image over the halo");
 
-__global__ __launch_bounds__(256, 1) void conv_hx64(ConvParams p, int nby, int nbx) {
-  constexpr int TC = 4, TP = 4, NKS = 18;         // 64 channels, 4 rows per wave, 9 taps x 2 k-steps
+__global__ __launch_bounds__(256, 2) void conv_hx64(ConvParams p, int nby, int nbx) {
+  constexpr int TC = 4, TP = HX_TH / 4, NKS = 18;   // 64 channels, 3 rows per wave, 9 taps x 2 k-steps
   __shared__ __attribute__((aligned(16))) char halo[HX_BYTES];
-  __shared__ __attribute__((aligned(16))) char wring[3 * 16384];   // W_hi | W_lo of three taps
   const ConvSeg& S = p.seg[0];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -36,7 +39,7 @@ __global__ __launch_bounds__(256, 1) void conv_hx64(ConvParams p, int nby, int n
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)0xffffffff, 0x00020000);
   };
   const __amdgpu_buffer_rsrc_t xrs = rsrc(S.x);
-  const __amdgpu_buffer_rsrc_t wrs = rsrc(p.w);
+  const __amdgpu_buffer_rsrc_t wrs = rsrc(p.wfrag);
 
   // ---- halo: LDS byte i*1024 + lane*16 = slot s, chunk position q, holding source chunk
   // q ^ (s & 15) of input pixel (oy0 - 1 + s / 18, ox0 - 1 + s % 18); zeros outside ----
@@ -53,25 +56,19 @@ __global__ __launch_bounds__(256, 1) void conv_hx64(ConvParams p, int nby, int n
     __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)(halo + i * 1024), 16, off, 0, 0, 0);
   }
 
-  // weights: per tap, W_hi and W_lo (64 rows of 128 B each, from the [W_hi, W_hi, W_lo]-per-tap
-  // layout, 192 per tap) through a 3-slot LDS ring by LDS-DMA, two taps ahead - register loads
-  // of the same fragments by every workgroup at once ran at ~2 us per k-step (r04)
-  const int lrow = lane >> 3, lch = lane & 7;
-  auto issue_w = [&](int tap, int slot) __attribute__((always_inline)) {
-    // 16 pieces of 8 rows: pieces 0-7 W_hi rows, 8-15 W_lo rows; wave w issues pieces w, w+4, ...
+  // weight fragments of k-step s (tap s / 2, channel block s % 2): the packed K tile cb * 9 + tap,
+  // 4 row blocks x [W_hi, W_lo] x 1 KiB (lane l: row 16 a + (l & 15), channels 8 (l >> 4) .. +8)
+  auto wload = [&](f16x8* wh, f16x8* wl, int s) __attribute__((always_inline)) {
+    const int kt = (s & 1) * 9 + (s >> 1);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int pc = wave + 4 * j;
-      const int half = pc >> 3, r = (pc & 7) * 8 + lrow;   // r: output channel row
-      unsigned off = (unsigned)((long long)r * p.ktot * 2) + (unsigned)(tap * 192 + half * 128) * 2 +
-                     ((lch ^ ((r >> 1) & 7)) << 4);
-      asm volatile("" : "+v"(off));
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_ptr_t)(wring + slot * 16384 + pc * 1024), 16, off, 0, 0, 0);
+    for (int a = 0; a < TC; ++a) {
+      wh[a] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16 + (a * 2) * 1024, kt * 8192, 0));
+      wl[a] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16 + (a * 2 + 1) * 1024, kt * 8192, 0));
     }
   };
-  issue_w(0, 0);
-  issue_w(1, 1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // halo and the first two taps' weights
+  f16x8 wbh[2][TC], wbl[2][TC];
+  wload(wbh[0], wbl[0], 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the halo (and k-step 0's weights)
   __syncthreads();
   if (p.dbg & 8) return;   // tuning only (PC_CONV_DBG): staging only
 
@@ -84,54 +81,35 @@ __global__ __launch_bounds__(256, 1) void conv_hx64(ConvParams p, int nby, int n
   int bslot[TP];
 #pragma unroll
   for (int t = 0; t < TP; ++t) bslot[t] = (wave * TP + t) * HX_PW + fr;
-  const int arow_sw = (fr >> 1) & 7;   // row a*16 + fr: the swizzle depends on fr only
 
-  static_for<9>([&](auto tc) __attribute__((always_inline)) {
-    constexpr int tap = decltype(tc)::value;
+  static_for<NKS>([&](auto sc) __attribute__((always_inline)) {
+    constexpr int s = decltype(sc)::value, tap = s / 2, ks = s % 2, q = s & 1;
     constexpr int toff = (tap / 3) * HX_PW + (tap % 3);
-    if constexpr (tap > 0) {
-      // tap's weights (issued two taps ago) landed: at most one tap's pieces still in flight
-      if constexpr (tap < 8) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+    if constexpr (s + 1 < NKS) wload(wbh[q ^ 1], wbl[q ^ 1], s + 1);
+    f16x8 bh[TP], bl[TP];
+#pragma unroll
+    for (int t = 0; t < TP; ++t) {
+      const int sl = bslot[t] + toff;
+      const int sw = sl & 15;
+      bh[t] = *reinterpret_cast<const f16x8*>(halo + sl * HX_SB + (((ks * 4 + g) ^ sw) << 4));
+      bl[t] = *reinterpret_cast<const f16x8*>(halo + sl * HX_SB + (((8 + ks * 4 + g) ^ sw) << 4));
     }
-    if constexpr (tap + 2 < 9) {
-      if (!(p.dbg & 1)) issue_w(tap + 2, (tap + 2) % 3);   // dbg 1: no weight stream (tuning only)
-    }
-    const char* ws = wring + (tap % 3) * 16384;
-    static_for<2>([&](auto kc) __attribute__((always_inline)) {
-      constexpr int ks = decltype(kc)::value;
-      f16x8 wh[TC], wl[TC], bh[TP], bl[TP];
-      const unsigned ach = (unsigned)(((ks * 4 + g) ^ arow_sw) << 4);
+    if (p.dbg & 2) return;   // tuning only: no MFMAs
 #pragma unroll
-      for (int a = 0; a < TC; ++a) {
-        wh[a] = *reinterpret_cast<const f16x8*>(ws + (a * 16 + fr) * 128 + ach);
-        wl[a] = *reinterpret_cast<const f16x8*>(ws + 8192 + (a * 16 + fr) * 128 + ach);
-      }
+    for (int a = 0; a < TC; ++a)
 #pragma unroll
-      for (int t = 0; t < TP; ++t) {
-        const int s = bslot[t] + toff;
-        const int sw = s & 15;
-        bh[t] = *reinterpret_cast<const f16x8*>(halo + s * HX_SB + (((ks * 4 + g) ^ sw) << 4));
-        bl[t] = *reinterpret_cast<const f16x8*>(halo + s * HX_SB + (((8 + ks * 4 + g) ^ sw) << 4));
-      }
-      if (p.dbg & 2) return;   // tuning only: no MFMAs
+      for (int t = 0; t < TP; ++t)
+        acc[a][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wbh[q][a], bh[t], acc[a][t], 0, 0, 0);
 #pragma unroll
-      for (int a = 0; a < TC; ++a)
+    for (int a = 0; a < TC; ++a)
 #pragma unroll
-        for (int t = 0; t < TP; ++t)
-          acc[a][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[a], bh[t], acc[a][t], 0, 0, 0);
+      for (int t = 0; t < TP; ++t)
+        acc[a][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wbl[q][a], bh[t], acc[a][t], 0, 0, 0);
 #pragma unroll
-      for (int a = 0; a < TC; ++a)
+    for (int a = 0; a < TC; ++a)
 #pragma unroll
-        for (int t = 0; t < TP; ++t)
-          acc[a][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[a], bh[t], acc[a][t], 0, 0, 0);
-#pragma unroll
-      for (int a = 0; a < TC; ++a)
-#pragma unroll
-        for (int t = 0; t < TP; ++t)
-          acc[a][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[a], bl[t], acc[a][t], 0, 0, 0);
-    });
+      for (int t = 0; t < TP; ++t)
+        acc[a][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wbh[q][a], bl[t], acc[a][t], 0, 0, 0);
   });
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
@@ -223,7 +201,7 @@ int conv_hx_ok(const ConvParams& p) {
   return p.nseg == 1 && S.C == 128 && S.KH == 3 && S.KW == 3 && S.stride == 1 && S.pad == 1 &&
          S.H == p.OH && S.W == p.OW && p.npad == 64 && p.ysplit == 64 && p.splitk == 1 && !p.out_f32 &&
          p.ktot == 9 * 192 && p.res_mode != RES_UP2 && (p.res_mode == RES_NONE || (p.rsplit == 64 && p.rcs % 8 == 0)) &&
-         p.ycs % 8 == 0 && p.cwrite == 64;
+         p.ycs % 8 == 0 && p.cwrite == 64 && p.wfrag != nullptr;
 }
 
 hipError_t conv_hx_launch(const ConvParams& p, hipStream_t s) {
