@@ -533,8 +533,8 @@ def dominant_conv(nets, names, programs=None, precisions=None) -> dict:
     prec = (precisions or {}).get(name, "f16")
     label = ""
     if code == 113:
-        label = (" = conv_fast<f16,256,224,64,4,2,2,1,SPLIT,SX> (fused f16x3 split tile, 64-byte K rows; "
-                 "ArcFace 14x14x256 layers)" if prec == "f16x3" else
+        label = (" = conv_fast<f16,256,224,64,4,2,4,1,SPLIT,SX,-,WG> (fused f16x3 split tile, 64-byte K rows, "
+                 "weight fragments in registers; ArcFace 14x14x256 layers)" if prec == "f16x3" else
                  " = conv_fast<f16,256,224,128,4,2,2,1> (ArcFace 14x14x256 layers)" if prec == "f16" else "")
     out = {"kernel": f"{_kernel_of(code, cfg)} in {name}" + label, "precision": prec, "peak_tflops": _peak_for(prec),
            "code": code, "launches": cnt, "avg_us": round(ms * 1e3 / cnt, 2), "flops_per_launch": round(fl / cnt),
@@ -573,8 +573,17 @@ def _traffic_for(dominant, code, prec="f16"):
         return None
     bc, bp = FAST_TILES.get(code % 100, (0, 0))
     name = dominant.get("kernel", "")
-    flags = "Lb1ELb1ELb1E" if code >= 600 else "Lb1ELb1ELb0E" if prec == "f16x3" else "ELb0ELb0E"
-    if f"Li{bc}ELi{bp}E" not in name or not name.endswith(flags + "EEvNS_10ConvParamsE"):
+    # template flags after OCC: SPLIT, SX, C8 [, WG]
+    tail = name.split(f"Li{bc}ELi{bp}E", 1)[-1] if f"Li{bc}ELi{bp}E" in name else None
+    if tail is None:
+        return None
+    if code >= 600:
+        ok = "Lb1ELb1ELb1E" in tail
+    elif prec == "f16x3":
+        ok = "Lb1ELb1ELb0E" in tail
+    else:
+        ok = "ELb1ELb1E" not in tail
+    if not ok:
         return None
     return dominant.get("hbm_bytes_per_launch")
 
