@@ -56,6 +56,20 @@ _CTX_CACHE: Dict[int, GpuContext] = {}
 _WEIGHT_CACHE: Dict[Tuple[str, int], models.Params] = {}
 
 
+class _IBox(tuple):
+    """An integer face box (x1, y1, x2, y2) that keeps the detector's float box it was truncated
+    from (`f`, reported with the debug chips: parity reports locate one-pixel box differences
+    between precisions at the int() of _accumulate, face_embedder.py:2214-2239)."""
+
+    def __new__(cls, box, f=None):
+        t = super().__new__(cls, box)
+        t.f = None if f is None else np.asarray(f, np.float64).copy()
+        return t
+
+    def __reduce__(self):
+        return (_IBox, (tuple(self), self.f))
+
+
 def _round32(x: int) -> int:
     return ((int(x) + 31) // 32) * 32
 
@@ -897,7 +911,8 @@ class FaceEmbedder(YoloFaceBranch):
         off = np.stack([xa1, ya1], axis=1).astype(np.float64)[:, None, :]
         pts = (kp.astype(np.float64) - off).astype(np.float32)
         sc = bb[:, 4].astype(np.float64)
-        return [((int(xa1[i]), int(ya1[i]), int(xa2[i]), int(ya2[i])), pts[i], float(sc[i])) for i in keep]
+        return [(_IBox((int(xa1[i]), int(ya1[i]), int(xa2[i]), int(ya2[i])), bb[i, :4]), pts[i], float(sc[i]))
+                for i in keep]
 
     def _scrfd_policy(self, im: _DevImage, dyn: int, first) -> List[tuple]:
         """face_embedder.py:2205-2443: from the 0-degree result through fallbacks to the
@@ -928,7 +943,10 @@ class FaceEmbedder(YoloFaceBranch):
                     mapped.append([float(ox - xa1), float(oy - ya1)])
                 pts = np.asarray(mapped[:5], dtype=np.float32) if len(mapped) >= 5 else None
             score = float(bb[4]) if len(bb) > 4 else 1.0
-            dets.append(((xa1, ya1, xa2, ya2), pts, score))
+            fb = None
+            if deg == 0:   # (the float box of an unrotated pass, for parity reports)
+                fb = np.asarray(bb[:4], np.float64)
+            dets.append((_IBox((xa1, ya1, xa2, ya2), fb), pts, score))
 
         bboxes, kpss = first
         if kpss is not None and len(kpss) == len(bboxes) and np.ndim(kpss) == 3 and np.shape(kpss)[1:] == (5, 2) \
@@ -1080,15 +1098,18 @@ class FaceEmbedder(YoloFaceBranch):
     # ------------------------------------------------------------------ align + embed
     @staticmethod
     def _face_jobs(im: _DevImage, fi: int, kept: list) -> List[tuple]:
-        """Integer crop boxes of the kept detections (face_embedder.py:2445-2452)."""
+        """Integer crop boxes of the kept detections (face_embedder.py:2445-2452), with the float
+        box they are rounded from (parity reports: a box that differs by one pixel between two
+        precisions has its float coordinate next to a .5)."""
         H0, W0 = im.H, im.W
         out = []
-        for (x1, y1, x2, y2), kps, _sc in kept:
+        for box, kps, _sc in kept:
+            x1, y1, x2, y2 = box
             xi1 = max(0, min(W0 - 1, int(round(x1))))
             yi1 = max(0, min(H0 - 1, int(round(y1))))
             xi2 = max(xi1 + 1, min(W0, int(round(x2))))
             yi2 = max(yi1 + 1, min(H0, int(round(y2))))
-            out.append((fi, (xi1, yi1, xi2, yi2), kps))
+            out.append((fi, (xi1, yi1, xi2, yi2), kps, getattr(box, "f", None)))
         return out
 
     def _do_flip(self) -> bool:
@@ -1179,7 +1200,7 @@ class FaceEmbedder(YoloFaceBranch):
     def _embed_collect(self, pend: tuple, out: List[list]) -> None:
         fence, jobs, q, feats, fd, chip_h = pend
         fence.wait()
-        for j, (fi, (x1, y1, x2, y2), kps) in enumerate(jobs):
+        for j, (fi, (x1, y1, x2, y2), kps, fbox) in enumerate(jobs):
             face = {'bbox': np.array([x1, y1, x2, y2], dtype=np.int32), 'feat': feats[j].copy(),
                     'quality': float(q[j])}
             if fd is not None:
@@ -1187,6 +1208,8 @@ class FaceEmbedder(YoloFaceBranch):
             if chip_h is not None:   # parity tests: the aligned chip and its landmarks
                 face['chip'] = chip_h[j].copy()
                 face['kps5'] = None if kps is None else np.asarray(kps, np.float32).copy()
+                if fbox is not None:
+                    face['bbox_f'] = fbox
             out[fi].append(face)
 
     def _resize_chip(self, crop: _DevImage, d_dst: int) -> None:
