@@ -222,7 +222,7 @@ int pc_net_profile(pc_net* net, int enable);
 int pc_net_calibrate(pc_net* net, const void* d_in, int N, int headroom_log2, float* h_absmax);
 int pc_net_profile_read(pc_net* net, double* h_out5);
 /* Per-launch detail of the profiled runs, 6 doubles per record: op index, op kind, ms, FLOPs,
-   kernel (100+k: static-schedule tile k, 600+k: its f16c8 form, 200+v: t2d variant v, 300: resident chain, 500: halo-staged f16x3, k >= 0: halo tile k, -1: generic implicit-GEMM), implicit-GEMM tile (static-schedule tiles: their form, 0 plain, 1 fused split, 3 fused split with register weight fragments). Returns the record count (<0: -status). */
+   kernel (100+k: static-schedule tile k, 600+k: its f16c8 form, 200+v: t2d variant v, 300: resident chain, 500: halo-staged f16x3, k >= 0: halo tile k, -1: generic implicit-GEMM), implicit-GEMM tile (static-schedule tiles: their form, bit 0 fused split, bit 1 register weight fragments, bit 2 128-byte K rows). Returns the record count (<0: -status). */
 int pc_net_profile_ops(pc_net* net, double* h_out, int max_recs);
 
 /* ---- image kernels ---- */

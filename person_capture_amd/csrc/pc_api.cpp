@@ -825,27 +825,6 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
       if (try_sx) {   // the same choice among the tiles that can stage fused split tiles
         int bsx = -1, bsx_rowb = rowb;
         double bsx_t = 0;
-        // fused tiles walk K channel-block-major (each block through every tap, pc_conv_fast.hip
-        // advance), so the K-row width orders the accumulation: ONE width per conv for every
-        // plan class - the width of the tile the full-batch plan picks
-        int sx_rb = 64;
-        {
-          const long long Mfull = Mimg * n->max_batch;
-          double bt = 0;
-          bool found = false;
-          for (int k = 0; k < conv_fast_num_cfgs(); ++k) {
-            int bc = 0, bp = 0;
-            conv_fast_tile(k, &bc, &bp);
-            if ((k >= kFastSmallCfg0 && k <= kFastSmallCfg1) || npad % bc) continue;
-            for (int rb : {rowb, 64}) {
-              if (!conv_fast_valid_sx(k, rb)) continue;
-              const long long t = (Mfull + bp - 1) / bp * (npad / bc);
-              const double est = (double)((t + 255) / 256) * bc * bp * sxcost(k);
-              if (!found || est < bt) { found = true; bt = est; sx_rb = rb; }
-              break;
-            }
-          }
-        }
         for (int k = 0; k < conv_fast_num_cfgs(); ++k) {
           int bc = 0, bp = 0;
           conv_fast_tile(k, &bc, &bp);
@@ -856,7 +835,6 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
             // net (kC8Rowb; PC_C8_ROWB for tuning): the row width orders the f16 and block-scaled
             // MFMAs of a K tile, so a conv's output would otherwise depend on its batch class
             if (in_c8 && (!conv_fast_valid_c8(k, rb) || rb != c8_rowb())) continue;
-            if (!in_c8 && rb != sx_rb && force <= 0) continue;
             if (!conv_fast_valid_sx(k, rb)) continue;
             const long long t = (M + bp - 1) / bp * (npad / bc);
             const double est = (double)((t + 255) / 256) * bc * bp * sxcost(k);
@@ -1156,8 +1134,9 @@ static uint8_t e4m3_encode(float v) {
   return sgn | (uint8_t)(((E + 7) << 3) | (q - 8));
 }
 
-// Fragment-ordered copy of a fused f16x3 conv's weights (conv_fast WG): K tiles of 32 channels in the
-// fused tiles' channel-block-major order (segment, hi channel block, tap row, tap column); per tile
+// Fragment-ordered copy of a fused f16x3 conv's weights (conv_fast WG, conv_hx64): K tiles of 32
+// channels in the fused tiles' order at 64-byte rows (segment, group of 64 hi channels, tap row, tap
+// column, 32-channel block; ConvSeg::gt); per tile
 // npad / 16 row blocks of [W_hi, W_lo] fragments, each 64 lanes x 8 f16 (lane l: row l & 15,
 // channels 8 (l >> 4) .. +8), so a wave's fragment read is one contiguous KiB.
 static int pack_wfrag(pc_net* n, const NetOp& op, const float* wf, void** out) {
@@ -1178,9 +1157,11 @@ static int pack_wfrag(pc_net* n, const NetOp& op, const float* wf, void** out) {
   k0 = 0;
   for (int sg = 0; sg < w[2]; ++sg) {
     const int cp = n->tens[w[3 + 5 * sg]].C / 2, KH = w[4 + 5 * sg], KW = w[5 + 5 * sg];
-    for (int cb = 0; cb < cp / 32; ++cb)
+    const int gt = cp % 64 == 0 ? 2 : 1;   // the fused tiles' channel groups at 64-byte K rows
+    for (int g0 = 0; g0 < cp / 32; g0 += gt)
       for (int th = 0; th < KH; ++th)
-        for (int tw = 0; tw < KW; ++tw, ++kt) {
+        for (int tw = 0; tw < KW; ++tw)
+          for (int cb = g0; cb < g0 + gt; ++cb, ++kt) {
           const long long kbase = k0 + (long long)(th * KW + tw) * 3 * cp + cb * 32;
           for (int rb = 0; rb < npad / 16; ++rb)
             for (int hf = 0; hf < 2; ++hf)
@@ -1594,6 +1575,8 @@ static int run_ops(pc_net* n, int N, hipStream_t s) {
         if (X.split && pl.sx) {   // fused split tiles: the hi blocks; lo block = hi block + vwrap
           S.cblk = S.cblk / 2;
           S.vwrap = S.cblk;
+          // channel groups of 64 hi channels where they divide the channels (ConvSeg::gt)
+          S.gt = (X.C / 2) % 64 == 0 ? 64 / bke : 1;
         } else if (X.split) {     // virtual channel blocks [hi, lo, hi] (pc_common.h ConvSeg::vwrap)
           S.vwrap = S.cblk;
           S.cblk = S.cblk / 2 * 3;
@@ -1838,7 +1821,7 @@ extern "C" int pc_net_profile_read(pc_net* n, double* out) {
 }
 
 // Per-record detail of the profiled runs: 6 doubles per record
-// [op index, kind, ms, flops, kernel (100+k fast tile k, 200+v t2d variant v, 300 resident chain, 500 halo-staged f16x3, k halo tile k, -1 igemm), igemm cfg or the conv_fast form: 0 plain, 1 fused split, 3 fused split with register weight fragments]; returns the count.
+// [op index, kind, ms, flops, kernel (100+k fast tile k, 200+v t2d variant v, 300 resident chain, 500 halo-staged f16x3, k halo tile k, -1 igemm), igemm cfg or the conv_fast form: bit 0 fused split, bit 1 register weight fragments, bit 2 128-byte K rows]; returns the count.
 extern "C" int pc_net_profile_ops(pc_net* n, double* out, int max_recs) {
   if (!n || !out) return -PC_ERR_ARG;
   HIPCHK(n->ctx, hipStreamSynchronize(n->ctx->stream));
@@ -1858,10 +1841,10 @@ extern "C" int pc_net_profile_ops(pc_net* n, double* out, int max_recs) {
                                  : pl->fast >= 0   ? 100 + pl->fast
                                                    : pl->halo)
                               : -1;
-    // [5]: the generic kernel's tile cfg; for conv_fast launches its form: 1 fused split (SX), 3 SX
-    // with register weight fragments (WG), 0 plain
+    // [5]: the generic kernel's tile cfg; for conv_fast launches its form: bit 0 fused split (SX),
+    // bit 1 register weight fragments (WG), bit 2 128-byte K rows
     const bool fastk = conv && r.code < 0 && !pl->hx && pl->t2d < 0 && pl->fast >= 0;
-    o[5] = !conv ? -1 : fastk ? (pl->sx ? 1 : 0) + (pl->wg ? 2 : 0) : pl->cfg;
+    o[5] = !conv ? -1 : fastk ? (pl->sx ? 1 : 0) + (pl->wg ? 2 : 0) + (pl->rowb == 128 ? 4 : 0) : pl->cfg;
   }
   return k;
 }

@@ -37,6 +37,11 @@ struct ConvSeg {
   // e4m3 bytes [lo8 x 32 | hi8 x 32]; f8s = E8M0 exponents of their scales, lo | hi << 8
   // (true lo = lo8 * 2^(e_lo - 127))
   int f8s;
+  // fused split tiles (conv_fast SX): K tiles per channel group. The K loop walks channel groups of
+  // 64 hi channels (32 where the channels are not a multiple of 64): every tap of a group, then the
+  // next group - the same accumulation order at 64- and 128-byte K rows (gt 2 or 1 tiles per group
+  // and tap), so every plan class of a conv may pick its own row width
+  int gt;
 };
 
 struct ConvParams {
@@ -79,9 +84,10 @@ struct ConvParams {
   // hi8 = e4m3(hi * yhi_mul); residual: hi + lo8 * rlo_inv
   int yc8, rc8;
   float ylo_mul, yhi_mul, rlo_inv;
-  // fused f16x3 tiles, WG form (conv_fast): the weights in fragment order, per K tile (the SX
-  // channel-block-major order) x 16-row block x [W_hi, W_lo] x 64 lanes x 8 f16 (lane l: row l & 15,
-  // channels 8 (l >> 4) .. +8 of the tile's 32); null: the weights are staged from w
+  // fused f16x3 tiles, WG form (conv_fast) and the halo-staged kernel: the weights in fragment
+  // order, per 32-channel K tile (the SX channel-group order at 64-byte rows) x 16-row block x
+  // [W_hi, W_lo] x 64 lanes x 8 f16 (lane l: row l & 15, channels 8 (l >> 4) .. +8 of the tile's 32);
+  // null: the weights are staged from w
   const void* wfrag;
 };
 

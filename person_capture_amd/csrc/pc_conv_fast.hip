@@ -187,25 +187,34 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
   };
   // advance the issue iterator by one K-tile (no-op once the last tile was issued).
   // Plain tiles walk K tap-major (channel block fastest: the K order the chain / t2d kernels share
-  // bit for bit). Fused split tiles walk it channel-block-major (the 9 taps of one [hi | lo] block,
-  // then the next block): a tap-major pass re-reads the tile's whole split pixel rows per tap, which
-  // at 256x224 and 512 split channels (229 KB per workgroup, 7 MB per XCD) no longer fits the L2 -
-  // every tap went back to HBM (r05 profile: 650 MB fetched per 14x14x256 launch, 2.8x the tensor)
+  // bit for bit). Fused split tiles walk it channel-group-major (the 9 taps of one group of 64 hi
+  // channels - with its lo half - then the next group): a tap-major pass re-reads the tile's whole
+  // split pixel rows per tap, which at 256x224 and 512 split channels (229 KB per workgroup, 7 MB
+  // per XCD) no longer fits the L2 - every tap went back to HBM (r05 profile: 650 MB fetched per
+  // 14x14x256 launch, 2.8x the tensor). Within a group and tap the tiles are in channel order, so
+  // 64- and 128-byte K rows accumulate in the same order (ConvSeg::gt).
+  int igt = 0;   // tile within the current group and tap
+  int sgt = p.seg[0].gt > 0 ? p.seg[0].gt : 1;
   auto advance = [&](bool more) __attribute__((always_inline)) {
     if (!more) return;
     if constexpr (SX) {
-      const int tw1 = itw + 1;
+      const int g1 = igt + 1;
+      const bool w0 = g1 == sgt;
+      igt = w0 ? 0 : g1;
+      icb += w0 ? 1 - sgt : 1;   // back to the group's first tile at the next tap
+      const int tw1 = itw + (w0 ? 1 : 0);
       const bool w1 = tw1 == sKW;
       itw = w1 ? 0 : tw1;
       const int th1 = ith + (w1 ? 1 : 0);
       const bool w2 = th1 == sKH;
       ith = w2 ? 0 : th1;
-      icb += w2 ? 1 : 0;
+      icb += w2 ? sgt : 0;        // next group
       if (iseg == 0 && icb == seg0_cb) {   // once per launch, 2-segment convs only
         iseg = 1;
         icb = 0;
         swk = swk1;
         sKH = p.seg[1].KH;
+        sgt = p.seg[1].gt > 0 ? p.seg[1].gt : 1;
         load_seg(p.seg[1]);
       }
     } else {

@@ -56,10 +56,11 @@ __global__ __launch_bounds__(256, 2) void conv_hx64(ConvParams p, int nby, int n
     __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)(halo + i * 1024), 16, off, 0, 0, 0);
   }
 
-  // weight fragments of k-step s (tap s / 2, channel block s % 2): the packed K tile cb * 9 + tap,
+  // weight fragments of k-step s (tap s / 2, channel block s % 2): packed K tile s (the fused tiles'
+  // channel-group order: one group of 64 channels, every tap, its two 32-channel blocks per tap),
   // 4 row blocks x [W_hi, W_lo] x 1 KiB (lane l: row 16 a + (l & 15), channels 8 (l >> 4) .. +8)
   auto wload = [&](f16x8* wh, f16x8* wl, int s) __attribute__((always_inline)) {
-    const int kt = (s & 1) * 9 + (s >> 1);
+    const int kt = s;
 #pragma unroll
     for (int a = 0; a < TC; ++a) {
       wh[a] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16 + (a * 2) * 1024, kt * 8192, 0));

@@ -3,7 +3,9 @@ the tiles planned for its batch class (1 / 4 / 16 / 32 / 64 images, up to a quar
 max_batch) - including the deep-ring small conv_fast tiles 15-19 that only those plans use.
 Tile shape, ring depth and K-row width do not change any output's K order, so the same rows must come out
 bit for bit as inside a large batch (the max-batch plans): extract() and extract_batch() are
-bit-identical by contract (test_gpu_face_embedder). The f16x3 split program too."""
+bit-identical by contract (test_gpu_face_embedder). The f16x3 split program too: its fused split
+tiles walk K in channel groups of 64 (every tap of a group, then the next group), an order that
+64- and 128-byte K rows share, so its classes pick their row widths freely - and do."""
 import numpy as np
 import pytest
 
@@ -14,11 +16,14 @@ from person_capture_amd.runtime import Net
 pytestmark = pytest.mark.gpu
 
 
-def _run(ctx, net, x, N, outs):
+def _run(ctx, net, x, N, outs, forms=None):
     d = ctx.upload(np.ascontiguousarray(x[:N]))
     net.profile(True)
     net.run(d.ptr, N)
-    codes = [int(r[4]) for r in net.profile_ops()]
+    recs = net.profile_ops()
+    codes = [int(r[4]) for r in recs]
+    if forms is not None:   # op -> (kernel code, conv_fast form bits)
+        forms.update({int(r[0]): (int(r[4]), int(r[5])) for r in recs})
     net.profile(False)
     res = [net.read_output(k, N).copy() for k in range(outs)]
     d.free()
@@ -45,15 +50,23 @@ def test_arcface_small_batches_bit_identical_to_large_batch(gpu_ctx, depth, mode
             d = gpu_ctx.upload(x)
             net.calibrate(d.ptr, 200)
             d.free()
-        (large,), _ = _run(gpu_ctx, net, x, 200, 1)
+        large_forms, rows_differ = {}, 0
+        (large,), _ = _run(gpu_ctx, net, x, 200, 1, large_forms)
         ran_small = 0
         for N in (1, 2, 5, 12, 30, 64):
-            (small,), codes = _run(gpu_ctx, net, x, N, 1)
+            small_forms = {}
+            (small,), codes = _run(gpu_ctx, net, x, N, 1, small_forms)
             ran_small += sum(1 for c in codes if 115 <= c % 500 < 120)   # conv_fast small-batch tiles (C8: 615..)
+            # fused split tiles of one conv at different K-row widths in the two classes (the
+            # channel-group K order makes them accumulate alike)
+            rows_differ += sum(1 for op, (c, f) in small_forms.items() if 100 <= c < 200 and f & 1 and
+                               op in large_forms and large_forms[op][1] & 1 and (f ^ large_forms[op][1]) & 4)
             assert small.dtype == large.dtype
             assert np.array_equal(small.view(np.uint8), large[:N].view(np.uint8)), \
                 (N, float(np.abs(small.astype(np.float64) - large[:N]).max()))
         assert ran_small >= 100, ran_small
+        if mode == "f16x3":
+            assert rows_differ > 0
     finally:
         net.close()
 
