@@ -72,7 +72,7 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
   constexpr int RING = NSTAGE * BUF;
   constexpr int EPI_MAX = OCC == 1 ? 131072 : 65536;
   constexpr int EPI = fast_epi_bytes<BC, BP, WC, WP, EPI_MAX>();
-  constexpr int TRASH = NB % NW ? NW * 1024 : 0;
+  constexpr int TRASH = (NB % NW || WG) ? NW * 1024 : 0;   // (WG: the prologue's filler DMAs too)
   constexpr int SMEM = RING + TRASH > EPI ? RING + TRASH : EPI;
   static_assert(SMEM * OCC <= 163840, "LDS");
   static_assert(WTC % 16 == 0 && WTP % 16 == 0, "wave tile");
@@ -460,30 +460,34 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
 
   // ---- prologue: tiles 0 .. NSTAGE-2 in flight ----
   int kiss = 0;   // next K-tile index the iterator points at
+  // WG: every step issues NI DMAs and then 2 TC weight loads; the prologue keeps that pattern (2 TC
+  // filler DMAs into the trash rows after each of its tile DMAs, tile 0's weights after the last),
+  // so every step waits for the same count of younger loads, (NSTAGE-2) (NI + 2 TC) + 2 TC
+  constexpr int WGL = WG ? 2 * TC : 0;
   static_for<NSTAGE - 1>([&](auto jc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
     issue(std::integral_constant<int, j>{}, kiss);
     const bool more = kiss + 1 < nk;
     advance(more);
     kiss += more ? 1 : 0;
+    if constexpr (WG) {
+      if constexpr (j + 2 < NSTAGE) {
+        static_for<WGL>([&](auto) __attribute__((always_inline)) {
+          unsigned off = b_zero;
+          asm volatile("" : "+v"(off));
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)(smem + RING + wave * 1024), 16, off, 0, 0, 0);
+        });
+      } else {   // tile 0's weight fragments
+        wg_load(wgl, 0, std::integral_constant<int, 1>{});
+        wg_load(wgh, 0, std::integral_constant<int, 0>{});
+      }
+    }
   });
-  if constexpr (WG) {   // tile 0's weight fragments, behind the prologue's DMAs
-    wg_load(wgl, 0, std::integral_constant<int, 1>{});
-    wg_load(wgh, 0, std::integral_constant<int, 0>{});
-  }
   int it = 0;
-  // one step: retire tile `it`, refill the slot of tile it-1 with tile it+NSTAGE-1.
-  // WG: the 2 TC weight loads of step k follow its DMA, so NI + 2 TC loads per step are issued
-  // after tile it's DMAs (NI in the prologue, where tile 0's weights come once after all DMAs):
-  // step j of the first round waits for (NSTAGE-2) NI + 2 TC (j + 1) younger loads, later steps
-  // for (NSTAGE-2) (NI + 2 TC) + 2 TC
-  constexpr int WGL = WG ? 2 * TC : 0;
-  auto step = [&](auto jc, auto firstc) __attribute__((always_inline)) {
+  // one step: retire tile `it`, refill the slot of tile it-1 with tile it+NSTAGE-1
+  auto step = [&](auto jc, auto) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
-    constexpr bool first = decltype(firstc)::value;
-    constexpr int steady = (NSTAGE - 2) * (NI + WGL) + WGL;
-    constexpr int early = (NSTAGE - 2) * NI + WGL * (j + 1);
-    constexpr int wcnt = first && early < steady ? early : steady;
+    constexpr int wcnt = (NSTAGE - 2) * (NI + WGL) + WGL;
     static_assert(wcnt <= 63, "vmcnt range");
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(wcnt) : "memory");
     bar();
@@ -494,29 +498,12 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
     if (!(p.dbg & 2)) compute(std::integral_constant<int, j>{}, it + j);
   };
   if (p.dbg & 8) return;   // tuning only: prologue only
-  using first_t = std::integral_constant<bool, true>;   // only WG's early waits differ
   using later_t = std::integral_constant<bool, false>;
-  if constexpr (WG) {   // the first round of steps peeled (its own wait counts)
-    if (it + NSTAGE <= nk) {
-      static_for<NSTAGE>([&](auto jc) __attribute__((always_inline)) { step(jc, first_t{}); });
-      it += NSTAGE;
-      for (; it + NSTAGE <= nk; it += NSTAGE)
-        static_for<NSTAGE>([&](auto jc) __attribute__((always_inline)) { step(jc, later_t{}); });
-      static_for<NSTAGE - 1>([&](auto jc) __attribute__((always_inline)) {
-        if (it + decltype(jc)::value < nk) step(jc, later_t{});
-      });
-    } else {
-      static_for<NSTAGE - 1>([&](auto jc) __attribute__((always_inline)) {
-        if (it + decltype(jc)::value < nk) step(jc, first_t{});
-      });
-    }
-  } else {   // (the peeled form cost the plain f16 256x224 tile 120 -> 187 us per launch, r05s)
-    for (; it + NSTAGE <= nk; it += NSTAGE)
-      static_for<NSTAGE>([&](auto jc) __attribute__((always_inline)) { step(jc, later_t{}); });
-    static_for<NSTAGE - 1>([&](auto jc) __attribute__((always_inline)) {
-      if (it + decltype(jc)::value < nk) step(jc, later_t{});
-    });
-  }
+  for (; it + NSTAGE <= nk; it += NSTAGE)
+    static_for<NSTAGE>([&](auto jc) __attribute__((always_inline)) { step(jc, later_t{}); });
+  static_for<NSTAGE - 1>([&](auto jc) __attribute__((always_inline)) {
+    if (it + decltype(jc)::value < nk) step(jc, later_t{});
+  });
 
   // drain the (dummy) tail DMAs and every wave's last reads before the LDS is reused
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
