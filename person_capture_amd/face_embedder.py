@@ -1148,7 +1148,7 @@ class FaceEmbedder(YoloFaceBranch):
                 resize_jobs.extend(int(j) for j in np.asarray(aligned_idx)[~ok])
         for j in range(m):
             if not valid[j]:
-                fi, box, kps = jobs[j]
+                fi, box, kps = jobs[j][:3]
                 if kps is not None:
                     self._upright_by_eye_roll(imgs[fi], box, kps, chips.ptr + j * chip_sz, warps, resize_jobs, j)
                 else:
@@ -1166,7 +1166,7 @@ class FaceEmbedder(YoloFaceBranch):
             check(ctx.lib.pc_warp_affine(ctx.handle, arr.ctypes.data_as(C.POINTER(WarpDesc)), len(arr)),
                   ctx.handle, "warp_affine")
         for j in resize_jobs:
-            fi, (xi1, yi1, xi2, yi2), _ = jobs[j]
+            fi, (xi1, yi1, xi2, yi2), _ = jobs[j][:3]
             im = imgs[fi]
             crop = _DevImage(im.ptr + yi1 * im.stride + xi1 * 3, yi2 - yi1, xi2 - xi1, im.stride)
             self._resize_chip(crop, chips.ptr + j * chip_sz)
