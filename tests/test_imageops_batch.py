@@ -86,3 +86,21 @@ def test_resize_plan_dispatch():
     assert p["kind"] == "area" and (p["new_w"], p["new_h"]) == (960, 540) and p["scale_x"] == 1 / 0.75
     # scale is 1/(new/old), which can differ from old/new in the last bit
     assert resize_plan(130, 130, (112, 112), area=True)["scale_x"] == 1.0 / (112 / 130)
+
+
+def test_accumulate0_boxes_keep_their_float_source():
+    """The int boxes of _accumulate0 are plain 4-tuples to every consumer (equality, unpacking,
+    pickling across the pre-scan shard gather) and carry the detector's float box (`f`) that the
+    parity reports use to locate one-pixel box differences at the int() boundary."""
+    import pickle
+    from person_capture_amd.face_embedder import FaceEmbedder, _IBox
+    bb = np.array([[10.7, 20.2, 80.9, 99.99, 0.9]], np.float32)
+    kp = np.zeros((1, 5, 2), np.float32)
+    (box, _pts, _sc), = FaceEmbedder._accumulate0(bb, kp, 1920, 1080)
+    assert box == (10, 20, 80, 99) and isinstance(box, tuple) and tuple(box) == (10, 20, 80, 99)
+    assert np.allclose(box.f, bb[0, :4])
+    x1, y1, x2, y2 = box
+    assert (x1, y1, x2, y2) == (10, 20, 80, 99)
+    c = pickle.loads(pickle.dumps(box))
+    assert c == box and np.array_equal(c.f, box.f)
+    assert _IBox((1, 2, 3, 4)).f is None
