@@ -305,7 +305,10 @@ class FaceEmbedder(YoloFaceBranch):
         two = self.detector_backend == "scrfd" and os.getenv("PERSON_CAPTURE_AMD_EMBED_STREAM", "1") != "0"
         self._ectx = get_context(self._device_index, "embed") if two else self._ctx
         if two and "PERSON_CAPTURE_AMD_EMBED_QUANTUM" not in os.environ:
-            self._embed_quantum = 128
+            # (the f32-class ArcFace is ~3x the work of the f16 one and outweighs SCRFD: a full round
+            # of its tiles, 146 faces, leads - C3 r05: 912 / 908 vs 904 / 902 frames/s with 128,
+            # 824 with 192, 858 with 112, profiles/r05ae_embed_quantum_sweep.txt)
+            self._embed_quantum = 128 if self.arc_precision == PC_PREC_F16 else 146
         # host frames (extract / extract_batch without dev_frames) reach the device through the
         # native pinned staging ring on a copy stream of their own (pc_frame_stage)
         self._h2d = get_context(self._device_index, "h2d")
