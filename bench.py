@@ -462,6 +462,8 @@ def _kernel_of(code: float, cfg: float) -> str:
         return f"conv_fast C8 tile cfg {c - 600} (f16c8, pc_conv_fast.hip kFastCfgs)"
     if c == 500:
         return "conv_hx64 (halo-staged f16x3, pc_conv_hx.hip)"
+    if c == 501:
+        return "conv_hxg<96,96,5> (halo-staged f16x3 per 32-channel group, pc_conv_hx.hip)"
     if c >= 200:
         return f"conv_t2d (2-D block kernel, variant {c - 200})"
     if c >= 100:
@@ -477,8 +479,12 @@ def _net_roof(name, p_, steps, fe):
     tf = p_["conv_flops"] / (p_["conv_ms"] * 1e-3) / 1e12 if p_["conv_ms"] > 0 else None
     r = {"conv_ms_per_step": round(p_["conv_ms"] / steps, 3), "tflops": round(tf, 1) if tf else None}
     prec = getattr(fe, "arc_precision", None) if name == "arcface" else getattr(fe, "det_precision", None)
-    if prec == 2 and tf:   # PC_PREC_F16X3
-        r.update(dtype="f16x3", mfma_tflops=round(3 * tf, 1), mfma_frac=round(3 * tf / PEAK_F16_TFLOPS, 4))
+    pn = _prec_name(prec)
+    if tf:
+        r.update(dtype=pn, frac=round(tf / _peak_for(pn), 4))
+        if _issue_factor(pn) != 1.0:
+            r.update(mfma_tflops=round(_issue_factor(pn) * tf, 1),
+                     mfma_frac=round(_issue_factor(pn) * tf / _peak_for(pn), 4))
     return r
 
 
@@ -509,11 +515,35 @@ def _prec_name(prec) -> str:
 
 
 def _peak_for(prec_name: str) -> float:
-    """Dense MFMA roofline of a conv kernel in algorithmic FLOPs: f16x3 issues 3 f16 MFMAs per
-    product (a third of dense f16); f16c8 2 f16 + 1 block-scaled e4m3 MFMA per 64-channel K tile
-    where f16 takes 2 (x 2/3, at the e4m3 instruction's measured equal issue time)."""
-    return {"f16": PEAK_F16_TFLOPS, "f16x3": PEAK_F16_TFLOPS / 3,
-            "f16c8": PEAK_F16_TFLOPS * 2 / 3}.get(prec_name, PEAK_F32_TFLOPS)
+    """Dense MFMA peak a conv's ALGORITHMIC FLOPs are priced against: the f16 matrix
+    rate (2.5 PF/s) for every form that runs on the f16 MFMA - f16, and the f32-class f16x3 / f16c8,
+    whose extra correction MFMAs are overhead, not work - and the f32 rate for f32."""
+    return PEAK_F32_TFLOPS if prec_name == "f32" else PEAK_F16_TFLOPS
+
+
+def _issue_factor(prec_name: str) -> float:
+    """MFMA work issued per algorithmic FLOP: f16x3 issues 3 f16 MFMAs per product (DESIGN.md §3.6);
+    f16c8 2 f16 + 1 block-scaled e4m3 MFMA (of equal issue time) per 64-channel K tile where f16
+    takes 2, i.e. 1.5x. `issued_mfma_frac` = frac x this: how busy the matrix pipe is."""
+    return {"f16x3": 3.0, "f16c8": 1.5}.get(prec_name, 1.0)
+
+
+def _dtype_label(fe) -> str:
+    """Top-level dtype of a FaceEmbedder run: the arithmetic both nets compute in ("f16x3" when both
+    run split), or "det/arcface" when they differ."""
+    d, a = _prec_name(fe.det_precision), _prec_name(fe.arc_precision)
+    return a if d == a else f"{d} (SCRFD) / {a} (ArcFace)"
+
+
+def _precision_env(prec: str) -> None:
+    """--precision of a FaceEmbedder workload (C3/C4/C5) -> the FaceEmbedder's variables: f16 = the
+    timed mode (both nets' defaults), f32 = the parity mode, f16x3 / f16c8 = the timed mode with
+    ArcFace in that form (PERSON_CAPTURE_AMD_ARC_PRECISION; the detector stays f16x3)."""
+    if prec in ("f16x3", "f16c8"):
+        os.environ.setdefault("PERSON_CAPTURE_AMD_PRECISION", "f16")
+        os.environ.setdefault("PERSON_CAPTURE_AMD_ARC_PRECISION", prec)
+    else:
+        os.environ.setdefault("PERSON_CAPTURE_AMD_PRECISION", prec)
 
 
 def dominant_conv(nets, names, programs=None, precisions=None) -> dict:
@@ -547,8 +577,8 @@ def dominant_conv(nets, names, programs=None, precisions=None) -> dict:
     prec = (precisions or {}).get(name, "f16")
     label = ""
     if code == 113:
-        label = (" = conv_fast<f16,256,224,64,4,2,4,1,SPLIT,SX,-,WG> (fused f16x3 split tile, 64-byte K rows, "
-                 "weight fragments in registers; ArcFace 14x14x256 layers)" if prec == "f16x3" else
+        label = (" = conv_fast<f16,256,224,64,8,1,4,1,SPLIT,SX,-,WG> (fused f16x3 split tile, 64-byte K rows, "
+                 "weight fragments in registers, 8x1 waves of 32x224; ArcFace 14x14x256 layers)" if prec == "f16x3" else
                  " = conv_fast<f16,256,224,128,4,2,2,1> (ArcFace 14x14x256 layers)" if prec == "f16" else "")
     out = {"kernel": f"{_kernel_of(code, cfg)} in {name}" + label, "precision": prec, "peak_tflops": _peak_for(prec),
            "code": code, "launches": cnt, "avg_us": round(ms * 1e3 / cnt, 2), "flops_per_launch": round(fl / cnt),
@@ -669,7 +699,7 @@ def main():
 
     world, rank, local = _dist_init()
     local = _device(local)
-    os.environ.setdefault("PERSON_CAPTURE_AMD_PRECISION", args.precision)
+    _precision_env(args.precision)
     os.environ.setdefault("PERSON_CAPTURE_AMD_DET_BATCH", str(args.batch))
     os.environ.setdefault("PERSON_CAPTURE_AMD_ARC_BATCH", "512")
     from person_capture_amd._lib import PC_PREC_F16C8, PC_PREC_F16X3, PC_PREC_F32
@@ -773,7 +803,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": args.precision,
+        "dtype": _dtype_label(fe),
         "data": "synthetic (seeded u8 1080p frames, seeded synthetic SCRFD-10G/IResNet-100 weights)",
         "config": {"workload": "C3: SCRFD-10G detect + ArcFace-R100 embed (flip-TTA) + cosine match vs "
                                f"{args.bank}-embedding bank, 1080p, batch {args.batch} frames per GPU",
@@ -790,6 +820,11 @@ def main():
                    "parallelism": f"frame-shard x{world} (no collective)"},
         "roofline": {"bound": "mfma", "achieved": dom["achieved_tflops"], "peak": peak, "unit": "TFLOP/s",
                      "frac": round(dom["achieved_tflops"] / peak, 4),
+                     "issued_mfma_frac": round(dom["achieved_tflops"] * _issue_factor(dom.get("precision", "f16")) /
+                                               peak, 4),
+                     "frac_definition": "algorithmic FLOPs of the dominant kernel / its HIP-event launch time / the "
+                                        "dense MFMA peak of its arithmetic (f16 MFMA 2500 TF/s for f16 and f16x3); "
+                                        "issued_mfma_frac counts the 3 f16 MFMAs f16x3 issues per product",
                      "traffic": _traffic_for(dominant, dom["code"], dom.get("precision", "f16")),
                      "kernel": dom["kernel"], "kernel_launches": dom["launches"],
                      "kernel_avg_launch_us": dom["avg_us"], "kernel_flops_per_launch": dom["flops_per_launch"],
@@ -929,9 +964,8 @@ def main_c2(args):
     dom = dominant_conv([eng.net], ("arcface",), [eng.program], {"arcface": args.precision})
     recs = eng.net.profile_ops()
     eng.net.profile(False)
-    # f16x3 issues 3 f16 MFMAs per algorithmic product: its roofline is a third of dense f16
-    # (f16c8: 2 f16 MFMAs + 1 block-scaled e4m3 MFMA per 64-channel K tile where f16 takes 2; its
-    # roofline is the f16 peak x 2 / 3 at the e4m3 instruction's measured equal issue time)
+    # algorithmic FLOPs over the dense f16 peak for every f16-MFMA form (f16x3 / f16c8 issue 3x / 1.5x
+    # that work: issued_mfma_frac)
     peak = _peak_for(args.precision)
     fl = eng.flops_per_forward * B
     ms = elapsed / args.steps * 1e3
@@ -953,6 +987,7 @@ def main_c2(args):
                    "parallelism": f"replica x{world} (no collective)"},
         "roofline": {"bound": "mfma", "achieved": round(net_tf, 2), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(net_tf / peak, 4), "traffic": None,
+                     "issued_mfma_frac": round(net_tf * _issue_factor(args.precision) / peak, 4),
                      "scope": "whole IResNet-100 forward: algorithmic conv FLOPs of 256 rows / step time "
                               f"({fl / 1e12:.3f} TFLOP per step)",
                      "dominant_kernel": dom,
@@ -1005,7 +1040,7 @@ def main_other(args):
     workloads, same JSON contract."""
     world, rank, local = _dist_init()
     local = _device(local)
-    os.environ.setdefault("PERSON_CAPTURE_AMD_PRECISION", args.precision)
+    _precision_env(args.precision)
     os.environ.setdefault("PERSON_CAPTURE_AMD_DET_BATCH", str(args.batch))
     os.environ.setdefault("PERSON_CAPTURE_AMD_ARC_BATCH", "512")
     from person_capture_amd.face_embedder import FaceEmbedder, _DevImage
@@ -1094,10 +1129,26 @@ def main_other(args):
         stats["face_prior_logit_shift"] = round(shift, 4)
         stats["face_conf_calibrated"] = conf_used
 
-        def step():
+        def step(phases=None):
+            # phases (diagnostic pass outside the timed region): wall ms of each stage with the device
+            # drained between them, and the FaceEmbedder's host phase times of its extract_batch
+            def mark(key):
+                if phases is not None:
+                    ctx.sync()
+                    fe._ectx.sync()
+                    reid._ctx.sync()
+                    t = time.perf_counter()
+                    phases[key] = round((t - phases.pop("_t")) * 1e3, 3)
+                    phases["_t"] = t
+            if phases is not None:
+                ctx.sync()
+                phases["_t"] = time.perf_counter()
             crops = person_crops()
+            mark("persons_yolo_ms")
             faces = fe.extract_batch([None] * len(crops), dev_frames=crops, bank=bank) if crops else []
+            mark("faces_extract_batch_ms")
             feats = reid.extract_device([(c.ptr, c.H, c.W, c.stride) for c in crops])
+            mark("reid_ms")
             stats["persons"] = len(crops)
             stats["faces"] = sum(len(f) for f in faces)
             stats["faces_per_crop"] = round(stats["faces"] / max(1, len(crops)), 3)
@@ -1161,6 +1212,17 @@ def main_other(args):
     prof = [n.profile_read() for n in nets]
     for n in nets:
         n.profile(False)
+    if c4:
+        # where a C4 step goes: one more step, stage by stage with the device drained
+        # between stages (so the stages do not overlap here as they may in the timed steps), with the
+        # FaceEmbedder's host phase timers on
+        phases = {}
+        fe.host_times = {}
+        step(phases)
+        phases.pop("_t", None)
+        stats["phase_ms_one_step"] = phases
+        stats["face_host_phase_ms_one_step"] = {k: round(v * 1e3, 3) for k, v in fe.host_times.items()}
+        fe.host_times = None
     conv_ms = sum(p["conv_ms"] for p in prof)
     conv_flops = sum(p["conv_flops"] for p in prof)
     conv_launches = sum(p["conv_launches"] for p in prof)
@@ -1178,9 +1240,10 @@ def main_other(args):
         pk = _peak_for(pn)
         per_net[nm] = {"dtype": pn, "conv_ms_per_step": round(p_["conv_ms"] / args.steps, 3),
                        "achieved_tflops": round(tf, 1), "peak": round(pk, 1), "frac": round(tf / pk, 4)}
-        if pn == "f16x3":   # algorithmic FLOPs above; 3 MFMAs issued per product
-            per_net[nm].update(mfma_tflops=round(3 * tf, 1), mfma_frac=round(3 * tf / PEAK_F16_TFLOPS, 4))
-    peak = PEAK_F16_TFLOPS if args.precision == "f16" else PEAK_F32_TFLOPS
+        if _issue_factor(pn) != 1.0:   # algorithmic FLOPs above; MFMA work issued
+            per_net[nm].update(mfma_tflops=round(_issue_factor(pn) * tf, 1),
+                               mfma_frac=round(_issue_factor(pn) * tf / pk, 4))
+    peak = _peak_for(args.precision)
     total_units = units_per_step * args.steps if scaling == "strong" else _sum_over_ranks(world, units_per_step *
                                                                                            args.steps)
     out = {
@@ -1188,7 +1251,7 @@ def main_other(args):
         else "frames/sec pre-scan detect+embed+match @4K, 1/2/4/8 GPU; MFMA util %",
         "value": round(total_units / elapsed, 3), "unit": "frames/s" if c4 else "samples/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-        "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": args.precision,
+        "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": _dtype_label(fe),
         "data": "synthetic (seeded u8 frames, seeded synthetic weights of every net)",
         "config": {"workload": wl, ("frames_per_step_per_gpu" if c4 else "samples_per_clip"): units_per_step,
                    "bank": bank_n, **{k: v for k, v in stats.items()},

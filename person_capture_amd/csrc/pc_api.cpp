@@ -30,6 +30,7 @@ hipError_t conv_launch(int f32, int rowb, int cfg, const ConvParams& p, hipStrea
 hipError_t conv_halo_launch(int f32, int cfg, const ConvParams& p, hipStream_t s);
 hipError_t conv_fast_launch(int f32, int rowb, int cfg, const ConvParams& p, hipStream_t s);
 hipError_t conv_hx_launch(const ConvParams& p, hipStream_t s);
+hipError_t conv_hxg_launch(const ConvParams& p, hipStream_t s);
 int conv_fast_num_cfgs();
 constexpr int kFastSmallCfg0 = 15, kFastSmallCfg1 = 19;   // conv_fast tiles 15..19: small-batch plans only
 int conv_fast_tile(int cfg, int* bc, int* bp);
@@ -777,6 +778,7 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
   int nc8 = 0;
   for (int sg = 0; sg < nseg; ++sg) nc8 += n->tens[w[3 + 5 * sg]].c8;
   const bool in_c8 = nc8 > 0;
+  const bool out_c8 = n->tens[out].c8 || (w[21] >= 0 && n->tens[w[21]].c8);
   if (in_c8 && nc8 != nseg) return fail(n->ctx, PC_ERR_FORMAT, "conv mixes f16c8 and other input segments");
   if (in_c8 && (w[24] > 1 || n->f32 || (getenv("PC_SPLIT_FUSED") && atoi(getenv("PC_SPLIT_FUSED")) == 0)))
     return fail(n->ctx, PC_ERR_FORMAT, "f16c8 convs run on conv_fast's fused C8 tiles only (no split-K)");
@@ -835,6 +837,7 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
             // net (kC8Rowb; PC_C8_ROWB for tuning): the row width orders the f16 and block-scaled
             // MFMAs of a K tile, so a conv's output would otherwise depend on its batch class
             if (in_c8 && (!conv_fast_valid_c8(k, rb) || rb != c8_rowb())) continue;
+            if (out_c8 && !conv_fast_valid_c8(k, rb)) continue;   // f16c8 output / residual: LDS epilogue
             if (!conv_fast_valid_sx(k, rb)) continue;
             const long long t = (M + bp - 1) / bp * (npad / bc);
             const double est = (double)((t + 255) / 256) * bc * bp * sxcost(k);
@@ -895,6 +898,18 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
       pl.fast = pl.halo = pl.t2d = -1;
       pl.sx = 0;
     }
+    // 96 -> 96 channel layers (SCRFD's 80x80 / 40x40 / 20x20 x96 trunk) on conv_hxg<96, 96>: one
+    // workgroup per CU, every output channel per wave, the halo staged per 32-channel group
+    // (PC_CONV_HXG=0 disables, for A/B)
+    if (X.split && !X.c8 && !Y.c8 && X.C == 192 && X.cs == 192 && Y.split && Y.C == 192 && npad == 96 && w[4] == 3 &&
+        w[5] == 3 && w[6] == 1 && w[7] == 1 && X.H == Y.H && X.W == Y.W && w[15] == 9 * 288 &&
+        !(w[21] >= 0 && (w[22] == RES_UP2 || !n->tens[w[21]].split || n->tens[w[21]].c8)) &&
+        (double)X.H * X.W * n->max_batch * X.cs * esz + kZeroTail < 4294967296.0 &&
+        !(getenv("PC_CONV_HXG") && atoi(getenv("PC_CONV_HXG")) == 0)) {
+      pl.hx = 2;
+      pl.fast = pl.halo = pl.t2d = -1;
+      pl.sx = 0;
+    }
   }
   // small-batch plan: a long-K conv of a few images fills a fraction of the CUs (a 14x14x256
   // conv of 12 rows: 56 workgroups of 2304-long K) - split K over the generic kernel so the
@@ -923,8 +938,11 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
     pl.hx = 0;
     pl.splitk = 1;
   }
-  if ((Y.c8 || (w[21] >= 0 && n->tens[w[21]].c8)) && (pl.fast < 0 || !pl.sx || pl.t2d >= 0 || pl.hx || pl.halo >= 0))
-    return fail(n->ctx, PC_ERR_FORMAT, "f16c8 outputs and residuals are written / read by conv_fast's fused tiles only");
+  // (and only by those with the LDS epilogue: the per-fragment epilogue of the 96 / 224-channel tiles
+  // has no f8 region handling)
+  if ((Y.c8 || (w[21] >= 0 && n->tens[w[21]].c8)) &&
+      (pl.fast < 0 || !pl.sx || pl.t2d >= 0 || pl.hx || pl.halo >= 0 || !conv_fast_valid_c8(pl.fast, pl.rowb)))
+    return fail(n->ctx, PC_ERR_FORMAT, "f16c8 outputs and residuals are written / read by conv_fast's fused LDS-epilogue tiles only");
   // fused f16x3 tiles of 64-byte K rows on the WG form where it is instantiated (PC_SX_WG=0: staged
   // weights, for A/B). Same K order and pass order as the staged form: bit-identical outputs.
   pl.wg = 0;
@@ -1624,7 +1642,9 @@ static int run_ops(pc_net* n, int N, hipStream_t s) {
       p.partial = n->partial;
       p.zero = c->zero;
       if (const char* e = getenv("PC_CONV_DBG")) p.dbg = atoi(e);
-      if (pl.hx) {
+      if (pl.hx == 2) {
+        HIPCHK(c, conv_hxg_launch(p, s));
+      } else if (pl.hx) {
         HIPCHK(c, conv_hx_launch(p, s));
       } else if (pl.t2d >= 0) {
         HIPCHK(c, conv_t2d_launch(p, pl.t2d, s));
@@ -1835,7 +1855,7 @@ extern "C" int pc_net_profile_ops(pc_net* n, double* out, int max_recs) {
     o[0] = r.op; o[1] = r.kind; o[2] = ms; o[3] = r.flops;
     const ConvPlan* pl = conv ? (r.small >= 0 ? &n->plans_cls[r.small][r.op] : &n->plans[r.op]) : nullptr;
     o[4] = r.code >= 0 ? r.code
-                       : conv ? (pl->hx            ? 500
+                       : conv ? (pl->hx            ? 499 + pl->hx   // 500 conv_hx64, 501 conv_hxg
                                  : pl->c8          ? 600 + pl->fast
                                  : pl->t2d >= 0    ? 200 + pl->t2d
                                  : pl->fast >= 0   ? 100 + pl->fast
@@ -1866,14 +1886,17 @@ extern "C" int pc_net_run(pc_net* n, const void* d_in, int N) {
   auto it = n->graphs.find(key);
   if (it == n->graphs.end()) {
     if (!n->cap_stream) HIPCHK(c, hipStreamCreateWithFlags(&n->cap_stream, hipStreamNonBlocking));
-    hipGraph_t g;
+    hipGraph_t g = nullptr;
     HIPCHK(c, hipStreamBeginCapture(n->cap_stream, hipStreamCaptureModeThreadLocal));
     n->capturing = 1;
     int rc = run_ops(n, N, n->cap_stream);
     n->capturing = 0;
     hipError_t e = hipStreamEndCapture(n->cap_stream, &g);
-    if (rc != PC_OK) return rc;
-    if (e != hipSuccess) return fail(c, PC_ERR_HIP, std::string("graph capture: ") + hipGetErrorString(e));
+    if (rc != PC_OK || e != hipSuccess) {   // a failed capture leaves no graph behind
+      if (g) hipGraphDestroy(g);
+      if (rc != PC_OK) return rc;
+      return fail(c, PC_ERR_HIP, std::string("graph capture: ") + hipGetErrorString(e));
+    }
     hipGraphExec_t ge;
     e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
     hipGraphDestroy(g);

@@ -283,10 +283,14 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
   const int xsc0 = klo ? (p.seg[0].f8s & 0xff) : ((p.seg[0].f8s >> 8) & 0xff);
   const int xsc1 = klo ? (p.seg[1].f8s & 0xff) : ((p.seg[1].f8s >> 8) & 0xff);
   const int kt0 = p.seg[0].kt;
-  // WG: this wave's W_hi / W_lo fragments of the current K tile (the next tile's W_lo is loaded once
-  // the first pass has consumed it, its W_hi after the last pass)
+  // WG: this wave's W_hi / W_lo fragments of the current K tile. Wave tiles of at most 2 row blocks
+  // (the 8x1 / 4x2 layouts) double-buffer them by K-tile parity and load the next
+  // tile's at the start of the current one; wider ones load the next tile's W_lo once the first pass
+  // has consumed it, its W_hi after the last pass (one register set)
   // (MUBUF loads: tile offset in an SGPR, two lane offsets, fragment offsets as immediates)
-  f16x8 wgh[WG ? TC : 1], wgl[WG ? TC : 1];
+  constexpr bool WDB = WG && TC <= 2;
+  static_assert(!WDB || NSTAGE % 2 == 0, "K-tile parity of the weight buffers");
+  f16x8 wgh[WDB ? 2 : 1][WG ? TC : 1], wgl[WDB ? 2 : 1][WG ? TC : 1];
   const __amdgpu_buffer_rsrc_t wgrs = rsrc(WG ? p.wfrag : p.w);
   const int wgoff0 = ((c0 + wr * WTC) / 16) * 2048 + lane * 16, wgoff1 = wgoff0 + 4096;
   const int wgstride = (p.npad / 16) * 2048;   // bytes per K tile
@@ -351,38 +355,51 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
     // fused split tiles: per k-substep three passes over the fragment grid (a dependent MFMA is
     // TC*TP issues away), W_lo*x_hi, W_hi*x_hi, W_hi*x_lo - the same order in every SX form
     if constexpr (WG) {
-      // x_hi fragments, W_lo*x_hi; x_lo reads behind W_hi*x_hi; the next tile's W_lo after it,
-      // W_hi*x_lo, the next tile's W_hi (at most 2 TP + 2 TC fragments live beside the accumulators)
+      // per group of pixel fragments: x_hi fragments, W_lo*x_hi; x_lo reads behind W_hi*x_hi; W_hi*x_lo.
+      // Wave tiles over 8 pixel fragments (the 8x1 layout's 32x224) walk them in two groups, so at
+      // most 2 TPG fragments are live beside the accumulators; every accumulator still takes
+      // W_lo*x_hi, W_hi*x_hi, W_hi*x_lo in that order (bit-identical across layouts)
+      constexpr int TPG = TP > 8 && TP % 2 == 0 ? TP / 2 : TP;
+      constexpr int NG = TP / TPG;
+      constexpr int cur = WDB ? (slot & 1) : 0;
       const unsigned ko = ((lane >> 4) ^ sw) << 4;
-      f16x8 fbh[TP], fbl[TP];
       const int tn = tix + 1 < nk ? tix + 1 : nk - 1;
+      if constexpr (WDB) {
+        wg_load(wgl[cur ^ 1], tn, std::integral_constant<int, 1>{});
+        wg_load(wgh[cur ^ 1], tn, std::integral_constant<int, 0>{});
+      }
+      static_for<NG>([&](auto gc) __attribute__((always_inline)) {
+        constexpr int g = decltype(gc)::value, b0 = g * TPG;
+        f16x8 fbh[TPG], fbl[TPG];
 #pragma unroll
-      for (int t = 0; t < TP; ++t) fbh[t] = *reinterpret_cast<const f16x8*>(base + b_row + ko + t * 16 * ROWB);
+        for (int t = 0; t < TPG; ++t) fbh[t] = *reinterpret_cast<const f16x8*>(base + b_row + ko + (b0 + t) * 16 * ROWB);
 #pragma unroll
-      for (int a = 0; a < TC; ++a)
+        for (int a = 0; a < TC; ++a)
 #pragma unroll
-        for (int b = 0; b < TP; ++b)
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wgl[a], fbh[b], acc[a][b], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
+          for (int b = 0; b < TPG; ++b)
+            acc[a][b0 + b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wgl[cur][a], fbh[b], acc[a][b0 + b], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int t = 0; t < TP; ++t) fbl[t] = *reinterpret_cast<const f16x8*>(base + b_row + BP * ROWB + ko + t * 16 * ROWB);
-      __builtin_amdgcn_sched_barrier(0);
+        for (int t = 0; t < TPG; ++t)
+          fbl[t] = *reinterpret_cast<const f16x8*>(base + b_row + BP * ROWB + ko + (b0 + t) * 16 * ROWB);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int a = 0; a < TC; ++a)
+        for (int a = 0; a < TC; ++a)
 #pragma unroll
-        for (int b = 0; b < TP; ++b)
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wgh[a], fbh[b], acc[a][b], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      wg_load(wgl, tn, std::integral_constant<int, 1>{});
-      __builtin_amdgcn_sched_barrier(0);
+          for (int b = 0; b < TPG; ++b)
+            acc[a][b0 + b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wgh[cur][a], fbh[b], acc[a][b0 + b], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (!WDB && g + 1 == NG) wg_load(wgl[0], tn, std::integral_constant<int, 1>{});
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int a = 0; a < TC; ++a)
+        for (int a = 0; a < TC; ++a)
 #pragma unroll
-        for (int b = 0; b < TP; ++b)
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wgh[a], fbl[b], acc[a][b], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      wg_load(wgh, tn, std::integral_constant<int, 0>{});
-      __builtin_amdgcn_sched_barrier(0);
+          for (int b = 0; b < TPG; ++b)
+            acc[a][b0 + b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wgh[cur][a], fbl[b], acc[a][b0 + b], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (!WDB && g + 1 == NG) wg_load(wgh[0], tn, std::integral_constant<int, 0>{});
+        __builtin_amdgcn_sched_barrier(0);
+      });
       return;
     }
     if constexpr (SX) {
@@ -478,8 +495,8 @@ __global__ __launch_bounds__(64 * WC * WP, (WC * WP * OCC + 3) / 4) void conv_fa
           __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)(smem + RING + wave * 1024), 16, off, 0, 0, 0);
         });
       } else {   // tile 0's weight fragments
-        wg_load(wgl, 0, std::integral_constant<int, 1>{});
-        wg_load(wgh, 0, std::integral_constant<int, 0>{});
+        wg_load(wgl[0], 0, std::integral_constant<int, 1>{});
+        wg_load(wgh[0], 0, std::integral_constant<int, 0>{});
       }
     }
   });
@@ -602,6 +619,12 @@ constexpr bool fast_wg_fits() {
 template <int BC>
 constexpr bool LDS_EPI_OK() { return ((BC / 8) & (BC / 8 - 1)) == 0 && ((BC / 16) & (BC / 16 - 1)) == 0; }
 
+// (read per launch, like PC_CONV_DBG: the A/B test switches it inside one process)
+static int wg_layout() {
+  const char* e = getenv("PC_WG_LAYOUT");
+  return e ? atoi(e) : 1;
+}
+
 template <typename T, int BC, int BP, int ROWB, int WC, int WP, int NSTAGE, int OCC = 1>
 static hipError_t launch_fast_cfg(const ConvParams& p, hipStream_t s) {
   if constexpr (!fast_valid<BC, BP, ROWB, WC * WP>()) {
@@ -610,10 +633,18 @@ static hipError_t launch_fast_cfg(const ConvParams& p, hipStream_t s) {
     const int nwg = (p.M + BP - 1) / BP * (p.npad / BC);
     if (p.sx) {   // fused f16x3 / f16c8 tiles: always the split epilogue
       if (p.wfrag && !p.c8) {   // weight fragments from global memory: 4 stages of pixel rows
+        // wave layout: 8x1 waves of 32x224 on 256x224, 4x2 of 32x128 on 128x256 -
+        // each weight fragment is loaded by 1 or 2 waves instead of 2 or 4 (PC_WG_LAYOUT=0: the
+        // cfg table's 4x2 / 2x4 layouts, for A/B; same accumulation order, bit-identical)
+        constexpr int WC2 = BC == 256 ? 8 : 4, WP2 = BC == 256 ? 1 : 2;
         if constexpr (sizeof(T) == 2 && ROWB == 64 && OCC == 1 && ((BC == 256 && BP == 224) || (BC == 128 && BP == 256)) &&
-                      fast_wg_fits<BC, BP, WC, WP>()) {
-          hipLaunchKernelGGL((conv_fast<T, BC, BP, ROWB, WC, WP, 4, 1, true, true, false, true>), dim3(nwg),
-                             dim3(64 * WC * WP), 0, s, p);
+                      fast_wg_fits<BC, BP, WC, WP>() && fast_wg_fits<BC, BP, WC2, WP2>()) {
+          if (wg_layout())
+            hipLaunchKernelGGL((conv_fast<T, BC, BP, ROWB, WC2, WP2, 4, 1, true, true, false, true>), dim3(nwg),
+                               dim3(64 * WC2 * WP2), 0, s, p);
+          else
+            hipLaunchKernelGGL((conv_fast<T, BC, BP, ROWB, WC, WP, 4, 1, true, true, false, true>), dim3(nwg),
+                               dim3(64 * WC * WP), 0, s, p);
           return hipGetLastError();
         } else {
           return hipErrorInvalidValue;

@@ -10,8 +10,11 @@
 // fragments come from the conv's fragment-ordered weight copy (pc_api.cpp pack_wfrag) straight into
 // registers, one k-step ahead: the K loop has no barrier, and two workgroups share a CU (round 4's
 // form staged 16x16 blocks and a 3-tap weight ring through the LDS, 131 KB: one workgroup per CU).
-// Per k-step and fragment the MFMAs are conv_fast SX's: W_hi*x_hi, W_lo*x_hi, W_hi*x_lo, k-steps
-// in (tap row, tap column, 32-channel block) order.
+// Per k-step and fragment the MFMAs are W_hi*x_hi, W_lo*x_hi, W_hi*x_lo, k-steps in (tap row, tap
+// column, 32-channel block) order. That is NOT conv_fast SX's accumulation order (channel-group-major
+// K, W_lo*x_hi first, round 5), so PC_CONV_HX=0 changes these layers' outputs in the last bits (both
+// f32 class); what the code guarantees is that every plan class of a net runs the same kernel on them
+// (plan_conv picks this one independently of the batch), so small and large batches stay bit-identical.
 #include "pc_conv_common.h"
 
 namespace pc {
@@ -193,6 +196,234 @@ __global__ __launch_bounds__(256, 2) void conv_hx64(ConvParams p, int nby, int n
     *reinterpret_cast<f16x8*>(yp) = yh;
     *reinterpret_cast<f16x8*>(yp + p.ysplit) = yl;
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// conv_hxg<CIN, COUT, TP>: the halo-staged f16x3 3x3 conv for wider channel counts - SCRFD's
+// 80x80x96 / 40x40x96 / 20x20x96 trunk (CIN = COUT = 96: 29 % of SCRFD-10G's FLOPs, 131 TF/s on the
+// fused 32x256 tile). Where conv_hx64 stages all 64 input channels of a 16x12 block at
+// once (63 KB, two workgroups and 8 waves per CU) and every wave loads all 64 output channels' weight
+// fragments from L2 for 3 output rows (8 fragment loads per 36 MFMAs: the TA / TD return path, not the
+// matrix pipe, is its limit), this kernel runs ONE workgroup of 4 waves per CU, one wave per SIMD with
+// up to 512 registers, so each wave owns every output channel of TP output rows (6 x TP fragments):
+// 12 weight fragment loads per 18 TP MFMAs (0.13 per MFMA at TP 5, against 0.22).
+//  * the block is 16 x 4 TP output pixels of one image; its (4 TP + 2) x 18 input halo is staged per
+//    group of 32 input channels (hi and lo: 128-byte slots, 16-byte chunk q of slot s holding source
+//    chunk q ^ (s & 7) - conflict-free ds_read_b128 for any 16 consecutive slots) in a 2-stage ring:
+//    group g + 1's LDS-DMA is issued right after the barrier that opens group g, so it lands while
+//    group g's 9 taps run; one barrier per group, none inside it;
+//  * K walks (32-channel group, tap row, tap column) - the packed fragment copy's order for channel
+//    counts that are not a multiple of 64 (pc_api.cpp pack_wfrag, gt 1) - with the weight fragments of
+//    the next k-step loaded into registers under the current one; per k-step and fragment the MFMAs
+//    are conv_hx64's: W_hi*x_hi, W_lo*x_hi, W_hi*x_lo;
+//  * epilogue: conv_hx64's (f32 image over the LDS, 16-byte hi and lo stores per pixel and 8 channels).
+template <int CIN, int COUT, int TP>
+__global__ __launch_bounds__(256, 1) void conv_hxg(ConvParams p, int nby, int nbx) {
+  constexpr int TC = COUT / 16, NG = CIN / 32, NKS = 9 * NG;
+  constexpr int BW = 16, BH = 4 * TP, PW = BW + 2, SLOTS = (BH + 2) * PW;
+  constexpr int SB = 128;                                    // slot: 32 hi + 32 lo f16 channels
+  constexpr int PIECES = (SLOTS * SB / 1024 + 3) / 4 * 4;    // 1 KiB DMA pieces per stage, 4 waves alike
+  constexpr int STAGE = PIECES * 1024;
+  constexpr int RS = COUT + 4;                               // epilogue image row (floats)
+  constexpr int EPI = BH * BW * RS * 4;
+  constexpr int SMEM = 2 * STAGE > EPI ? 2 * STAGE : EPI;
+  static_assert(COUT % 16 == 0 && CIN % 32 == 0 && CIN % 64 != 0, "32-channel groups (pack_wfrag gt 1)");
+  static_assert(SMEM <= 163840, "LDS");
+  static_assert((BH * BW * (COUT / 8)) % 256 == 0, "epilogue work split");
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  const ConvSeg& S = p.seg[0];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nblk = p.N * nby * nbx;
+  const int b = xcd_remap(blockIdx.x, nblk);
+  const int n = b / (nby * nbx), rem = b - n * (nby * nbx);
+  const int oy0 = (rem / nbx) * BH, ox0 = (rem - (rem / nbx) * nbx) * BW;
+  const int H = S.H, W = S.W;
+  const int fr = lane & 15, kg = lane >> 4;
+
+  auto rsrc = [](const void* base) __attribute__((always_inline)) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)0xffffffff, 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t xrs = rsrc(S.x);
+  const __amdgpu_buffer_rsrc_t wrs = rsrc(p.wfrag);
+
+  // this lane's share of a stage: piece i = wave + 4 j, LDS byte i * 1024 + lane * 16 = slot s,
+  // chunk position q (source chunk q ^ (s & 7): hi channels 8 c.. for c < 4, lo channels 8 (c - 4)..)
+  constexpr int PPW = PIECES / 4;
+  unsigned src[PPW];
+#pragma unroll
+  for (int j = 0; j < PPW; ++j) {
+    const int bb = (wave + 4 * j) * 1024 + lane * 16;
+    const int sl = bb >> 7, q = (bb >> 4) & 7;
+    const int c = q ^ (sl & 7);
+    const int iy = oy0 - 1 + sl / PW, ix = ox0 - 1 + (sl - (sl / PW) * PW);
+    const bool ok = sl < SLOTS && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+    // (unsigned: the pixel byte offset fits 32 bits only, the planner keeps buffers below 4 GiB)
+    src[j] = ok ? (unsigned)((n * H + iy) * W + ix) * (unsigned)(S.cs * 2) + (unsigned)(((c & 3) * 8 + (c >> 2) * CIN) * 2)
+                : S.zero_off + (unsigned)(q << 4);
+  }
+  auto stage = [&](int g, int st) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+      unsigned off = src[j];
+      asm volatile("" : "+v"(off));
+      // a group's channels ride in the instruction's scalar offset (64 bytes per group); the zero
+      // tail is wider than any pixel row, so out-of-image slots stay zero for every group
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)(smem + st * STAGE + (wave + 4 * j) * 1024), 16, off,
+                                               g * 64, 0, 0);
+    }
+  };
+  // weight fragments of k-step s = 32-channel group s / 9, tap s % 9 (packed K tile s): TC row blocks
+  // x [W_hi, W_lo] x 1 KiB (lane l: row 16 a + (l & 15), channels 8 (l >> 4) .. +8)
+  constexpr int TILE = TC * 2 * 1024;
+  auto wload = [&](f16x8* wh, f16x8* wl, int s) __attribute__((always_inline)) {
+#pragma unroll
+    for (int a = 0; a < TC; ++a) {
+      wh[a] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16 + (a * 2) * 1024, s * TILE, 0));
+      wl[a] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16 + (a * 2 + 1) * 1024, s * TILE, 0));
+    }
+  };
+  f16x8 wbh[2][TC], wbl[2][TC];
+  stage(0, 0);
+  wload(wbh[0], wbl[0], 0);
+
+  f32x4 acc[TC][TP];
+#pragma unroll
+  for (int a = 0; a < TC; ++a)
+#pragma unroll
+    for (int t = 0; t < TP; ++t) acc[a][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (p.dbg & 8) return;   // tuning only (PC_CONV_DBG): prologue only
+
+  static_for<NG>([&](auto gc) __attribute__((always_inline)) {
+    constexpr int g = decltype(gc)::value, st = g & 1;
+    // group g's halo: every VMEM op but the youngest 2 TC (k-step 9 g's weights) has landed
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * TC) : "memory");
+    __syncthreads();   // every wave's pieces of group g; every wave done with group g - 1's stage
+    if constexpr (g + 1 < NG) stage(g + 1, st ^ 1);
+    const char* base = smem + st * STAGE;
+    static_for<9>([&](auto tc) __attribute__((always_inline)) {
+      constexpr int tap = decltype(tc)::value, s = g * 9 + tap, q = s & 1;
+      constexpr int toff = (tap / 3) * PW + (tap % 3);
+      if constexpr (s + 1 < NKS) wload(wbh[q ^ 1], wbl[q ^ 1], s + 1);
+      f16x8 bh[TP], bl[TP];
+#pragma unroll
+      for (int t = 0; t < TP; ++t) {
+        const int sl = (wave * TP + t) * PW + fr + toff;
+        bh[t] = *reinterpret_cast<const f16x8*>(base + sl * SB + ((kg ^ (sl & 7)) << 4));
+        bl[t] = *reinterpret_cast<const f16x8*>(base + sl * SB + (((4 + kg) ^ (sl & 7)) << 4));
+      }
+      if (p.dbg & 2) return;   // tuning only: no MFMAs
+#pragma unroll
+      for (int a = 0; a < TC; ++a)
+#pragma unroll
+        for (int t = 0; t < TP; ++t)
+          acc[a][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wbh[q][a], bh[t], acc[a][t], 0, 0, 0);
+#pragma unroll
+      for (int a = 0; a < TC; ++a)
+#pragma unroll
+        for (int t = 0; t < TP; ++t)
+          acc[a][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wbl[q][a], bh[t], acc[a][t], 0, 0, 0);
+#pragma unroll
+      for (int a = 0; a < TC; ++a)
+#pragma unroll
+        for (int t = 0; t < TP; ++t)
+          acc[a][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wbh[q][a], bl[t], acc[a][t], 0, 0, 0);
+    });
+  });
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (p.dbg & 4) return;   // tuning only: no epilogue
+
+  // ---- epilogue (conv_hx64's): f32 [pixel][channel] image over the LDS, then 8 channels of one
+  // pixel per thread and step: bias, activation select, split residual hi + lo, hi / lo stores ----
+  __syncthreads();   // every wave is done with the stages
+  float* im = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int a = 0; a < TC; ++a)
+#pragma unroll
+    for (int t = 0; t < TP; ++t) {
+      const int pl = (wave * TP + t) * BW + fr;
+      *reinterpret_cast<f32x4*>(im + pl * RS + a * 16 + kg * 4) = acc[a][t];
+    }
+  __syncthreads();
+  const int OW = p.OW, OH = p.OH;
+  const bool smooth = p.act == ACT_SILU || p.act == ACT_GELU;
+  const bool has_res = p.res_mode != RES_NONE;
+  const bool pre_act = !p.act_after_res;
+  constexpr int CGN = COUT / 8;
+  for (int it = threadIdx.x; it < BH * BW * CGN; it += 256) {
+    const int pl = it / CGN, ch = (it - pl * CGN) * 8;
+    const int oy = oy0 + pl / BW, ox = ox0 + (pl & (BW - 1));
+    if (oy >= OH || ox >= OW) continue;
+    const long long pix = ((long long)n * OH + oy) * OW + ox;
+    const f32x4 lo4 = *reinterpret_cast<const f32x4*>(im + pl * RS + ch);
+    const f32x4 hi4 = *reinterpret_cast<const f32x4*>(im + pl * RS + ch + 4);
+    float v[8] = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
+    if (p.bias_mode == BIAS_CHANNEL) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += p.bias[ch + j];
+    } else if (p.bias_mode == BIAS_BORDER9) {
+      const int rc = oy - 1 < 0 ? 0 : (oy + 1 >= H ? 2 : 1);
+      const int cc = ox - 1 < 0 ? 0 : (ox + 1 >= W ? 2 : 1);
+      const float* bp = p.bias + (rc * 3 + cc) * p.npad + ch;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += bp[j];
+    }
+    float r[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (has_res) {
+      const f16* rp = reinterpret_cast<const f16*>(p.res) + pix * p.rcs + ch;
+      const f16x8 rh = *reinterpret_cast<const f16x8*>(rp);
+      const f16x8 rl = *reinterpret_cast<const f16x8*>(rp + p.rsplit);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] = (float)rh[j] + (float)rl[j];
+    }
+    if (has_res && !pre_act) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += r[j];
+    }
+    if (smooth) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j], p.act, 0.f);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float sl = p.act == ACT_PRELU ? p.slope[ch + j] : (p.act == ACT_RELU ? 0.f : 1.f);
+        v[j] = v[j] > 0.f ? v[j] : v[j] * sl;
+      }
+    }
+    if (has_res && pre_act) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += r[j];
+    }
+    f16x8 yh, yl;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float x = ch + j < p.cout ? v[j] : 0.f;
+      yh[j] = (f16)x;
+      yl[j] = (f16)(x - (float)yh[j]);
+    }
+    f16* yp = reinterpret_cast<f16*>(p.y) + pix * p.ycs + ch;
+    *reinterpret_cast<f16x8*>(yp) = yh;
+    *reinterpret_cast<f16x8*>(yp + p.ysplit) = yl;
+  }
+}
+
+constexpr int HXG_TP = 5;   // 16 x 20 output blocks: 80 / 20 rows, no waste on the 80x80 maps
+
+// can a conv run on conv_hxg<96, 96>: split 96-channel input (X.C 192 = [hi | lo]), 96 output
+// channels written split, 3x3 stride 1 pad 1, same size, plain or same-size split residual
+int conv_hxg_ok(const ConvParams& p) {
+  const ConvSeg& S = p.seg[0];
+  return p.nseg == 1 && S.C == 192 && S.cs == 192 && S.KH == 3 && S.KW == 3 && S.stride == 1 && S.pad == 1 &&
+         S.H == p.OH && S.W == p.OW && p.npad == 96 && p.ysplit == 96 && p.splitk == 1 && !p.out_f32 &&
+         p.ktot == 9 * 288 && p.res_mode != RES_UP2 && (p.res_mode == RES_NONE || (p.rsplit == 96 && p.rcs % 8 == 0)) &&
+         p.ycs % 8 == 0 && p.cwrite == 96 && p.wfrag != nullptr;
+}
+
+hipError_t conv_hxg_launch(const ConvParams& p, hipStream_t s) {
+  if (!conv_hxg_ok(p)) return hipErrorInvalidValue;
+  const int nby = (p.OH + 4 * HXG_TP - 1) / (4 * HXG_TP), nbx = (p.OW + 15) / 16;
+  hipLaunchKernelGGL((conv_hxg<96, 96, HXG_TP>), dim3(p.N * nby * nbx), dim3(256), 0, s, p, nby, nbx);
+  return hipGetLastError();
 }
 
 // can a conv run here: split 64-channel input (X.C 128 = [hi | lo]), 64 output channels

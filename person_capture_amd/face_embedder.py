@@ -101,9 +101,31 @@ def get_context(device_index: int, role: str = "") -> GpuContext:
     return c
 
 
+_PREC_WORDS = {"f32": PC_PREC_F32, "fp32": PC_PREC_F32, "float32": PC_PREC_F32,
+               "f16": PC_PREC_F16, "fp16": PC_PREC_F16, "float16": PC_PREC_F16, "half": PC_PREC_F16,
+               "f16x3": PC_PREC_F16X3, "x3": PC_PREC_F16X3, "split": PC_PREC_F16X3,
+               "f16c8": PC_PREC_F16C8, "c8": PC_PREC_F16C8}
+
+
+def _prec_word(var: str, allowed: Tuple[int, ...]) -> Optional[int]:
+    """The precision named by environment variable `var` (None when unset); an unknown word or a form
+    this net does not run raises instead of silently running plain f16."""
+    v = os.getenv(var, "").strip().lower()
+    if not v:
+        return None
+    p = _PREC_WORDS.get(v)
+    if p is None or p not in allowed:
+        names = sorted(k for k, q in _PREC_WORDS.items() if q in allowed)
+        raise ValueError(f"{var}={v!r}: expected one of {names}")
+    return p
+
+
 def _precision(var: str = "PERSON_CAPTURE_AMD_PRECISION") -> int:
-    v = os.getenv(var, os.getenv("PERSON_CAPTURE_AMD_PRECISION", "f16")).strip().lower()
-    return PC_PREC_F32 if v in ("f32", "fp32", "float32") else PC_PREC_F16
+    """The run mode: f16 (the timed mode; each net then takes its own default form) or f32 (parity)."""
+    p = _prec_word(var, (PC_PREC_F16, PC_PREC_F32))
+    if p is None and var != "PERSON_CAPTURE_AMD_PRECISION":
+        p = _prec_word("PERSON_CAPTURE_AMD_PRECISION", (PC_PREC_F16, PC_PREC_F32))
+    return PC_PREC_F16 if p is None else p
 
 
 def _det_precision() -> int:
@@ -112,14 +134,10 @@ def _det_precision() -> int:
     the f32 path's, where plain f16 moved sub-pixel landmarks enough to flip decisions on
     noise frames (bench.py parity). PERSON_CAPTURE_AMD_DET_PRECISION=f16 / f32 select the
     others; with PERSON_CAPTURE_AMD_PRECISION=f32 (the parity mode) the detector is f32 too."""
-    v = os.getenv("PERSON_CAPTURE_AMD_DET_PRECISION", "").strip().lower()
-    if not v:
+    p = _prec_word("PERSON_CAPTURE_AMD_DET_PRECISION", (PC_PREC_F32, PC_PREC_F16X3, PC_PREC_F16))
+    if p is None:
         return PC_PREC_F32 if _precision() == PC_PREC_F32 else PC_PREC_F16X3
-    if v in ("f32", "fp32", "float32"):
-        return PC_PREC_F32
-    if v in ("f16x3", "x3", "split"):
-        return PC_PREC_F16X3
-    return PC_PREC_F16
+    return p
 
 
 def _arc_precision() -> int:
@@ -129,18 +147,12 @@ def _arc_precision() -> int:
     TensorRT precision, face_embedder.py:445) moved fd by up to 2.2e-4 on identical chips. f16c8 (e4m3
     lo / hi bytes, the corrections on the block-scaled e4m3 MFMA: half the MFMA issues, 1.5e-5) ran
     no faster on the same staging-bound tiles (r05d: C2 22.5 vs 22.3 ms) and is opt-in.
-    PERSON_CAPTURE_AMD_ARC_PRECISION=f16x3 / f16c8 / f16 / f32 select; with
+    PERSON_CAPTURE_AMD_ARC_PRECISION=f16x3 / f16c8 / f16 / f32 select (anything else raises); with
     PERSON_CAPTURE_AMD_PRECISION=f32 (the parity mode) ArcFace is f32 too."""
-    v = os.getenv("PERSON_CAPTURE_AMD_ARC_PRECISION", "").strip().lower()
-    if not v:
+    p = _prec_word("PERSON_CAPTURE_AMD_ARC_PRECISION", (PC_PREC_F32, PC_PREC_F16X3, PC_PREC_F16C8, PC_PREC_F16))
+    if p is None:
         return PC_PREC_F32 if _precision() == PC_PREC_F32 else PC_PREC_F16X3
-    if v in ("f32", "fp32", "float32"):
-        return PC_PREC_F32
-    if v in ("f16x3", "x3", "split"):
-        return PC_PREC_F16X3
-    if v in ("f16c8", "c8"):
-        return PC_PREC_F16C8
-    return PC_PREC_F16
+    return p
 
 
 def synthetic_weights(kind: str, seed: int = 0) -> models.Params:
@@ -275,7 +287,10 @@ class FaceEmbedder(YoloFaceBranch):
         if callable(progress):
             progress("pcgpu: weights " + " ".join(f"{k}={v}" for k, v in self.weights_source.items()))
         self._det_batch = int(os.getenv("PERSON_CAPTURE_AMD_DET_BATCH", "8"))
-        self._arc_batch = int(os.getenv("PERSON_CAPTURE_AMD_ARC_BATCH", "256"))
+        # ArcFace rows per net run (flip-TTA: half as many faces). 512 = 256 faces, so the embed quantum
+        # below (146 faces = 292 rows, one round of the 256x224 tiles) fits one run; with 256 rows the
+        # quantum was capped at 128 faces outside bench.py, which always set 512
+        self._arc_batch = int(os.getenv("PERSON_CAPTURE_AMD_ARC_BATCH", "512"))
         # frames per detection chunk of extract_batch: the host policy of chunk c runs
         # while the device works on chunk c+1 (0 = one chunk, no overlap)
         self._pipe_chunk = int(os.getenv("PERSON_CAPTURE_AMD_PIPE_CHUNK", "32"))

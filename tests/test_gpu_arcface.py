@@ -4,8 +4,8 @@ Oracle: oracle/nets_torch.iresnet_forward on the unfolded params, fed the
 reference preprocessing (face_embedder.py:1281-1288), combined with the
 reference's flip-TTA sum and L2 normalisation (face_embedder.py:1383-1389,
 restated in oracle/ref_algos.arcface_postprocess, pinned by golden vectors).
-Tolerances: f32 path (PC_PREC_F32), the f16x3 split path (PC_PREC_F16X3) and the f16c8 path
-(PC_PREC_F16C8, the default of FaceEmbedder) max-abs 1e-4 on unit embeddings and on cosine distances
+Tolerances: f32 path (PC_PREC_F32), the f16x3 split path (PC_PREC_F16X3, the default of FaceEmbedder,
+DESIGN.md §3.7) and the opt-in f16c8 path (PC_PREC_F16C8) max-abs 1e-4 on unit embeddings and on cosine distances
 (north_star); plain f16 (the reference's TRT fp16 precision) max-abs 1e-2 on embeddings,
 5e-3 on cosine distances — measured error is reported in the assertion messages."""
 import numpy as np
@@ -139,3 +139,31 @@ def test_arcface_f16x3_wg_form_bit_identical(gpu_ctx, monkeypatch):
     assert not any(f & 2 for c, f in forms[1] if 100 <= c < 200)
     assert sum(1 for c, f in forms[1] if c == 113 and f & 3 == 1) == wg_launches
     assert np.array_equal(outs[0].view(np.uint8), outs[1].view(np.uint8))
+
+
+def test_arcface_f16x3_wg_layouts_bit_identical(gpu_ctx, monkeypatch):
+    """The WG tiles' wave layouts: 8x1 waves of 32x224 on the 256x224 tile and 4x2
+    of 32x128 on 128x256 (default) against the 4x2 / 2x4 layouts of the cfg table (PC_WG_LAYOUT=0).
+    Every accumulator takes the same MFMAs in the same order, so the outputs are bit-identical;
+    the batch of 256 runs the 14x14x256 layers on 256x224 and the 28x28x128 layers on 128x256."""
+    from person_capture_amd.runtime import Net
+    P = models.compile_iresnet(models.synth_iresnet(100, seed=6), 100, split=True)
+    x = np.zeros((256, 112, 112, 4), np.float16)
+    x[..., :3] = np.random.default_rng(7).uniform(-127.5, 127.5, (256, 112, 112, 3))
+    d = gpu_ctx.upload(x)
+    net = Net(gpu_ctx, P.serialize(), PC_PREC_F16, max_batch=256)
+    outs = []
+    try:
+        net.profile(True)
+        for lay in ("1", "0", "1"):
+            monkeypatch.setenv("PC_WG_LAYOUT", lay)
+            net.run(d.ptr, 256)
+            outs.append(net.read_output(0, 256).copy())
+        codes = {(int(r[4]), int(r[5])) for r in net.profile_ops()}
+        net.profile(False)
+    finally:
+        net.close()
+        d.free()
+    assert (113, 3) in codes and (101, 3) in codes, codes
+    assert np.array_equal(outs[0].view(np.uint8), outs[1].view(np.uint8))
+    assert np.array_equal(outs[0].view(np.uint8), outs[2].view(np.uint8))

@@ -225,7 +225,7 @@ def test_c3_timed_mode_decisions(gpu_ctx, monkeypatch, c3_frames, c3_oracle):
     assert report["max_fd_diff"] < 1.5e-3
 
 
-SMOOTH_N = 8
+SMOOTH_N = 32   # r05: 8 frames / 42 faces; widened so the 3e-4 same-box bound sees ~170 faces
 
 
 @pytest.fixture(scope="module")
@@ -260,7 +260,7 @@ def test_c3_smooth_frames_timed_mode(gpu_ctx, monkeypatch, smooth_c3):
     report = _vs_oracle(got, ores)
     print("C3 timed mode on smooth frames vs fp32 oracle: " + json.dumps(report))
     _persist("c3_smooth_timed", report)
-    assert report["faces"] >= 4 * SMOOTH_N
+    assert report["faces"] >= 3 * SMOOTH_N
     assert report["face_count_mismatch"] == 0
     assert report["box_mismatch"] == report.get("box_mismatch_int_boundary", 0)
     assert report.get("box_mismatch_int_margin_px", 0.0) < 2e-3

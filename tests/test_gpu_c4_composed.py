@@ -20,6 +20,13 @@ crops in order) -> ReID tower on the same crop views.
 test_c4_composed_f32: SCRFD-2.5G + IResNet-50 + ViT-L/14 at depth 2 over 2 frames (the CPU
 oracle within seconds per crop). test_c4_full_nets_f32: the configured networks, SCRFD-10G +
 IResNet-100 + the full 24-layer ViT-L/14, on the first person crops of one frame.
+test_c4_timed_mode: the mode bench.py --workload c4 times - YOLOv8n f16 (the reference's own
+predict precision, detectors.py:80, 274), SCRFD f16x3 + ArcFace f16x3 (f32 class), ReID f32 - over
+2 frames / up to 4 crops. The f16 person boxes are checked against the oracle's at f16 tolerance
+(1 px, conf 5e-3) and the face pass then runs on the DEVICE's crops for both sides, so the face
+checks are those of the f32 test: identical int boxes (one face may sit on the int() boundary of
+_accumulate, face_embedder.py:2214-2239, where any non-bitwise path can land one pixel over),
+exact or chained chips, embeddings within 1e-4, device fd = fd_min within 1e-5.
 """
 import numpy as np
 import pytest
@@ -72,14 +79,28 @@ def test_c4_full_nets_f32(gpu_ctx, monkeypatch):
     _c4(monkeypatch, "10g", 100, "ViT-L-14", 1, 2)
 
 
-def _c4(monkeypatch, variant, depth, vit, nframes, max_crops):
-    monkeypatch.setenv("PERSON_CAPTURE_AMD_PRECISION", "f32")
+def test_c4_timed_mode(gpu_ctx, monkeypatch):
+    monkeypatch.setenv("PERSON_CAPTURE_AMD_ARCFACE", "iresnet50")
+    _c4(monkeypatch, "2.5g", 50, "ViT-L-14-d2", NFRAMES, MAX_CROPS, timed=True)
+
+
+def _c4(monkeypatch, variant, depth, vit, nframes, max_crops, timed=False):
+    if timed:   # bench.py c4's timed mode: every net at its default form
+        for v in ("PERSON_CAPTURE_AMD_PRECISION", "PERSON_CAPTURE_AMD_DET_PRECISION",
+                  "PERSON_CAPTURE_AMD_ARC_PRECISION"):
+            monkeypatch.delenv(v, raising=False)
+    else:
+        monkeypatch.setenv("PERSON_CAPTURE_AMD_PRECISION", "f32")
     monkeypatch.setenv("PERSON_CAPTURE_AMD_REID_PRECISION", "f32")
     frames = bench.synth_frames(0, nframes)
     H, W = frames.shape[1:3]
     det = PersonDetector("yolov8n.pt", device="cuda:0")
     fe = fe_mod.FaceEmbedder(ctx="cuda:0", yolo_model=f"scrfd_{variant}_bnkps", conf=FACE_CONF)
     assert fe._arc_depth == depth and fe.scrfd_variant == variant
+    if timed:
+        from person_capture_amd._lib import PC_PREC_F16, PC_PREC_F16X3
+        assert det.precision == PC_PREC_F16
+        assert fe.det_precision == PC_PREC_F16X3 and fe.arc_precision == PC_PREC_F16X3
     fe.debug_chips = True
     reid = ReIDEmbedder(device="cuda:0", model_name=vit)
     ctx = fe._ctx
@@ -97,16 +118,19 @@ def _c4(monkeypatch, variant, depth, vit, nframes, max_crops):
         x = torch.from_numpy(np.ascontiguousarray(canvas[None].transpose(0, 3, 1, 2)))
         heads = [t[0].numpy() for t in nt.yolov8_forward(det._params, "n", x)]
         want = ra.yolo_postprocess(heads, 0.35, 0.45, 40, Hp, Wp, H, W)
-        near = ra.yolo_postprocess(heads, 0.35 - 1e-4, 0.45, 40, Hp, Wp, H, W)
+        ctol = 5e-3 if timed else 1e-4   # f16 YOLO heads (timed) / f32
+        near = ra.yolo_postprocess(heads, 0.35 - ctol, 0.45, 40, Hp, Wp, H, W)
         assert len(near) == len(want), f"frame {fi}: a person candidate sits at the threshold"
         assert len(got) == len(want), f"frame {fi}: {len(got)} persons vs oracle {len(want)}"
-        np.testing.assert_allclose(got[:, :4], want[:, :4], atol=1e-2)
-        np.testing.assert_allclose(got[:, 4], want[:, 4], atol=1e-4)
+        if timed and len(want):   # f16 confidences may swap the order of near-equal persons: pair by box
+            want = want[[int(np.abs(want[:, :4] - g[:4]).sum(1).argmin()) for g in got]]
+        np.testing.assert_allclose(got[:, :4], want[:, :4], atol=1.0 if timed else 1e-2)
+        np.testing.assert_allclose(got[:, 4], want[:, 4], atol=ctol)
         for g, w in zip(got, want):
             n_boxes += 1
             gi, wi = _clamp(g, H, W), _clamp(w, H, W)
             for a, b, v in zip(gi, wi, w[:4]):
-                assert a == b or _near_int(float(v)), (fi, gi, wi)
+                assert a == b or _near_int(float(v)) or timed, (fi, gi, wi)
             x1, y1, x2, y2 = gi
             if x2 <= x1 + 2 or y2 <= y1 + 2:
                 continue
@@ -126,7 +150,7 @@ def _c4(monkeypatch, variant, depth, vit, nframes, max_crops):
     fe = fe2
     o = op.OracleFaceEmbedder(fe._scrfd_params, variant, fe._arc_params, depth, conf=FACE_CONF,
                               rot_phase=id(fe) & 7)
-    n_exact = n_chained = 0
+    n_exact = n_chained = n_boundary = 0
     for ci, (crop, g) in enumerate(zip(crops, got)):
         r = o.extract(crop)
         print(f"crop {ci} {crop.shape[:2]}: {len(g)} faces, oracle {len(r)} ({o.trace})", flush=True)
@@ -134,8 +158,14 @@ def _c4(monkeypatch, variant, depth, vit, nframes, max_crops):
         gs = sorted(g, key=lambda f: tuple(f["bbox"]))
         rs = sorted(r, key=lambda f: tuple(f["bbox"]))
         for a, b in zip(gs, rs):
-            assert np.array_equal(a["bbox"], b["bbox"]), (ci, a["bbox"], b["bbox"])
             assert abs(a["fd"] - ra.fd_min(a["feat"], bank_h)) < 1e-5, ci
+            if timed and not np.array_equal(a["bbox"], b["bbox"]):
+                # the int() boundary of _accumulate: one coordinate one pixel over, at most one face
+                assert np.abs(np.asarray(a["bbox"]) - np.asarray(b["bbox"])).max() <= 1 and n_boundary == 0, \
+                    (ci, a["bbox"], b["bbox"])
+                n_boundary += 1
+                continue
+            assert np.array_equal(a["bbox"], b["bbox"]), (ci, a["bbox"], b["bbox"])
             if np.array_equal(a["chip"], b["chip"]):
                 assert np.abs(a["feat"] - b["feat"]).max() < TOL, ci
                 assert abs(a["quality"] - b["quality"]) <= 1e-9 * max(1.0, b["quality"])
@@ -155,5 +185,7 @@ def _c4(monkeypatch, variant, depth, vit, nframes, max_crops):
     xr = torch.stack([nt.clip_preprocess_pil(c) for c in crops])
     ref = torch.nn.functional.normalize(nt.clip_vit_forward(clip_weights(vit, 0), vit, xr), dim=1).numpy()
     assert np.abs(feats - ref).max() < TOL
-    print(f"C4 composed f32 ({variant}, r{depth}, {vit}): {n_boxes} persons in {nframes} frames, {len(crops)} crops, "
-          f"{n_exact} faces exact + {n_chained} chained, ReID max |d| {np.abs(feats - ref).max():.2e}")
+    print(f"C4 composed {'timed' if timed else 'f32'} ({variant}, r{depth}, {vit}): {n_boxes} persons in {nframes} "
+          f"frames, {len(crops)} crops, {n_exact} faces exact + {n_chained} chained + {n_boundary} int-boundary, "
+          f"ReID max |d| {np.abs(feats - ref).max():.2e}")
+    assert n_exact + n_chained > 0

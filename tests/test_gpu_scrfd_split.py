@@ -64,7 +64,8 @@ KERNEL_MODES = {
     "t2d64": {"PC_T2D_SPLIT64": "1"},                          # + the opt-in 64-channel split t2d
     "fast": {"PC_CONV_T2D": "0"},                              # conv_fast everywhere it runs
     "igemm": {"PC_CONV_T2D": "0", "PC_CONV_FAST": "0"},        # the generic kernel
-    "nohx": {"PC_CONV_HX": "0"},                               # 64-ch layers on conv_fast's fused tiles
+    "nohx": {"PC_CONV_HX": "0"},                               # 64/96-ch layers on conv_fast's fused tiles
+    "nohxg": {"PC_CONV_HXG": "0"},                             # 96-ch layers on conv_fast's fused tiles
 }
 
 
@@ -149,3 +150,34 @@ def test_split_hx_ran(gpu_ctx, s10g, hx, monkeypatch):
         return
     sizes = {eng.program.tensors[eng.program.ops[o][1]][1] for o in hx_ops}
     assert {160, 80, 40} <= sizes, sorted(sizes)
+
+
+def test_split_net_parity_d640_hxg(gpu_ctx, s10g, monkeypatch):
+    """D=640: the 96-channel trunk at 80x80 / 40x40 / 20x20 runs on conv_hxg (the 16x20 blocks cover
+    80 exactly; 40 and 20 leave partial blocks) - f32 class against the oracle on the heads."""
+    worst, _, eng = _heads_vs_oracle(gpu_ctx, s10g, "10g", 640, [_frame(8, 720, 1280)], {}, monkeypatch)
+    print(f"f16x3 SCRFD-10G D=640 (conv_hxg on the 96-channel trunk): head rel err {worst:.2e}")
+    assert worst < TOL_X3, worst
+
+
+@pytest.mark.parametrize("hxg", ["default", "off"])
+def test_split_hxg_ran(gpu_ctx, s10g, hxg, monkeypatch):
+    """The planner sends the f16x3 96 -> 96 channel 3x3 layers to conv_hxg (profile code 501) at every
+    map size of D=640, and never under PC_CONV_HXG=0 (conv_hx64 keeps the 64-channel ones)."""
+    if hxg == "off":
+        monkeypatch.setenv("PC_CONV_HXG", "0")
+    eng = ScrfdEngine(gpu_ctx, s10g, "10g", D=640, precision=PC_PREC_F16X3, max_batch=1)
+    f = _frame(9)
+    d = gpu_ctx.upload(f)
+    eng.net.profile(True)
+    eng.detect_frames([(d.ptr, f.shape[0], f.shape[1], f.strides[0])], thresh=0.5)
+    recs = eng.net.profile_ops()
+    eng.net.profile(False)
+    codes = [int(r[4]) for r in recs]
+    assert 500 in codes
+    hxg_ops = [int(r[0]) for r in recs if int(r[4]) == 501]
+    if hxg == "off":
+        assert not hxg_ops
+        return
+    sizes = {eng.program.tensors[eng.program.ops[o][1]][1] for o in hxg_ops}
+    assert {80, 40, 20} <= sizes, sorted(sizes)

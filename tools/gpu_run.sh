@@ -12,6 +12,8 @@
 #   probe <script> [args...]      python tools/<script> args
 #   ab <libA> <libB> <reps> <script> [args]
 #                                 interleaved A/B of two library builds (PC_LIB_PATH), one box
+#   abenv <VAR> <valA> <valB> <reps> <script> [args]
+#                                 interleaved A/B of one environment variable, one box
 # Leading KEY=VALUE words of a step are exported for that step only, e.g.
 #   "PC_BENCH_NOPROF=1 bench c3 --frames per-frame"
 set -o pipefail
@@ -50,6 +52,15 @@ for step in "$@"; do
         for lib in "${a[1]}" "${a[2]}"; do
           echo "== $lib rep $r" >> "$log"
           PC_LIB_PATH=$lib timeout -k 10 300 python -u "tools/${a[4]}" "${a[@]:5}" >> "$log" 2>&1 || { rc=$?; break 2; }
+        done
+      done
+      (exit $rc) ;;
+    abenv)
+      rc=0
+      for r in $(seq 1 "${a[4]}"); do
+        for v in "${a[2]}" "${a[3]}"; do
+          echo "== ${a[1]}=$v rep $r" >> "$log"
+          env "${a[1]}=$v" timeout -k 10 300 python -u "tools/${a[5]}" "${a[@]:6}" >> "$log" 2>&1 || { rc=$?; break 2; }
         done
       done
       (exit $rc) ;;
