@@ -464,6 +464,8 @@ def _kernel_of(code: float, cfg: float) -> str:
         return "conv_hx64 (halo-staged f16x3, pc_conv_hx.hip)"
     if c == 501:
         return "conv_hxg<96,96,5> (halo-staged f16x3 per 32-channel group, pc_conv_hx.hip)"
+    if c == 502:
+        return "conv_hxi<256> (image-resident f16x3 14x14, pc_conv_hxi.hip)"
     if c >= 200:
         return f"conv_t2d (2-D block kernel, variant {c - 200})"
     if c >= 100:
@@ -1218,7 +1220,16 @@ def main_other(args):
         # FaceEmbedder's host phase timers on
         phases = {}
         fe.host_times = {}
+        fe.fb_stats[:] = [0, 0]
+        fe.fb_kind_stats.clear()
+        fe.spec_stats[:] = [0, 0]
+        n_eng = len(fe._scrfd_engines)
         step(phases)
+        stats["face_pass_counts_one_step"] = {
+            "zero_degree_speculative_hit_rerun": list(fe.spec_stats),
+            "fallback_prefetched_inline": list(fe.fb_stats),
+            "fallback_by_kind_prefetched_inline": {k: list(v) for k, v in fe.fb_kind_stats.items()},
+            "scrfd_det_sizes": sorted(fe._scrfd_engines), "scrfd_engines_created_in_step": len(fe._scrfd_engines) - n_eng}
         phases.pop("_t", None)
         stats["phase_ms_one_step"] = phases
         stats["face_host_phase_ms_one_step"] = {k: round(v * 1e3, 3) for k, v in fe.host_times.items()}

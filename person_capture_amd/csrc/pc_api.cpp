@@ -31,6 +31,7 @@ hipError_t conv_halo_launch(int f32, int cfg, const ConvParams& p, hipStream_t s
 hipError_t conv_fast_launch(int f32, int rowb, int cfg, const ConvParams& p, hipStream_t s);
 hipError_t conv_hx_launch(const ConvParams& p, hipStream_t s);
 hipError_t conv_hxg_launch(const ConvParams& p, hipStream_t s);
+hipError_t conv_hxi_launch(const ConvParams& p, hipStream_t s);
 int conv_fast_num_cfgs();
 constexpr int kFastSmallCfg0 = 15, kFastSmallCfg1 = 19;   // conv_fast tiles 15..19: small-batch plans only
 int conv_fast_tile(int cfg, int* bc, int* bp);
@@ -910,6 +911,21 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
       pl.fast = pl.halo = pl.t2d = -1;
       pl.sx = 0;
     }
+    // IResNet's 14x14x256 -> 256 layers at batches that give every CU an image (plans for >= 192
+    // images) on the image-resident conv_hxi: bit-identical to the fused tiles the smaller plan classes
+    // run (same K order, MFMA order and epilogue arithmetic). Opt-in (PC_CONV_HXI=1): alone it ran
+    // 157 vs 159 us per b256 launch against the 256x224 WG tile, and beside the SCRFD stream in C3 (383
+    // rows: 1.5 rounds of 133 KB workgroups) 278 vs 237 us (profiles/r06c_*).
+    if (plan_batch >= 192 && X.split && !X.c8 && !Y.c8 && X.C == 512 && X.cs == 512 && Y.split && Y.C == 512 &&
+        Y.cs == 512 && npad == 256 && w[4] == 3 && w[5] == 3 && w[6] == 1 && w[7] == 1 && X.H == 14 && X.W == 14 &&
+        Y.H == 14 && Y.W == 14 && w[15] == 9 * 768 &&
+        !(w[21] >= 0 && (w[22] == RES_UP2 || !n->tens[w[21]].split || n->tens[w[21]].c8)) &&
+        (double)X.H * X.W * n->max_batch * X.cs * esz + kZeroTail < 4294967296.0 &&
+        getenv("PC_CONV_HXI") && atoi(getenv("PC_CONV_HXI")) == 1) {
+      pl.hx = 3;
+      pl.fast = pl.halo = pl.t2d = -1;
+      pl.sx = 0;
+    }
   }
   // small-batch plan: a long-K conv of a few images fills a fraction of the CUs (a 14x14x256
   // conv of 12 rows: 56 workgroups of 2304-long K) - split K over the generic kernel so the
@@ -1642,7 +1658,9 @@ static int run_ops(pc_net* n, int N, hipStream_t s) {
       p.partial = n->partial;
       p.zero = c->zero;
       if (const char* e = getenv("PC_CONV_DBG")) p.dbg = atoi(e);
-      if (pl.hx == 2) {
+      if (pl.hx == 3) {
+        HIPCHK(c, conv_hxi_launch(p, s));
+      } else if (pl.hx == 2) {
         HIPCHK(c, conv_hxg_launch(p, s));
       } else if (pl.hx) {
         HIPCHK(c, conv_hx_launch(p, s));
@@ -1855,7 +1873,7 @@ extern "C" int pc_net_profile_ops(pc_net* n, double* out, int max_recs) {
     o[0] = r.op; o[1] = r.kind; o[2] = ms; o[3] = r.flops;
     const ConvPlan* pl = conv ? (r.small >= 0 ? &n->plans_cls[r.small][r.op] : &n->plans[r.op]) : nullptr;
     o[4] = r.code >= 0 ? r.code
-                       : conv ? (pl->hx            ? 499 + pl->hx   // 500 conv_hx64, 501 conv_hxg
+                       : conv ? (pl->hx            ? 499 + pl->hx   // 500 conv_hx64, 501 conv_hxg, 502 conv_hxi
                                  : pl->c8          ? 600 + pl->fast
                                  : pl->t2d >= 0    ? 200 + pl->t2d
                                  : pl->fast >= 0   ? 100 + pl->fast

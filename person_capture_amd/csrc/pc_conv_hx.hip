@@ -222,7 +222,7 @@ __global__ __launch_bounds__(256, 1) void conv_hxg(ConvParams p, int nby, int nb
   constexpr int TC = COUT / 16, NG = CIN / 32, NKS = 9 * NG;
   constexpr int BW = 16, BH = 4 * TP, PW = BW + 2, SLOTS = (BH + 2) * PW;
   constexpr int SB = 128;                                    // slot: 32 hi + 32 lo f16 channels
-  constexpr int PIECES = (SLOTS * SB / 1024 + 3) / 4 * 4;    // 1 KiB DMA pieces per stage, 4 waves alike
+  constexpr int PIECES = ((SLOTS * SB + 1023) / 1024 + 3) / 4 * 4;   // 1 KiB DMA pieces per stage, 4 waves alike
   constexpr int STAGE = PIECES * 1024;
   constexpr int RS = COUT + 4;                               // epilogue image row (floats)
   constexpr int EPI = BH * BW * RS * 4;

@@ -381,6 +381,8 @@ class FaceEmbedder(YoloFaceBranch):
         self._fb_cache: Dict[tuple, tuple] = {}
         self.fb_stats = [0, 0]   # fallback detections served by the batched prefetch / run one by one
         self.fb_kind_stats: Dict[str, List[int]] = {}   # the same per view kind ("tta", "pad", "rot")
+        # 0-degree passes served by the speculative batch / re-run because the state changed the det size
+        self.spec_stats = [0, 0]
         if self.detector_backend == "scrfd":
             self.scrfd = self._engine(640)
             if callable(progress):
@@ -642,7 +644,13 @@ class FaceEmbedder(YoloFaceBranch):
         self._fb_run(jobs)
 
     def _detect_once(self, img: _DevImage, dyn: int, conf: float):
-        return self._detect_batch([img], dyn, conf)[0]
+        if self.host_times is None:
+            return self._detect_batch([img], dyn, conf)[0]
+        t = time.perf_counter()   # (diagnostics: the synchronous detections inside the policy walk)
+        r = self._detect_batch([img], dyn, conf)[0]
+        self.host_times["inline_detect_within_policy"] = self.host_times.get("inline_detect_within_policy", 0.0) + \
+            time.perf_counter() - t
+        return r
 
     def _dev_rotate_pad(self, img: _DevImage, deg: int, pad: int, key: str) -> _DevImage:
         rh, rw = (img.W, img.H) if deg in (90, 270) else (img.H, img.W)
@@ -801,6 +809,7 @@ class FaceEmbedder(YoloFaceBranch):
                     continue
                 self._frame_idx += 1
                 dyn = self._dyn_for(im, imgsz)
+                self.spec_stats[0 if dyn == spec_dyn[i] else 1] += 1
                 first = spec[i] if dyn == spec_dyn[i] else self._detect_once(im, dyn, float(self.conf))
                 kept = self._scrfd_policy(im, dyn, first)
                 faces_per_frame[i] = kept

