@@ -156,6 +156,15 @@ VARIANTS = {
     "net + blk stages 1,2 + stream+in1": lambda s, st: s in NET or s in ("stream", "in1") or (s in BLK and st in (1, 2)),
     "net + blk 1,2,4 + stream+in1": lambda s, st: s in NET or s in ("stream", "in1") or (s in BLK and st in (1, 2, 4)),
 
+    # round 6: one operand of the 14x14x256 stage (stage 3: 58 of the 100 convs, 46 % of the x3 time)
+    # in f16 (2 MFMAs per product there), everything else split
+    "all split but w1,w2 at st3": lambda s, st: not (s in ("w1", "w2") and st == 3),
+    "all split but w2 at st3": lambda s, st: not (s == "w2" and st == 3),
+    "all split but w1 at st3": lambda s, st: not (s == "w1" and st == 3),
+    "all split but y1 at st3": lambda s, st: not (s == "y1" and st == 3),
+    "all split but in1 at st3": lambda s, st: not (s == "in1" and st == 3),
+    "all split but y1 at st2,3": lambda s, st: not (s == "y1" and st in (2, 3)),
+    "all split": lambda s, st: True,
     "f16": rule(),
     "stream": rule(["stream"]),
     "stream+in1": rule(["stream", "in1"]),
