@@ -911,17 +911,22 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
       pl.fast = pl.halo = pl.t2d = -1;
       pl.sx = 0;
     }
-    // IResNet's 14x14x256 -> 256 layers at batches that give every CU an image (plans for >= 192
-    // images) on the image-resident conv_hxi: bit-identical to the fused tiles the smaller plan classes
-    // run (same K order, MFMA order and epilogue arithmetic). Opt-in (PC_CONV_HXI=1): alone it ran
-    // 157 vs 159 us per b256 launch against the 256x224 WG tile, and beside the SCRFD stream in C3 (383
-    // rows: 1.5 rounds of 133 KB workgroups) 278 vs 237 us (profiles/r06c_*).
-    if (plan_batch >= 192 && X.split && !X.c8 && !Y.c8 && X.C == 512 && X.cs == 512 && Y.split && Y.C == 512 &&
-        Y.cs == 512 && npad == 256 && w[4] == 3 && w[5] == 3 && w[6] == 1 && w[7] == 1 && X.H == 14 && X.W == 14 &&
-        Y.H == 14 && Y.W == 14 && w[15] == 9 * 768 &&
+    // IResNet's 14x14x256 and 28x28x128 layers on the image-resident conv_hxi (pc_conv_hxi.hip) at
+    // batches that give every CU a workgroup (plans for >= 192 / 64 images): bit-identical to the fused
+    // tiles the smaller plan classes run (same K order, MFMA order and epilogue arithmetic).
+    // PC_CONV_HXI is a mask of the shapes it takes: bit 0 14x14x256, bit 1 28x28x128 (default 3). ArcFace-x3
+    // b256 per layer, interleaved on one box: 28x28x128 187.5 vs 224.2 us on the 128x256 WG tile,
+    // 14x14x256 149.3 vs 151.5 on the 256x224 one; C3 962 vs 930 frames/s with the embed quantum at 128
+    // faces (256 rows = one round of one-image workgroups; at 383 rows, 1.5 rounds, 876: the quantum
+    // follows, face_embedder.py), profiles/r06e_*
+    const int hxi_mask = getenv("PC_CONV_HXI") ? atoi(getenv("PC_CONV_HXI")) : 3;
+    const int hc = X.C / 2;
+    const bool hxi_shape = ((hxi_mask & 1) && hc == 256 && X.H == 14 && plan_batch >= 192) ||
+                           ((hxi_mask & 2) && hc == 128 && X.H == 28 && plan_batch >= 64);
+    if (hxi_shape && X.split && !X.c8 && !Y.c8 && X.cs == X.C && Y.split && Y.C == X.C && Y.cs == Y.C && npad == hc &&
+        w[4] == 3 && w[5] == 3 && w[6] == 1 && w[7] == 1 && X.W == X.H && Y.H == X.H && Y.W == X.W && w[15] == 27 * hc &&
         !(w[21] >= 0 && (w[22] == RES_UP2 || !n->tens[w[21]].split || n->tens[w[21]].c8)) &&
-        (double)X.H * X.W * n->max_batch * X.cs * esz + kZeroTail < 4294967296.0 &&
-        getenv("PC_CONV_HXI") && atoi(getenv("PC_CONV_HXI")) == 1) {
+        (double)X.H * X.W * n->max_batch * X.cs * esz + kZeroTail < 4294967296.0) {
       pl.hx = 3;
       pl.fast = pl.halo = pl.t2d = -1;
       pl.sx = 0;

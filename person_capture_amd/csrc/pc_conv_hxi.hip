@@ -1,49 +1,74 @@
-// Image-resident f16x3 3x3 convolution for IResNet's 14x14x256 stage (gfx950): the ArcFace-x3
-// layers that were C3's dominant kernel on conv_fast's 256x224 WG tile.
+// Image-resident f16x3 3x3 convolutions for IResNet's 28x28x128 and 14x14x256 stages (gfx950): the
+// ArcFace-x3 layers that run on conv_fast's fused WG tiles.
 //
 // conv_fast stages, per 32-channel K tile, the split pixel rows of one tap: every input pixel moves
-// L2 -> LDS nine times (the tile's 224 pixels re-read for each tap), through 4 LDS-DMA pieces per wave
-// and a barrier per K tile (1344 MFMA cycles per wave). Here one workgroup owns ONE image - every
-// output channel of its 14 x 14 pixels - and stages the image's padded halo once per group of 64 input
-// channels (16 x 16 slots + 2, hi and lo: 256-byte slots, 65 KB), in a 2-stage ring: group g + 1 lands
+// L2 -> LDS nine times (the tile's pixels re-read for each tap), through 4 LDS-DMA pieces per wave
+// and a barrier per K tile. Its 128x256 tile on 28x28x128 issues only 48 MFMAs per wave between two
+// barriers and ran at 36 % of the matrix pipe (r05/r06 per-layer probes). Here one workgroup owns
+// ROWS full output rows of one image - every output channel - and stages the rows' padded halo once
+// per group of 64 input channels (hi and lo: 256-byte slots), in a 2-stage ring: group g + 1 lands
 // while group g's 18 k-steps (9 taps x two 32-channel blocks) run; one barrier per group, none inside.
-//  * output pixels are enumerated as 14 rows x 16 slots (the halo's pitch), so a tap is one slot
-//    offset for every fragment: fragment t = output row t, columns 14 and 15 are discarded (the same
-//    12.5 % the 256x224 tile paid in idle CUs at batch 256: 224 of 256 CUs; here every CU has an image);
-//  * 8 waves, wave w = output channels 32 w .. 32 w + 31 (two 16-row fragments) x the 14 rows: the
-//    weight fragments come from the fragment-ordered copy (pc_api.cpp pack_wfrag) into registers a
-//    k-step ahead (double-buffered), the pixel fragments from the halo in two groups of 7 rows;
+//  * output pixels are enumerated as ROWS x PITCH slots (the halo's pitch: the map width + 2 padding
+//    columns, rounded up to 16), so a tap is one slot offset for every 16-slot pixel fragment; the
+//    PITCH - HW columns past the map are computed and discarded (12.5 % at 14x14 - what the 256x224
+//    tile paid in idle CUs at batch 256 - and at 28x28);
+//  * 8 waves = WCH channel groups x WPX fragment groups; a wave's weight fragments come from the
+//    fragment-ordered copy (pc_api.cpp pack_wfrag) into registers a k-step ahead (double-buffered),
+//    its pixel fragments from the halo in groups of at most 7;
 //  * K order and MFMA order are conv_fast SX / WG's exactly - channel groups of 64 (every tap of a
 //    group, the two 32-channel blocks per tap), per k-step W_lo*x_hi, W_hi*x_hi, W_hi*x_lo - and the
 //    epilogue arithmetic is conv_epilogue_lds<SPLIT>'s, so the outputs are bit-identical to the fused
 //    tiles every other plan class of the net runs (tests/test_gpu_arcface.py);
 //  * LDS chunk swizzle: chunk q of slot h holds source chunk q ^ ((h & 7) << 1) - conflict-free
 //    ds_read_b128 for 16 consecutive slots at any alignment, hi or lo, either block (checked
-//    exhaustively over the instruction's lane groups, MI355X_MICROARCH.md §LDS).
+//    exhaustively over the instruction's lane groups, MI355X_MICROARCH.md §LDS);
+//  * epilogue: the residual rows of a thread's items are requested before the accumulators go to
+//    the LDS image, so their latency overlaps the transposition (the first form loaded them item by
+//    item: 157 vs 142 us per 14x14x256 launch with and without a residual, r06).
 #include "pc_conv_common.h"
 
 namespace pc {
 
-constexpr int HXI_HW = 14;                     // map side
-constexpr int HXI_PW = 16;                     // halo pitch: 14 + 2 padding columns
-constexpr int HXI_SLOTS = 16 * 16 + 2;         // 16 halo rows + the 2 slots the discarded columns reach
-constexpr int HXI_SB = 256;                    // slot: 64 hi + 64 lo f16 channels
-constexpr int HXI_PIECES = (HXI_SLOTS * HXI_SB + 1023) / 1024;   // 65 x 1 KiB
-constexpr int HXI_STAGE = HXI_PIECES * 1024;
+constexpr int HXI_SB = 256;   // halo slot: 64 hi + 64 lo f16 channels
 
-template <int CIN>
+template <int HW, int PITCH, int ROWS, int CIN, int COUT, int WCH, int WPX>
+struct HxiGeom {
+  static constexpr int NW = WCH * WPX, NT = 64 * NW;
+  static constexpr int NF = ROWS * PITCH / 16;              // pixel fragments per workgroup
+  static constexpr int TP = NF / WPX, TC = COUT / WCH / 16;
+  static constexpr int TPG = TP > 7 ? (TP % 2 == 0 ? TP / 2 : TP) : TP;   // fragments per read group
+  static constexpr int NG = CIN / 64, NKS = NG * 18;
+  static constexpr int SLOTS = (ROWS + 2) * PITCH + 2;       // + the 2 slots discarded columns reach
+  static constexpr int PIECES = (SLOTS * HXI_SB + 1023) / 1024;
+  static constexpr int STAGE = PIECES * 1024;
+  static constexpr int NPIX = ROWS * HW;
+  static constexpr int PC = COUT * NPIX * 4 <= 131072 ? COUT : COUT / 2;   // channels per epilogue pass
+  static constexpr int NPASS = COUT / PC;
+  static constexpr int RS = PC + 4;
+  static constexpr int EPI = NPIX * RS * 4;
+  static constexpr int SMEM = 2 * STAGE > EPI ? 2 * STAGE : EPI;
+  static constexpr int CGN = PC / 8;                         // 8-channel items per pixel and pass
+  static constexpr int IT = (NPIX * CGN + NT - 1) / NT;      // items per thread and pass
+  static_assert(PITCH % 16 == 0 && PITCH >= HW + 2 && NF % WPX == 0 && TP % TPG == 0, "pixel fragments");
+  static_assert(COUT % (16 * WCH) == 0 && CIN % 64 == 0 && HW % ROWS == 0, "tiling");
+  static_assert(SMEM <= 163840, "LDS");
+  static_assert(NPASS == 1 || WCH % 2 == 0, "epilogue passes split the channel waves");
+};
+
+template <int HW, int PITCH, int ROWS, int CIN, int COUT, int WCH, int WPX>
 __global__ __launch_bounds__(512, 2) void conv_hxi(ConvParams p) {
-  constexpr int NW = 8, TC = 2, TP = HXI_HW, TPG = 7, NG = CIN / 64, NKS = NG * 18;
-  constexpr int NPIX = HXI_HW * HXI_HW;
-  constexpr int RS = 128 + 4;                  // epilogue image row: 128 channels per pass
-  constexpr int EPI = NPIX * RS * 4;
-  constexpr int SMEM = 2 * HXI_STAGE > EPI ? 2 * HXI_STAGE : EPI;
-  static_assert(CIN % 64 == 0 && SMEM <= 163840, "LDS");
-  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  using G = HxiGeom<HW, PITCH, ROWS, CIN, COUT, WCH, WPX>;
+  constexpr int NW = G::NW, NT = G::NT, TC = G::TC, TP = G::TP, TPG = G::TPG, NG = G::NG, NKS = G::NKS;
+  constexpr int STAGE = G::STAGE, PIECES = G::PIECES;
+  static_assert(NW == 8, "8 waves");
+  __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
   const ConvSeg& S = p.seg[0];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int n = xcd_remap(blockIdx.x, p.N);
+  const int wch = wave % WCH, wpx = wave / WCH;
+  constexpr int RB = HW / ROWS;                  // row blocks per image
+  const int b = xcd_remap(blockIdx.x, p.N * RB);
+  const int n = b / RB, r0 = (b - n * RB) * ROWS;
   const int fr = lane & 15, kg = lane >> 4;
 
   auto rsrc = [](const void* base) __attribute__((always_inline)) {
@@ -52,40 +77,39 @@ __global__ __launch_bounds__(512, 2) void conv_hxi(ConvParams p) {
   const __amdgpu_buffer_rsrc_t xrs = rsrc(S.x);
   const __amdgpu_buffer_rsrc_t wrs = rsrc(p.wfrag);
 
-  // this wave's halo pieces i = wave + 8 j (i < 65): LDS byte i * 1024 + lane * 16 = slot h = 4 i +
-  // lane / 16, chunk position q = lane % 16, holding source chunk c = q ^ ((h & 7) << 1): channels
-  // 8 (c & 7) .. of the group's hi (c < 8) or lo half; zeros outside the image
-  constexpr int PPW = (HXI_PIECES + NW - 1) / NW;
+  // this wave's halo pieces i = wave + 8 j: LDS byte i * 1024 + lane * 16 = slot h = 4 i + lane / 16,
+  // chunk position q = lane % 16, holding source chunk c = q ^ ((h & 7) << 1): channels 8 (c & 7) .. of
+  // the group's hi (c < 8) or lo half of input pixel (r0 - 1 + h / PITCH, h % PITCH - 1); zeros outside
+  constexpr int PPW = (PIECES + NW - 1) / NW;
   unsigned src[PPW];
 #pragma unroll
   for (int j = 0; j < PPW; ++j) {
     const int h = (wave + NW * j) * 4 + kg, q = fr;
     const int c = q ^ ((h & 7) << 1);
-    const int iy = (h >> 4) - 1, ix = (h & 15) - 1;
-    const bool ok = h < 256 && (unsigned)iy < (unsigned)HXI_HW && (unsigned)ix < (unsigned)HXI_HW;
-    src[j] = ok ? (unsigned)((n * HXI_HW + iy) * HXI_HW + ix) * (unsigned)(S.cs * 2) +
-                      (unsigned)(((c & 7) * 8 + (c >> 3) * CIN) * 2)
+    const int iy = r0 - 1 + h / PITCH, ix = h % PITCH - 1;
+    const bool ok = h < (ROWS + 2) * PITCH && (unsigned)iy < (unsigned)HW && (unsigned)ix < (unsigned)HW;
+    src[j] = ok ? (unsigned)((n * HW + iy) * HW + ix) * (unsigned)(S.cs * 2) + (unsigned)(((c & 7) * 8 + (c >> 3) * CIN) * 2)
                 : S.zero_off + (unsigned)(q << 4);
   }
   auto stage = [&](int g, int st) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < PPW; ++j) {
-      if (wave + NW * j < HXI_PIECES) {   // (wave-uniform)
+      if (wave + NW * j < PIECES) {   // (wave-uniform)
         unsigned off = src[j];
         asm volatile("" : "+v"(off));
         // the group's 64 channels ride in the scalar offset (128 bytes per group of each half)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)(smem + st * HXI_STAGE + (wave + NW * j) * 1024), 16,
-                                                 off, g * 128, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)(smem + st * STAGE + (wave + NW * j) * 1024), 16, off,
+                                                 g * 128, 0, 0);
       }
     }
   };
   // weight fragments of k-step s (packed K tile s: group s / 18, tap (s % 18) / 2, block s % 2): row
-  // blocks 2 wave, 2 wave + 1 of npad / 16, each [W_hi, W_lo] x 1 KiB
+  // blocks TC wch .. TC wch + TC - 1 of npad / 16, each [W_hi, W_lo] x 1 KiB
   const int tile = (p.npad / 16) * 2048;
   auto wload = [&](f16x8* wh, f16x8* wl, int s) __attribute__((always_inline)) {
 #pragma unroll
     for (int a = 0; a < TC; ++a) {
-      const int o = ((2 * wave + a) * 2) * 1024 + lane * 16;
+      const int o = ((TC * wch + a) * 2) * 1024 + lane * 16;
       wh[a] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, o, s * tile, 0));
       wl[a] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, o + 1024, s * tile, 0));
     }
@@ -101,10 +125,16 @@ __global__ __launch_bounds__(512, 2) void conv_hxi(ConvParams p) {
     for (int t = 0; t < TP; ++t) acc[a][t] = f32x4{0.f, 0.f, 0.f, 0.f};
   if (p.dbg & 8) return;   // tuning only (PC_CONV_DBG): prologue only
 
-  // per-lane LDS byte of (tap column dx, chunk kind) for fragment row 0, tap row 0: slot fr + dx
+  // per-lane LDS byte of (tap column dx, chunk kind) for slot fr + dx of halo row 0
   auto boff = [&](int dx, int chunk) __attribute__((always_inline)) {
     const int h = fr + dx;
     return (unsigned)(h * HXI_SB + ((chunk ^ ((h & 7) << 1)) << 4));
+  };
+  // halo slot of fragment t's first slot at tap (0, 0): fragment f = wpx * TP + t covers output row
+  // f / (PITCH / 16), columns 16 (f % (PITCH / 16)) .. +16
+  auto fslot = [&](int t) __attribute__((always_inline)) {
+    const int f = wpx * TP + t;
+    return (f / (PITCH / 16)) * PITCH + (f % (PITCH / 16)) * 16;
   };
   static_for<NG>([&](auto gc) __attribute__((always_inline)) {
     constexpr int g = decltype(gc)::value, st = g & 1;
@@ -112,7 +142,7 @@ __global__ __launch_bounds__(512, 2) void conv_hxi(ConvParams p) {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * TC) : "memory");
     __syncthreads();   // every wave's pieces of group g; every wave done reading group g - 1's stage
     if constexpr (g + 1 < NG) stage(g + 1, st ^ 1);
-    const char* base = smem + st * HXI_STAGE;
+    const char* base = smem + st * STAGE;
     static_for<18>([&](auto kc) __attribute__((always_inline)) {
       constexpr int k = decltype(kc)::value, tap = k / 2, blk = k % 2, s = g * 18 + k, q = s & 1;
       constexpr int dy = tap / 3, dx = tap % 3;
@@ -124,7 +154,7 @@ __global__ __launch_bounds__(512, 2) void conv_hxi(ConvParams p) {
         f16x8 bh[TPG], bl[TPG];
 #pragma unroll
         for (int t = 0; t < TPG; ++t)
-          bh[t] = *reinterpret_cast<const f16x8*>(base + oh + (t0 + t + dy) * HXI_PW * HXI_SB);
+          bh[t] = *reinterpret_cast<const f16x8*>(base + oh + (fslot(t0 + t) + dy * PITCH) * HXI_SB);
 #pragma unroll
         for (int a = 0; a < TC; ++a)
 #pragma unroll
@@ -133,7 +163,7 @@ __global__ __launch_bounds__(512, 2) void conv_hxi(ConvParams p) {
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int t = 0; t < TPG; ++t)
-          bl[t] = *reinterpret_cast<const f16x8*>(base + ol + (t0 + t + dy) * HXI_PW * HXI_SB);
+          bl[t] = *reinterpret_cast<const f16x8*>(base + ol + (fslot(t0 + t) + dy * PITCH) * HXI_SB);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int a = 0; a < TC; ++a)
@@ -153,33 +183,55 @@ __global__ __launch_bounds__(512, 2) void conv_hxi(ConvParams p) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (p.dbg & 4) return;   // tuning only: no epilogue
 
-  // ---- epilogue in two passes of 128 channels (waves 0-3, then 4-7, write their accumulators into
-  // an f32 [pixel][channel] image over the LDS; then every thread finishes 8 channels of one pixel
-  // per step with conv_epilogue_lds<SPLIT>'s arithmetic: bias (per channel, then the border class),
-  // residual hi + lo before or after the activation select, channel keep mask, hi / lo stores) ----
+  // ---- epilogue in NPASS passes of PC channels: the waves of a pass's channels write their
+  // accumulators into an f32 [pixel][channel] image over the LDS; then every thread finishes 8 channels
+  // of one pixel per item with conv_epilogue_lds<SPLIT>'s arithmetic: bias (per channel, then the border
+  // class), residual hi + lo before or after the activation select, channel keep mask, hi / lo stores ----
+  constexpr int NPIX = G::NPIX, RS = G::RS, PC = G::PC, NPASS = G::NPASS, CGN = G::CGN, IT = G::IT;
   float* im = reinterpret_cast<float*>(smem);
   const bool smooth = p.act == ACT_SILU || p.act == ACT_GELU;
   const bool has_res = p.res_mode != RES_NONE;
   const bool pre_act = !p.act_after_res;
+  const long long pix0 = (long long)n * HW * HW + r0 * HW;   // the workgroup's first output pixel
 #pragma unroll
-  for (int pass = 0; pass < 2; ++pass) {
+  for (int pass = 0; pass < NPASS; ++pass) {
+    // this thread's residual rows of the pass, requested before anything waits on them
+    f16x8 rh[IT], rl[IT];
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+      const int it = threadIdx.x + NT * k;
+      rh[k] = f16x8{};
+      rl[k] = f16x8{};
+      if (has_res && it < NPIX * CGN) {
+        const int pl = it / CGN, ch = pass * PC + (it - pl * CGN) * 8;
+        const f16* rp = reinterpret_cast<const f16*>(p.res) + (pix0 + pl) * p.rcs + ch;
+        rh[k] = *reinterpret_cast<const f16x8*>(rp);
+        rl[k] = *reinterpret_cast<const f16x8*>(rp + p.rsplit);
+      }
+    }
     __syncthreads();   // the stages (pass 0) / the previous pass's image are no longer read
-    if (wave / 4 == pass) {
+    if (NPASS == 1 || wch / (WCH / 2) == pass) {
 #pragma unroll
       for (int a = 0; a < TC; ++a)
 #pragma unroll
         for (int t = 0; t < TP; ++t) {
-          if (fr < HXI_HW) {
-            const int pl = t * HXI_HW + fr;
-            *reinterpret_cast<f32x4*>(im + pl * RS + (wave & 3) * 32 + a * 16 + kg * 4) = acc[a][t];
+          const int f = wpx * TP + t;
+          const int orow = f / (PITCH / 16), ocol = (f % (PITCH / 16)) * 16 + fr;
+          if (ocol < HW) {
+            const int pl = orow * HW + ocol;
+            const int cl = (NPASS == 1 ? wch : wch % (WCH / 2)) * TC * 16 + a * 16 + kg * 4;
+            *reinterpret_cast<f32x4*>(im + pl * RS + cl) = acc[a][t];
           }
         }
     }
     __syncthreads();
-    for (int it = threadIdx.x; it < NPIX * 16; it += 512) {
-      const int pl = it >> 4, cl = (it & 15) * 8, ch = pass * 128 + cl;
-      const int oy = pl / HXI_HW, ox = pl - oy * HXI_HW;
-      const long long pix = (long long)n * NPIX + pl;
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+      const int it = threadIdx.x + NT * k;
+      if (it >= NPIX * CGN) continue;
+      const int pl = it / CGN, cl = (it - pl * CGN) * 8, ch = pass * PC + cl;
+      const int oy = r0 + pl / HW, ox = pl % HW;
+      const long long pix = pix0 + pl;
       const f32x4 lo4 = *reinterpret_cast<const f32x4*>(im + pl * RS + cl);
       const f32x4 hi4 = *reinterpret_cast<const f32x4*>(im + pl * RS + cl + 4);
       float v[8] = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
@@ -190,21 +242,16 @@ __global__ __launch_bounds__(512, 2) void conv_hxi(ConvParams p) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] += 0.f;   // (conv_epilogue_lds adds a zero channel bias first)
         if (p.bias_mode == BIAS_BORDER9) {
-          const int rc = oy - 1 < 0 ? 0 : (oy + 1 >= HXI_HW ? 2 : 1);
-          const int cc = ox - 1 < 0 ? 0 : (ox + 1 >= HXI_HW ? 2 : 1);
+          const int rc = oy - 1 < 0 ? 0 : (oy + 1 >= HW ? 2 : 1);
+          const int cc = ox - 1 < 0 ? 0 : (ox + 1 >= HW ? 2 : 1);
           const float* bp = p.bias + (rc * 3 + cc) * p.npad + ch;
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[j] += bp[j];
         }
       }
-      float r[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      if (has_res) {
-        const f16* rp = reinterpret_cast<const f16*>(p.res) + pix * p.rcs + ch;
-        const f16x8 rh = *reinterpret_cast<const f16x8*>(rp);
-        const f16x8 rl = *reinterpret_cast<const f16x8*>(rp + p.rsplit);
+      float r[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) r[j] = (float)rh[j] + (float)rl[j];
-      }
+      for (int j = 0; j < 8; ++j) r[j] = (float)rh[k][j] + (float)rl[k][j];
       if (has_res && !pre_act) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] += r[j];
@@ -237,20 +284,30 @@ __global__ __launch_bounds__(512, 2) void conv_hxi(ConvParams p) {
   }
 }
 
-// can a conv run here: one 14x14 split segment of 256 channels (X.C 512 = [hi | lo], dense), 256
-// output channels written split (dense), 3x3 stride 1 pad 1, plain or same-size split residual
+// the instantiated shapes: IResNet's 14x14x256 (one image per workgroup, 8 x 1 waves of 32 channels x
+// 14 rows) and 28x28x128 (7 rows per workgroup, 4 x 2 waves of 32 channels x 7 fragments)
+#define PC_HXI_14 14, 16, 14, 256, 256, 8, 1
+#define PC_HXI_28 28, 32, 7, 128, 128, 4, 2
+
+// can a conv run here: one split segment of C channels (X.C 2 C = [hi | lo], dense) on an HW x HW map
+// of an instantiated shape, C output channels written split (dense), 3x3 stride 1 pad 1, plain or
+// same-size split residual
 int conv_hxi_ok(const ConvParams& p) {
   const ConvSeg& S = p.seg[0];
-  return p.nseg == 1 && S.C == 512 && S.cs == 512 && S.H == HXI_HW && S.W == HXI_HW && S.KH == 3 && S.KW == 3 &&
-         S.stride == 1 && S.pad == 1 && p.OH == HXI_HW && p.OW == HXI_HW && p.npad == 256 && p.ysplit == 256 &&
-         p.ycs == 512 && p.splitk == 1 && !p.out_f32 && !p.yc8 && !p.rc8 && p.ktot == 9 * 768 &&
-         p.res_mode != RES_UP2 && (p.res_mode == RES_NONE || (p.rsplit == 256 && p.rcs % 8 == 0)) &&
-         p.cwrite == 256 && p.wfrag != nullptr;
+  const int C = S.C / 2;
+  const bool shape = (S.H == 14 && C == 256) || (S.H == 28 && C == 128);
+  return shape && p.nseg == 1 && S.cs == 2 * C && S.W == S.H && S.KH == 3 && S.KW == 3 && S.stride == 1 && S.pad == 1 &&
+         p.OH == S.H && p.OW == S.H && p.npad == C && p.ysplit == C && p.ycs == 2 * C && p.splitk == 1 && !p.out_f32 &&
+         !p.yc8 && !p.rc8 && p.ktot == 9 * 3 * C && p.res_mode != RES_UP2 &&
+         (p.res_mode == RES_NONE || (p.rsplit == C && p.rcs % 8 == 0)) && p.cwrite == C && p.wfrag != nullptr;
 }
 
 hipError_t conv_hxi_launch(const ConvParams& p, hipStream_t s) {
   if (!conv_hxi_ok(p)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(conv_hxi<256>, dim3(p.N), dim3(512), 0, s, p);
+  if (p.OH == 14)
+    hipLaunchKernelGGL((conv_hxi<PC_HXI_14>), dim3(p.N), dim3(512), 0, s, p);
+  else
+    hipLaunchKernelGGL((conv_hxi<PC_HXI_28>), dim3(p.N * 4), dim3(512), 0, s, p);
   return hipGetLastError();
 }
 

@@ -298,13 +298,13 @@ class FaceEmbedder(YoloFaceBranch):
         # at the end of every detection chunk's policy (but the last), launch the faces
         # collected so far as ArcFace batches of whole quanta: the device then never waits
         # for the host to fill a full batch. The quantum is the face count whose flip-TTA
-        # images fill one round of the dominant 14x14x256 conv's 256x224 tiles over the CUs
-        # (256 CUs x 224 px / 196 px per image / 2 images per face = 146); partial rounds
-        # cost a whole round of that layer. 0 = full batches only. (Resident block chains
-        # change the round: see below. Beside the detection stream the quantum is 128 faces:
-        # their 256 rows fill 224 CUs and leave 32 to the SCRFD chunks - C3 r04: 1578 / 1596
-        # frames/s against 1561 / 1562 / 1567 with 146, profiles/r04sw_c3_pipeline_sweep.txt.)
-        self._embed_quantum = int(os.getenv("PERSON_CAPTURE_AMD_EMBED_QUANTUM", "146"))
+        # images fill one round of the dominant 14x14x256 conv over the CUs: one image per
+        # workgroup on conv_hxi (f16x3, pc_conv_hxi.hip) = 256 rows = 128 faces (round 5's
+        # 256x224 tiles: 256 CUs x 224 px / 196 px per image / 2 images per face = 146); partial
+        # rounds cost a whole round of that layer. 0 = full batches only. (Resident block chains
+        # change the round: see below. f16 beside the detection stream: 128 faces too - C3 r04:
+        # 1578 / 1596 frames/s against 1561 / 1562 / 1567 with 146, profiles/r04sw_c3_pipeline_sweep.txt.)
+        self._embed_quantum = int(os.getenv("PERSON_CAPTURE_AMD_EMBED_QUANTUM", "128"))
         # batched speculative fallback passes (TTA / edge pad / pre-scan rotations) per chunk
         self._fb_prefetch = os.getenv("PERSON_CAPTURE_AMD_FALLBACK_PREFETCH", "1") != "0"
         # host phase timers of extract_batch (diagnostics; bench.py prints them)
@@ -320,10 +320,10 @@ class FaceEmbedder(YoloFaceBranch):
         two = self.detector_backend == "scrfd" and os.getenv("PERSON_CAPTURE_AMD_EMBED_STREAM", "1") != "0"
         self._ectx = get_context(self._device_index, "embed") if two else self._ctx
         if two and "PERSON_CAPTURE_AMD_EMBED_QUANTUM" not in os.environ:
-            # (the f32-class ArcFace is ~3x the work of the f16 one and outweighs SCRFD: a full round
-            # of its tiles, 146 faces, leads - C3 r05: 912 / 908 vs 904 / 902 frames/s with 128,
-            # 824 with 192, 858 with 112, profiles/r05ae_embed_quantum_sweep.txt)
-            self._embed_quantum = 128 if self.arc_precision == PC_PREC_F16 else 146
+            # (f16: 128 faces, r04. f16x3: the 14x14x256 layers run one image per workgroup on
+            # conv_hxi (pc_conv_hxi.hip), so a round is 256 rows = 128 faces - C3 r06 962 vs 876 frames/s
+            # with the 146 of round 5's 256x224 tiles, profiles/r06e_*)
+            self._embed_quantum = 128
         # host frames (extract / extract_batch without dev_frames) reach the device through the
         # native pinned staging ring on a copy stream of their own (pc_frame_stage)
         self._h2d = get_context(self._device_index, "h2d")

@@ -173,10 +173,11 @@ def test_arcface_f16x3_wg_layouts_bit_identical(gpu_ctx, monkeypatch):
 
 @pytest.mark.parametrize("batch", [256, 300])
 def test_arcface_f16x3_hxi_bit_identical(gpu_ctx, monkeypatch, batch):
-    """conv_hxi (pc_conv_hxi.hip: one workgroup per 14x14 image, the padded halo staged per group of 64
-    input channels) runs the 58 14x14x256 -> 256 layers of a large batch (profile code
-    502) and gives the fused tiles' bits (PC_CONV_HXI=0): same K order (64-channel groups, taps, 32-
-    channel blocks), same MFMA order per k-step, conv_epilogue_lds's arithmetic."""
+    """conv_hxi (pc_conv_hxi.hip: a workgroup per 14x14 image / per 7 rows of a 28x28 image, the padded
+    halo staged per group of 64 input channels) runs the 58 14x14x256 and 24 28x28x128
+    layers of a large batch (profile code 502, PC_CONV_HXI=3: both shapes) and gives the fused tiles'
+    bits (PC_CONV_HXI=0): same K order (64-channel groups, taps, 32-channel blocks), same MFMA order per
+    k-step, conv_epilogue_lds's arithmetic (with and without residual)."""
     from person_capture_amd.runtime import Net
     P = models.compile_iresnet(models.synth_iresnet(100, seed=8), 100, split=True)
     x = np.zeros((batch, 112, 112, 4), np.float16)
@@ -184,7 +185,7 @@ def test_arcface_f16x3_hxi_bit_identical(gpu_ctx, monkeypatch, batch):
     d = gpu_ctx.upload(x)
     outs, codes = [], []
     try:
-        for hxi in ("1", "0"):   # (opt-in: the default plans keep the fused tiles)
+        for hxi in ("3", "0"):
             monkeypatch.setenv("PC_CONV_HXI", hxi)
             net = Net(gpu_ctx, P.serialize(), PC_PREC_F16, max_batch=batch)
             try:
@@ -197,6 +198,6 @@ def test_arcface_f16x3_hxi_bit_identical(gpu_ctx, monkeypatch, batch):
                 net.close()
     finally:
         d.free()
-    assert sum(1 for c in codes[0] if c == 502) == 58, codes[0]
+    assert sum(1 for c in codes[0] if c == 502) == 58 + 24, codes[0]
     assert 502 not in codes[1]
     assert np.array_equal(outs[0].view(np.uint8), outs[1].view(np.uint8))
