@@ -465,7 +465,9 @@ def _kernel_of(code: float, cfg: float) -> str:
     if c == 501:
         return "conv_hxg<96,96,5> (halo-staged f16x3 per 32-channel group, pc_conv_hx.hip)"
     if c == 502:
-        return "conv_hxi<256> (image-resident f16x3 14x14, pc_conv_hxi.hip)"
+        return "conv_hxi<14,16,14,256,256,8,1> (image-resident f16x3, one 14x14 image per workgroup, pc_conv_hxi.hip)"
+    if c == 503:
+        return "conv_hxi<28,32,7,128,128,4,2> (image-resident f16x3, 7 rows of a 28x28 image per workgroup, pc_conv_hxi.hip)"
     if c >= 200:
         return f"conv_t2d (2-D block kernel, variant {c - 200})"
     if c >= 100:
@@ -615,7 +617,13 @@ def _traffic_for(dominant, code, prec="f16"):
     """HBM bytes per launch of the rocprofv3 dominant kernel when it is the bench's dominant conv_fast
     tile: same channel x pixel tile and the same form - the template's last three flags (SPLIT, SX,
     C8) are false for f16, SX for the fused f16x3 tiles, all three for f16c8."""
-    if not dominant or code is None or not (100 <= code < 200 or 600 <= code < 700):
+    if not dominant or code is None:
+        return None
+    # the halo-staged kernels: one instantiation per code
+    hx_names = {500: "conv_hx64", 501: "conv_hxg<96, 96", 502: "conv_hxi<14, 16, 14", 503: "conv_hxi<28, 32, 7"}
+    if code in hx_names:
+        return dominant.get("hbm_bytes_per_launch") if hx_names[code] in dominant.get("kernel", "") else None
+    if not (100 <= code < 200 or 600 <= code < 700):
         return None
     bc, bp = FAST_TILES.get(code % 100, (0, 0))
     name = dominant.get("kernel", "")

@@ -927,7 +927,7 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
         w[4] == 3 && w[5] == 3 && w[6] == 1 && w[7] == 1 && X.W == X.H && Y.H == X.H && Y.W == X.W && w[15] == 27 * hc &&
         !(w[21] >= 0 && (w[22] == RES_UP2 || !n->tens[w[21]].split || n->tens[w[21]].c8)) &&
         (double)X.H * X.W * n->max_batch * X.cs * esz + kZeroTail < 4294967296.0) {
-      pl.hx = 3;
+      pl.hx = hc == 256 ? 3 : 4;   // (profile codes 502 / 503)
       pl.fast = pl.halo = pl.t2d = -1;
       pl.sx = 0;
     }
@@ -1663,7 +1663,7 @@ static int run_ops(pc_net* n, int N, hipStream_t s) {
       p.partial = n->partial;
       p.zero = c->zero;
       if (const char* e = getenv("PC_CONV_DBG")) p.dbg = atoi(e);
-      if (pl.hx == 3) {
+      if (pl.hx >= 3) {
         HIPCHK(c, conv_hxi_launch(p, s));
       } else if (pl.hx == 2) {
         HIPCHK(c, conv_hxg_launch(p, s));
@@ -1878,7 +1878,7 @@ extern "C" int pc_net_profile_ops(pc_net* n, double* out, int max_recs) {
     o[0] = r.op; o[1] = r.kind; o[2] = ms; o[3] = r.flops;
     const ConvPlan* pl = conv ? (r.small >= 0 ? &n->plans_cls[r.small][r.op] : &n->plans[r.op]) : nullptr;
     o[4] = r.code >= 0 ? r.code
-                       : conv ? (pl->hx            ? 499 + pl->hx   // 500 conv_hx64, 501 conv_hxg, 502 conv_hxi
+                       : conv ? (pl->hx            ? 499 + pl->hx   // 500 conv_hx64, 501 conv_hxg, 502 / 503 conv_hxi 14x14 / 28x28
                                  : pl->c8          ? 600 + pl->fast
                                  : pl->t2d >= 0    ? 200 + pl->t2d
                                  : pl->fast >= 0   ? 100 + pl->fast

@@ -229,7 +229,6 @@ __global__ __launch_bounds__(256, 1) void conv_hxg(ConvParams p, int nby, int nb
   constexpr int SMEM = 2 * STAGE > EPI ? 2 * STAGE : EPI;
   static_assert(COUT % 16 == 0 && CIN % 32 == 0 && CIN % 64 != 0, "32-channel groups (pack_wfrag gt 1)");
   static_assert(SMEM <= 163840, "LDS");
-  static_assert((BH * BW * (COUT / 8)) % 256 == 0, "epilogue work split");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
   const ConvSeg& S = p.seg[0];
   const int lane = threadIdx.x & 63;
@@ -349,61 +348,80 @@ __global__ __launch_bounds__(256, 1) void conv_hxg(ConvParams p, int nby, int nb
   const bool smooth = p.act == ACT_SILU || p.act == ACT_GELU;
   const bool has_res = p.res_mode != RES_NONE;
   const bool pre_act = !p.act_after_res;
-  constexpr int CGN = COUT / 8;
-  for (int it = threadIdx.x; it < BH * BW * CGN; it += 256) {
-    const int pl = it / CGN, ch = (it - pl * CGN) * 8;
-    const int oy = oy0 + pl / BW, ox = ox0 + (pl & (BW - 1));
-    if (oy >= OH || ox >= OW) continue;
-    const long long pix = ((long long)n * OH + oy) * OW + ox;
-    const f32x4 lo4 = *reinterpret_cast<const f32x4*>(im + pl * RS + ch);
-    const f32x4 hi4 = *reinterpret_cast<const f32x4*>(im + pl * RS + ch + 4);
-    float v[8] = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
-    if (p.bias_mode == BIAS_CHANNEL) {
+  // a thread keeps one 8-channel group (threads past the last whole pixel lane idle), so the channel
+  // terms load once; the pixels' residual rows are requested before the first store
+  constexpr int CGN = COUT / 8, PL = 256 / CGN, NPX = BH * BW, ITP = (NPX + PL - 1) / PL;
+  const int cg = threadIdx.x % CGN, pl0 = threadIdx.x / CGN;
+  if (pl0 >= PL) return;
+  const int ch = cg * 8;
+  float bc[8], sl[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] += p.bias[ch + j];
-    } else if (p.bias_mode == BIAS_BORDER9) {
-      const int rc = oy - 1 < 0 ? 0 : (oy + 1 >= H ? 2 : 1);
-      const int cc = ox - 1 < 0 ? 0 : (ox + 1 >= W ? 2 : 1);
-      const float* bp = p.bias + (rc * 3 + cc) * p.npad + ch;
+  for (int j = 0; j < 8; ++j) {
+    bc[j] = p.bias_mode == BIAS_CHANNEL ? p.bias[ch + j] : 0.f;
+    sl[j] = p.act == ACT_PRELU ? p.slope[ch + j] : (p.act == ACT_RELU ? 0.f : 1.f);
+  }
+  constexpr int RGP = 8;   // residual rows in flight per group of pixels
+  for (int k0 = 0; k0 < ITP; k0 += RGP) {
+    f16x8 rh[RGP], rl[RGP];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] += bp[j];
-    }
-    float r[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (has_res) {
-      const f16* rp = reinterpret_cast<const f16*>(p.res) + pix * p.rcs + ch;
-      const f16x8 rh = *reinterpret_cast<const f16x8*>(rp);
-      const f16x8 rl = *reinterpret_cast<const f16x8*>(rp + p.rsplit);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) r[j] = (float)rh[j] + (float)rl[j];
-    }
-    if (has_res && !pre_act) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] += r[j];
-    }
-    if (smooth) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j], p.act, 0.f);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float sl = p.act == ACT_PRELU ? p.slope[ch + j] : (p.act == ACT_RELU ? 0.f : 1.f);
-        v[j] = v[j] > 0.f ? v[j] : v[j] * sl;
+    for (int kk = 0; kk < RGP; ++kk) {
+      rh[kk] = f16x8{};
+      rl[kk] = f16x8{};
+      const int pl = pl0 + PL * (k0 + kk);
+      const int oy = oy0 + pl / BW, ox = ox0 + (pl & (BW - 1));
+      if (has_res && pl < NPX && oy < OH && ox < OW) {
+        const f16* rp = reinterpret_cast<const f16*>(p.res) + (((long long)n * OH + oy) * OW + ox) * p.rcs + ch;
+        rh[kk] = *reinterpret_cast<const f16x8*>(rp);
+        rl[kk] = *reinterpret_cast<const f16x8*>(rp + p.rsplit);
       }
     }
-    if (has_res && pre_act) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] += r[j];
-    }
-    f16x8 yh, yl;
+    for (int kk = 0; kk < RGP; ++kk) {
+      const int pl = pl0 + PL * (k0 + kk);
+      if (pl >= NPX) continue;
+      const int oy = oy0 + pl / BW, ox = ox0 + (pl & (BW - 1));
+      if (oy >= OH || ox >= OW) continue;
+      const long long pix = ((long long)n * OH + oy) * OW + ox;
+      const f32x4 lo4 = *reinterpret_cast<const f32x4*>(im + pl * RS + ch);
+      const f32x4 hi4 = *reinterpret_cast<const f32x4*>(im + pl * RS + ch + 4);
+      float v[8] = {lo4[0] + bc[0], lo4[1] + bc[1], lo4[2] + bc[2], lo4[3] + bc[3],
+                    hi4[0] + bc[4], hi4[1] + bc[5], hi4[2] + bc[6], hi4[3] + bc[7]};
+      if (p.bias_mode == BIAS_BORDER9) {
+        const int rc = oy - 1 < 0 ? 0 : (oy + 1 >= H ? 2 : 1);
+        const int cc = ox - 1 < 0 ? 0 : (ox + 1 >= W ? 2 : 1);
+        const float* bp = p.bias + (rc * 3 + cc) * p.npad + ch;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float x = ch + j < p.cout ? v[j] : 0.f;
-      yh[j] = (f16)x;
-      yl[j] = (f16)(x - (float)yh[j]);
+        for (int j = 0; j < 8; ++j) v[j] += bp[j];
+      }
+      float r[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] = (float)rh[kk][j] + (float)rl[kk][j];
+      if (has_res && !pre_act) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] += r[j];
+      }
+      if (smooth) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j], p.act, 0.f);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = v[j] > 0.f ? v[j] : v[j] * sl[j];
+      }
+      if (has_res && pre_act) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] += r[j];
+      }
+      f16x8 yh, yl;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float x = ch + j < p.cout ? v[j] : 0.f;
+        yh[j] = (f16)x;
+        yl[j] = (f16)(x - (float)yh[j]);
+      }
+      f16* yp = reinterpret_cast<f16*>(p.y) + pix * p.ycs + ch;
+      *reinterpret_cast<f16x8*>(yp) = yh;
+      *reinterpret_cast<f16x8*>(yp + p.ysplit) = yl;
     }
-    f16* yp = reinterpret_cast<f16*>(p.y) + pix * p.ycs + ch;
-    *reinterpret_cast<f16x8*>(yp) = yh;
-    *reinterpret_cast<f16x8*>(yp + p.ysplit) = yl;
   }
 }
 

@@ -22,9 +22,11 @@
 //  * LDS chunk swizzle: chunk q of slot h holds source chunk q ^ ((h & 7) << 1) - conflict-free
 //    ds_read_b128 for 16 consecutive slots at any alignment, hi or lo, either block (checked
 //    exhaustively over the instruction's lane groups, MI355X_MICROARCH.md §LDS);
-//  * epilogue: the residual rows of a thread's items are requested before the accumulators go to
-//    the LDS image, so their latency overlaps the transposition (the first form loaded them item by
-//    item: 157 vs 142 us per 14x14x256 launch with and without a residual, r06).
+//  * epilogue: a thread keeps one 8-channel group for all its pixels, so the channel bias and slopes
+//    are loaded once, and the per-pixel term of each of its pixels (the residual's hi + lo, or a folded
+//    pre-BN's border-class bias) is requested before the accumulators go to the LDS image, so the loads
+//    overlap the transposition (the first form loaded both per item: its epilogue took 53 of 184 us on
+//    28x28x128, profiles/r06f_hxi28_phase_split.txt).
 #include "pc_conv_common.h"
 
 namespace pc {
@@ -48,7 +50,7 @@ struct HxiGeom {
   static constexpr int EPI = NPIX * RS * 4;
   static constexpr int SMEM = 2 * STAGE > EPI ? 2 * STAGE : EPI;
   static constexpr int CGN = PC / 8;                         // 8-channel items per pixel and pass
-  static constexpr int IT = (NPIX * CGN + NT - 1) / NT;      // items per thread and pass
+  static constexpr int IT = (NPIX + NT / CGN - 1) / (NT / CGN);   // items (pixels) per thread and pass
   static_assert(PITCH % 16 == 0 && PITCH >= HW + 2 && NF % WPX == 0 && TP % TPG == 0, "pixel fragments");
   static_assert(COUT % (16 * WCH) == 0 && CIN % 64 == 0 && HW % ROWS == 0, "tiling");
   static_assert(SMEM <= 163840, "LDS");
@@ -188,25 +190,49 @@ __global__ __launch_bounds__(512, 2) void conv_hxi(ConvParams p) {
   // of one pixel per item with conv_epilogue_lds<SPLIT>'s arithmetic: bias (per channel, then the border
   // class), residual hi + lo before or after the activation select, channel keep mask, hi / lo stores ----
   constexpr int NPIX = G::NPIX, RS = G::RS, PC = G::PC, NPASS = G::NPASS, CGN = G::CGN, IT = G::IT;
+  static_assert(NT % CGN == 0, "a thread keeps one 8-channel group");
+  constexpr int PSTEP = NT / CGN;                     // pixel stride between a thread's items
   float* im = reinterpret_cast<float*>(smem);
   const bool smooth = p.act == ACT_SILU || p.act == ACT_GELU;
   const bool has_res = p.res_mode != RES_NONE;
   const bool pre_act = !p.act_after_res;
+  const bool border = p.bias_mode == BIAS_BORDER9;
   const long long pix0 = (long long)n * HW * HW + r0 * HW;   // the workgroup's first output pixel
+  const int cg = threadIdx.x % CGN, pl0 = threadIdx.x / CGN;
 #pragma unroll
   for (int pass = 0; pass < NPASS; ++pass) {
-    // this thread's residual rows of the pass, requested before anything waits on them
-    f16x8 rh[IT], rl[IT];
+    const int ch = pass * PC + cg * 8;
+    // per-thread channel terms (one 8-channel group for all of the thread's pixels): channel bias (0
+    // otherwise, as conv_epilogue_lds adds it), negative-side slope (PReLU / 0 for ReLU / 1)
+    float bc[8], sl[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      bc[j] = p.bias_mode == BIAS_CHANNEL ? p.bias[ch + j] : 0.f;
+      sl[j] = p.act == ACT_PRELU ? p.slope[ch + j] : (p.act == ACT_RELU ? 0.f : 1.f);
+    }
+    // the per-pixel term of each of the thread's items, requested before anything waits on it: the
+    // residual hi + lo (its f32 value), or the border-class bias of a folded pre-BN conv
+    float pre[IT][8];
 #pragma unroll
     for (int k = 0; k < IT; ++k) {
-      const int it = threadIdx.x + NT * k;
-      rh[k] = f16x8{};
-      rl[k] = f16x8{};
-      if (has_res && it < NPIX * CGN) {
-        const int pl = it / CGN, ch = pass * PC + (it - pl * CGN) * 8;
+      const int pl = pl0 + PSTEP * k;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pre[k][j] = 0.f;
+      if (pl >= NPIX) continue;
+      if (has_res) {
         const f16* rp = reinterpret_cast<const f16*>(p.res) + (pix0 + pl) * p.rcs + ch;
-        rh[k] = *reinterpret_cast<const f16x8*>(rp);
-        rl[k] = *reinterpret_cast<const f16x8*>(rp + p.rsplit);
+        const f16x8 rh = *reinterpret_cast<const f16x8*>(rp);
+        const f16x8 rl = *reinterpret_cast<const f16x8*>(rp + p.rsplit);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pre[k][j] = (float)rh[j] + (float)rl[j];
+      } else if (border) {
+        const int oy = r0 + pl / HW, ox = pl % HW;
+        const int rc = oy - 1 < 0 ? 0 : (oy + 1 >= HW ? 2 : 1);
+        const int cc = ox - 1 < 0 ? 0 : (ox + 1 >= HW ? 2 : 1);
+        const f32x4* bp = reinterpret_cast<const f32x4*>(p.bias + (rc * 3 + cc) * p.npad + ch);
+        const f32x4 b0 = bp[0], b1 = bp[1];
+        pre[k][0] = b0[0]; pre[k][1] = b0[1]; pre[k][2] = b0[2]; pre[k][3] = b0[3];
+        pre[k][4] = b1[0]; pre[k][5] = b1[1]; pre[k][6] = b1[2]; pre[k][7] = b1[3];
       }
     }
     __syncthreads();   // the stages (pass 0) / the previous pass's image are no longer read
@@ -227,48 +253,40 @@ __global__ __launch_bounds__(512, 2) void conv_hxi(ConvParams p) {
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < IT; ++k) {
-      const int it = threadIdx.x + NT * k;
-      if (it >= NPIX * CGN) continue;
-      const int pl = it / CGN, cl = (it - pl * CGN) * 8, ch = pass * PC + cl;
-      const int oy = r0 + pl / HW, ox = pl % HW;
+      const int pl = pl0 + PSTEP * k;
+      if (pl >= NPIX) continue;
       const long long pix = pix0 + pl;
-      const f32x4 lo4 = *reinterpret_cast<const f32x4*>(im + pl * RS + cl);
-      const f32x4 hi4 = *reinterpret_cast<const f32x4*>(im + pl * RS + cl + 4);
-      float v[8] = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
-      if (p.bias_mode == BIAS_CHANNEL) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] += p.bias[ch + j];
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] += 0.f;   // (conv_epilogue_lds adds a zero channel bias first)
-        if (p.bias_mode == BIAS_BORDER9) {
+      const f32x4 lo4 = *reinterpret_cast<const f32x4*>(im + pl * RS + cg * 8);
+      const f32x4 hi4 = *reinterpret_cast<const f32x4*>(im + pl * RS + cg * 8 + 4);
+      float v[8] = {lo4[0] + bc[0], lo4[1] + bc[1], lo4[2] + bc[2], lo4[3] + bc[3],
+                    hi4[0] + bc[4], hi4[1] + bc[5], hi4[2] + bc[6], hi4[3] + bc[7]};
+      if (border) {
+        if (has_res) {   // (both: not produced by the programs that run here; loaded in place)
+          const int oy = r0 + pl / HW, ox = pl % HW;
           const int rc = oy - 1 < 0 ? 0 : (oy + 1 >= HW ? 2 : 1);
           const int cc = ox - 1 < 0 ? 0 : (ox + 1 >= HW ? 2 : 1);
           const float* bp = p.bias + (rc * 3 + cc) * p.npad + ch;
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[j] += bp[j];
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] += pre[k][j];
         }
       }
-      float r[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) r[j] = (float)rh[k][j] + (float)rl[k][j];
       if (has_res && !pre_act) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] += r[j];
+        for (int j = 0; j < 8; ++j) v[j] += pre[k][j];
       }
       if (smooth) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j], p.act, 0.f);
       } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float sl = p.act == ACT_PRELU ? p.slope[ch + j] : (p.act == ACT_RELU ? 0.f : 1.f);
-          v[j] = v[j] > 0.f ? v[j] : v[j] * sl;
-        }
+        for (int j = 0; j < 8; ++j) v[j] = v[j] > 0.f ? v[j] : v[j] * sl[j];
       }
       if (has_res && pre_act) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] += r[j];
+        for (int j = 0; j < 8; ++j) v[j] += pre[k][j];
       }
       f16x8 yh, yl;
 #pragma unroll

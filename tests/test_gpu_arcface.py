@@ -175,7 +175,7 @@ def test_arcface_f16x3_wg_layouts_bit_identical(gpu_ctx, monkeypatch):
 def test_arcface_f16x3_hxi_bit_identical(gpu_ctx, monkeypatch, batch):
     """conv_hxi (pc_conv_hxi.hip: a workgroup per 14x14 image / per 7 rows of a 28x28 image, the padded
     halo staged per group of 64 input channels) runs the 58 14x14x256 and 24 28x28x128
-    layers of a large batch (profile code 502, PC_CONV_HXI=3: both shapes) and gives the fused tiles'
+    layers of a large batch (profile codes 502 / 503, PC_CONV_HXI=3: both shapes) and gives the fused tiles'
     bits (PC_CONV_HXI=0): same K order (64-channel groups, taps, 32-channel blocks), same MFMA order per
     k-step, conv_epilogue_lds's arithmetic (with and without residual)."""
     from person_capture_amd.runtime import Net
@@ -198,6 +198,6 @@ def test_arcface_f16x3_hxi_bit_identical(gpu_ctx, monkeypatch, batch):
                 net.close()
     finally:
         d.free()
-    assert sum(1 for c in codes[0] if c == 502) == 58 + 24, codes[0]
-    assert 502 not in codes[1]
+    assert sum(1 for c in codes[0] if c == 502) == 58 and sum(1 for c in codes[0] if c == 503) == 24, codes[0]
+    assert 502 not in codes[1] and 503 not in codes[1]
     assert np.array_equal(outs[0].view(np.uint8), outs[1].view(np.uint8))

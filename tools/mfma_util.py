@@ -50,7 +50,7 @@ def main():
                 dur[r.get("Name", "")] = float(r.get("AverageNs", 0) or 0)
     res = {}
     for name, c in rows.items():
-        if not any(t in name for t in ("conv_fast", "conv_igemm", "conv_halo", "conv_t2d", "conv_chain", "stem")):
+        if not any(t in name for t in ("conv_fast", "conv_igemm", "conv_halo", "conv_hx", "conv_t2d", "conv_chain", "stem")):
             continue
         busy = sum(c.get("SQ_VALU_MFMA_BUSY_CYCLES", [])) / max(1, len(c.get("SQ_VALU_MFMA_BUSY_CYCLES", [])))
         gui = sum(c.get("GRBM_GUI_ACTIVE", [])) / max(1, len(c.get("GRBM_GUI_ACTIVE", [])))

@@ -19,6 +19,9 @@ import os
 import sys
 from collections import defaultdict
 
+# every conv kernel family of the engine (pc_conv*.hip)
+CONV_KERNELS = ("conv_igemm", "conv_fast", "conv_halo", "conv_hx", "conv_t2d", "conv_chain")
+
 
 def load(dirs):
     vals = defaultdict(lambda: defaultdict(list))   # counter -> kernel -> [values]
@@ -41,7 +44,7 @@ def dominant_kernel(stats_csv, per_kernel):
     with open(stats_csv) as fh:
         for row in csv.DictReader(fh):
             name = row.get("Name") or row.get("KernelName") or ""
-            if not any(t in name for t in ("conv_igemm", "conv_fast", "conv_halo")):
+            if not any(t in name for t in CONV_KERNELS):
                 continue
             tot = float(row.get("TotalDurationNs", 0) or 0)
             if best is None or tot > best[1]:
@@ -73,7 +76,7 @@ def main():
     for ctr, kern in vals.items():
         for name, v in kern.items():
             per_kernel.setdefault(name, {})[ctr] = (sum(v) / len(v), len(v))
-    conv = {k: v for k, v in per_kernel.items() if any(t in k for t in ("conv_igemm", "conv_fast", "conv_halo"))}
+    conv = {k: v for k, v in per_kernel.items() if any(t in k for t in CONV_KERNELS)}
     fetch = sum(v.get("FETCH_SIZE", (0, 0))[0] * v.get("FETCH_SIZE", (0, 0))[1] for v in conv.values())
     nf = sum(v.get("FETCH_SIZE", (0, 0))[1] for v in conv.values())
     write = sum(v.get("WRITE_SIZE", (0, 0))[0] * v.get("WRITE_SIZE", (0, 0))[1] for v in conv.values())
