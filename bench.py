@@ -241,11 +241,20 @@ def hbm_kernels(fe, devs, H: int, W: int, reps: int = 20, kinds=("letterbox", "w
     out = {}
     n, D = min(32, len(devs)), 640
     if "resize_area" in kinds:   # the pre-scan downscale (gui_app.py:1505-1507): 4K -> 416 wide
+        from person_capture_amd.face_embedder import dev_resize_batch
         k = devs[0]
         nh = int(round(k.H * (416 / float(k.W))))
-        sec = timed(lambda: dev_resize(ctx, k, "hbm_area", (416, nh), 0.0, 0.0, True))
-        out["resize_area_u8"] = entry("resize_area_u8 (pc_image.hip)", f"1 frame {k.H}x{k.W} -> {nh}x416 INTER_AREA",
-                                      k.H * k.W * 3 + nh * 416 * 3, sec, "4K frame + 416-wide output", "resize_area")
+        # one speculative pre-scan chunk (the driver's batch, prescan._downscale_many): every sample's
+        # frame in one pc_resize_area_batch launch (row-staged kernel)
+        nb = min(32, len(devs))
+        keys = [f"hbm_area{i}" for i in range(nb)]
+        sec = timed(lambda: dev_resize_batch(ctx, devs[:nb], keys, (416, nh)))
+        out["resize_area_u8"] = entry("resize_area_rows_u8 (pc_image.hip)",
+                                      f"{nb} frames {k.H}x{k.W} -> {nh}x416 INTER_AREA",
+                                      nb * (k.H * k.W * 3 + nh * 416 * 3), sec, "4K frames + 416-wide outputs",
+                                      "resize_area_rows")
+        sec1 = timed(lambda: dev_resize(ctx, k, "hbm_area", (416, nh), 0.0, 0.0, True))
+        out["resize_area_u8"]["one_frame_launch_us"] = round(sec1 * 1e6, 2)
     if "letterbox" not in kinds:
         return out
     # letterbox_blob: a 32-frame detection chunk, 1080p -> 640 f16 NHWC4 blob

@@ -30,6 +30,7 @@
  *   pc_rotate_pad                      cv2.rotate + cv2.copyMakeBorder(BORDER_REPLICATE)
  *                                      (face_embedder.py:2165-2169, 2292-2294, 2394)
  *   pc_resize_area                     cv2.resize(..., INTER_AREA) (gui_app.py:1505-1507)
+ *   pc_resize_area_batch               the same over a chunk of pre-scan samples (gui_app.py:1505-1507)
  *   pc_resize_linear                   cv2.resize(..., INTER_LINEAR) (face_embedder.py:2264, 2460)
  *   pc_resize_area_fast                cv2.resize(..., INTER_AREA) at integer ratios (face_embedder.py:2460)
  *   pc_yolo_detect                     PersonDetector.detect -> [ext] ultralytics YOLO.predict(conf, iou=0.45,
@@ -240,6 +241,13 @@ int pc_resize_area_fast(pc_ctx* ctx, const uint8_t* d_src, int row_stride, int i
 int pc_resize_area(pc_ctx* ctx, const uint8_t* d_src, int row_stride, const pc_area_tab* h_xtab,
                    const int32_t* h_xstart, int n_x, const pc_area_tab* h_ytab, const int32_t* h_ystart, int n_y,
                    uint8_t* d_dst, int OH, int OW);
+/* The same cv2.resize INTER_AREA for n equally sized frames at once (the pre-scan's downscale of a
+ * speculative chunk of samples, gui_app.py:1505-1507 per sample): h_srcs / h_dsts are host arrays of n
+ * device pointers, tables as pc_resize_area. 16-byte aligned sources and row_stride take the row-
+ * staged kernel (one launch); others the per-pixel one. Output bytes equal pc_resize_area's. */
+int pc_resize_area_batch(pc_ctx* ctx, const uint8_t* const* h_srcs, uint8_t* const* h_dsts, int n, int row_stride,
+                         const pc_area_tab* h_xtab, const int32_t* h_xstart, int n_x, const pc_area_tab* h_ytab,
+                         const int32_t* h_ystart, int n_y, int OH, int OW);
 
 /* ---- detection ---- */
 /* Runs letterbox -> SCRFD net -> decode(score >= det_thresh) -> NMS(nms_thresh) for n frames.

@@ -128,6 +128,8 @@ SIGNATURES = {
     "pc_resize_area_fast": ([_P, _P, _I, _I, _I, _P, _I, _I], _I),
     "pc_resize_area": ([_P, _P, _I, C.POINTER(AreaTab), C.POINTER(C.c_int32), _I, C.POINTER(AreaTab),
                         C.POINTER(C.c_int32), _I, _P, _I, _I], _I),
+    "pc_resize_area_batch": ([_P, _P, _P, _I, _I, C.POINTER(AreaTab), C.POINTER(C.c_int32), _I, C.POINTER(AreaTab),
+                              C.POINTER(C.c_int32), _I, _I, _I], _I),
     "pc_scrfd_detect": ([_P, C.POINTER(LetterboxDesc), _I, _I, _F, _F, C.POINTER(_F), _I, _P, _P, _P, _P], _I),
     "pc_embed_finalize": ([_P, _P, _I, _I, _I, _I, _P], _I),
     "pc_arcface_embed": ([_P, _P, _I, _I, _P], _I),

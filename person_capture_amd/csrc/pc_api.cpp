@@ -75,6 +75,9 @@ hipError_t resize_area_fast_launch(const uint8_t* src, int row_stride, int isx, 
                                    hipStream_t s);
 hipError_t resize_area_launch(const uint8_t* src, int row_stride, const AreaTab* xtab, const int* xstart,
                               const AreaTab* ytab, const int* ystart, uint8_t* dst, int OH, int OW, hipStream_t s);
+hipError_t resize_area_rows_launch(const void* jobs, int n, int row_stride, const AreaTab* xtab, const int* xstart,
+                                  const AreaTab* ytab, const int* ystart, int OH, int OW, int span_bytes,
+                                  hipStream_t s);
 hipError_t embed_finalize_launch(const float* e, int ld, int n, int dim, int flip, float* out, hipStream_t s);
 hipError_t bank_match_launch(const float* q, int n, const float* bank, int B, int dim, float* fd, int* idx,
                              hipStream_t s);
@@ -2046,18 +2049,59 @@ extern "C" int pc_rotate_pad(pc_ctx* c, const uint8_t* src, int H, int W, int ro
   return PC_OK;
 }
 
+extern "C" int pc_resize_area_batch(pc_ctx* c, const uint8_t* const* srcs, uint8_t* const* dsts, int n, int row_stride,
+                                    const pc_area_tab* xt, const int32_t* xs, int n_x, const pc_area_tab* yt,
+                                    const int32_t* ys, int n_y, int OH, int OW);
+
 extern "C" int pc_resize_area(pc_ctx* c, const uint8_t* src, int row_stride, const pc_area_tab* xt,
                               const int32_t* xs, int n_x, const pc_area_tab* yt, const int32_t* ys, int n_y,
                               uint8_t* dst, int OH, int OW) {
   if (!c || !src || !dst || !xt || !xs || !yt || !ys) return fail(c, PC_ERR_ARG, "pc_resize_area: bad arguments");
+  return pc_resize_area_batch(c, &src, &dst, 1, row_stride, xt, xs, n_x, yt, ys, n_y, OH, OW);
+}
+
+// LDS span of resize_area_rows_u8: the widest 256-pixel output group's source bytes from a 16-byte
+// boundary to one past its last byte rounded up to 16
+static int area_span_bytes(const pc_area_tab* xt, const int32_t* xs, int OW) {
+  int m = 0;
+  for (int x0 = 0; x0 < OW; x0 += 256) {
+    const int xl = std::min(x0 + 255, OW - 1);
+    const int c0 = xt[xs[x0]].si, c1 = xt[xs[xl + 1] - 1].si;
+    m = std::max(m, ((c1 * 3 + 3 + 15) & ~15) - ((c0 * 3) & ~15));
+  }
+  return m;
+}
+
+extern "C" int pc_resize_area_batch(pc_ctx* c, const uint8_t* const* srcs, uint8_t* const* dsts, int n, int row_stride,
+                                    const pc_area_tab* xt, const int32_t* xs, int n_x, const pc_area_tab* yt,
+                                    const int32_t* ys, int n_y, int OH, int OW) {
+  if (!c || !srcs || !dsts || !xt || !xs || !yt || !ys || n < 0 || OH <= 0 || OW <= 0 || n_x <= 0 || n_y <= 0)
+    return fail(c, PC_ERR_ARG, "pc_resize_area_batch: bad arguments");
+  if (n == 0) return PC_OK;
+  bool aligned = row_stride % 16 == 0;
+  for (int i = 0; i < n; ++i) {
+    if (!srcs[i] || !dsts[i]) return fail(c, PC_ERR_ARG, "pc_resize_area_batch: null frame");
+    aligned = aligned && ((uintptr_t)srcs[i] & 15) == 0;
+  }
+  const int span = area_span_bytes(xt, xs, OW);
   void *dxt, *dxs, *dyt, *dys;
   int rc;
   if ((rc = stage_copy(c, xt, sizeof(pc_area_tab) * n_x, &dxt))) return rc;
   if ((rc = stage_copy(c, xs, sizeof(int32_t) * (OW + 1), &dxs))) return rc;
   if ((rc = stage_copy(c, yt, sizeof(pc_area_tab) * n_y, &dyt))) return rc;
   if ((rc = stage_copy(c, ys, sizeof(int32_t) * (OH + 1), &dys))) return rc;
-  HIPCHK(c, resize_area_launch(src, row_stride, (const AreaTab*)dxt, (const int*)dxs, (const AreaTab*)dyt,
-                               (const int*)dys, dst, OH, OW, c->stream));
+  if (aligned && 2 * span <= 65536) {
+    std::vector<const void*> jobs(2 * (size_t)n);
+    for (int i = 0; i < n; ++i) { jobs[2 * i] = srcs[i]; jobs[2 * i + 1] = dsts[i]; }
+    void* dj;
+    if ((rc = stage_copy(c, jobs.data(), sizeof(void*) * jobs.size(), &dj))) return rc;
+    HIPCHK(c, resize_area_rows_launch(dj, n, row_stride, (const AreaTab*)dxt, (const int*)dxs, (const AreaTab*)dyt,
+                                      (const int*)dys, OH, OW, span, c->stream));
+    return PC_OK;
+  }
+  for (int i = 0; i < n; ++i)   // unaligned frames: the per-pixel kernel
+    HIPCHK(c, resize_area_launch(srcs[i], row_stride, (const AreaTab*)dxt, (const int*)dxs, (const AreaTab*)dyt,
+                                 (const int*)dys, dsts[i], OH, OW, c->stream));
   return PC_OK;
 }
 

@@ -212,6 +212,33 @@ def dev_resize(ctx: GpuContext, img: _DevImage, key: str, dsize: Optional[Tuple[
     return _DevImage(buf.ptr, p["new_h"], p["new_w"], p["new_w"] * 3, buf)
 
 
+def dev_resize_batch(ctx: GpuContext, imgs: Sequence[_DevImage], keys: Sequence[str], dsize: Tuple[int, int],
+                     area: bool = True) -> List[_DevImage]:
+    """dev_resize of several images to one dsize: the frames that share a source geometry and take the
+    generic INTER_AREA path go through one pc_resize_area_batch launch (the pre-scan's speculative
+    chunk, gui_app.py:1505-1507 per sample); anything else one dev_resize each. Same bytes."""
+    out: List[Optional[_DevImage]] = [None] * len(imgs)
+    groups: Dict[Tuple[int, int, int], List[int]] = {}
+    for i, im in enumerate(imgs):
+        p = imageops.resize_plan(im.H, im.W, dsize, 0.0, 0.0, area)
+        if p["kind"] == "area":
+            groups.setdefault((im.H, im.W, im.stride), []).append(i)
+        else:
+            out[i] = dev_resize(ctx, im, keys[i], dsize, area=area)
+    for (H, W, stride), idx in groups.items():
+        p = imageops.resize_plan(H, W, dsize, 0.0, 0.0, area)
+        nw, nh = p["new_w"], p["new_h"]
+        (xt, xs), (yt, ys) = imageops.area_tables(W, nw, p["scale_x"]), imageops.area_tables(H, nh, p["scale_y"])
+        bufs = [ctx.scratch(keys[i], nw * nh * 3) for i in idx]
+        srcs = (C.c_void_p * len(idx))(*[imgs[i].ptr for i in idx])
+        dsts = (C.c_void_p * len(idx))(*[b.ptr for b in bufs])
+        check(ctx.lib.pc_resize_area_batch(ctx.handle, srcs, dsts, len(idx), stride, xt, xs, len(xt), yt, ys, len(yt),
+                                           nh, nw), ctx.handle, "resize_area_batch")
+        for i, b in zip(idx, bufs):
+            out[i] = _DevImage(b.ptr, nh, nw, nw * 3, b)
+    return out
+
+
 class FaceEmbedder(YoloFaceBranch):
     """Face detection (SCRFD, or the YOLOv8-face default) + ArcFace identity embedding on the MI355X.
     Returns list of dicts: {'bbox': np.int32[x1,y1,x2,y2], 'feat': np.float32[D], 'quality': float}."""

@@ -181,12 +181,13 @@ class PrescanRunner:
         f._prescan_rr_mode = "full" if active0 else "rr"
         f.set_prescan_hint(escalate=active0)
         todo = [j for j, skip in plan if not skip]
-        ims = []
+        srcs = []
         for j in todo:
             im = frame_at(samples[j])
             if not hasattr(im, "ptr"):
                 im = f._upload(np.ascontiguousarray(im), key=f"prescan_src{j % self.batch}")
-            ims.append(self._downscale(im, j - k))
+            srcs.append(im)
+        ims = self._downscale_many(srcs, [j - k for j in todo])
         state0 = f.policy_state()
         f.state_trace = []
         try:
@@ -248,6 +249,23 @@ class PrescanRunner:
             if st.fd9_streak >= grace:
                 return (st.fd9_streak % period) != 0, True
         return False, False
+
+    def _downscale_many(self, ims, ks):
+        """_downscale of a chunk's samples: the frames wider than prescan_max_width in one batched
+        INTER_AREA launch (face_embedder.dev_resize_batch), the same bytes as one resize each."""
+        from .face_embedder import dev_resize_batch
+        Wmax = int(self.cfg.prescan_max_width)
+        out = list(ims)
+        wide = [t for t, im in enumerate(ims) if im.W > Wmax]
+        by_dims = {}
+        for t in wide:
+            by_dims.setdefault((ims[t].H, ims[t].W), []).append(t)
+        for (H, W), ts in by_dims.items():
+            nh = int(round(H * (Wmax / float(W))))
+            res = dev_resize_batch(self.face._ctx, [ims[t] for t in ts], [f"prescan{ks[t]}" for t in ts], (Wmax, nh))
+            for t, r in zip(ts, res):
+                out[t] = r
+        return out
 
     def _downscale(self, im, k: int):
         """gui_app.py:1505-1507: INTER_AREA to prescan_max_width when wider."""

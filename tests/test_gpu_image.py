@@ -133,6 +133,30 @@ def test_resize_area_bit_exact(gpu_ctx, HW, OW):
     assert np.array_equal(got, ref)
 
 
+@pytest.mark.parametrize("offset", [0, 3])
+def test_resize_area_batch_bit_exact(gpu_ctx, offset):
+    """pc_resize_area_batch (the pre-scan chunk's downscale in one launch, face_embedder.dev_resize_batch):
+    16-byte aligned frames take the row-staged kernel (resize_area_rows_u8), a view 3 bytes into its
+    buffer the per-pixel one; every frame equals the oracle's INTER_AREA."""
+    from person_capture_amd.face_embedder import _DevImage, dev_resize_batch
+    rng = np.random.default_rng(40 + offset)
+    H, W, OW = 2160, 3840, 416
+    OH = int(round(H * OW / W))
+    frames = [_frame(rng, H, W) for _ in range(3)]
+    bufs = [gpu_ctx.alloc(f.nbytes + 64) for f in frames]
+    ims = []
+    for f, b in zip(frames, bufs):
+        host = np.zeros(f.nbytes + 64, np.uint8)
+        host[offset:offset + f.nbytes] = f.reshape(-1)
+        gpu_ctx.upload(host, b)
+        ims.append(_DevImage(b.ptr + offset, H, W, W * 3))
+    outs = dev_resize_batch(gpu_ctx, ims, [f"t_area_batch{i}" for i in range(3)], (OW, OH))
+    for f, o in zip(frames, outs):
+        assert (o.H, o.W) == (OH, OW)
+        got = gpu_ctx.download(o.ptr, (OH, OW, 3), np.uint8)
+        assert np.array_equal(got, cv_ops.resize_area(f, OW, OH))
+
+
 # (H, W, dsize, fx, area): chip resize fallbacks (face_embedder.py:2458-2460, 1579-1582) with
 # mixed axes (one down, one up -> area-mode linear), exact 2x/3x (resizeAreaFast), same size
 # (copy), pure up/down; TTA rescales by fx (:2264); the pre-scan downscale (gui_app.py:1505-1507)
