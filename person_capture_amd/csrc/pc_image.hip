@@ -428,18 +428,39 @@ __global__ __launch_bounds__(256) void resize_area_rows_u8(const AreaJob* __rest
   };
   const bool live = dx < OW;
   const int i0 = live ? xtab_start[dx] : 0, i1 = live ? xtab_start[dx + 1] : 0;
+  // the pixel's x-window in registers (<= MAXT taps: scale < MAXT - 1; wider windows re-read the table)
+  constexpr int MAXT = 16;
+  const int nt = i1 - i0;
+  int xo[MAXT];
+  float xa[MAXT];
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t) {
+    const AreaTab tx = t < nt ? xtab[i0 + t] : AreaTab{0, 0, 0.f};
+    xo[t] = tx.si * 3 - b0;
+    xa[t] = tx.alpha;
+  }
   float acc[3] = {0.f, 0.f, 0.f};
   copy_row(j0, 0);
   for (int j = j0; j < j1; ++j) {
     __syncthreads();   // row j is in its buffer; every thread is done with the other one
     if (j + 1 < j1) copy_row(j + 1, (j + 1 - j0) & 1);
-    const uint8_t* row = rowbuf + ((j - j0) & 1) * span_bytes - b0;
+    const uint8_t* row = rowbuf + ((j - j0) & 1) * span_bytes;
     const AreaTab ty = ytab[j];
     float rs[3] = {0.f, 0.f, 0.f};
-    for (int i = i0; i < i1; ++i) {
-      const AreaTab tx = xtab[i];
+    if (nt <= MAXT) {
 #pragma unroll
-      for (int c = 0; c < 3; ++c) rs[c] += (float)row[tx.si * 3 + c] * tx.alpha;
+      for (int t = 0; t < MAXT; ++t) {
+        if (t < nt) {
+#pragma unroll
+          for (int c = 0; c < 3; ++c) rs[c] += (float)row[xo[t] + c] * xa[t];
+        }
+      }
+    } else {
+      for (int i = i0; i < i1; ++i) {
+        const AreaTab tx = xtab[i];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) rs[c] += (float)row[tx.si * 3 - b0 + c] * tx.alpha;
+      }
     }
 #pragma unroll
     for (int c = 0; c < 3; ++c) acc[c] += rs[c] * ty.alpha;

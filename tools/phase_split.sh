@@ -3,7 +3,7 @@
 # epilogue, 8 prologue only, 16 no output stores), single-conv probe, HIP events. usage (GPU box):
 #   bash tools/phase_split.sh <probe shape> <VAR> <valA> <valB> [dbg values]   e.g. s3_3x3_256 PC_CONV_HXI 1 0
 set -o pipefail
-SHAPE=$1; VAR=$2; A=$3; B=$4; DBGS=${5:-"0 2 4 8 16"}
+SHAPE=$1; VAR=$2; A=$3; B=$4; DBGS=$(echo "${5:-0,2,4,8,16}" | tr "," " ")
 for v in "$A" "$B"; do
   for d in $DBGS; do
     echo "== $VAR=$v PC_CONV_DBG=$d"
