@@ -396,35 +396,51 @@ __global__ void resize_area_u8(const uint8_t* __restrict__ src, int row_stride,
 
 // The same arithmetic for a batch of equally sized frames (the pre-scan's 4K -> 416 downscale of a
 // speculative chunk, gui_app.py:1505-1507), with the source rows staged through the LDS: a workgroup
-// is 256 consecutive output pixels of one output row of one frame; per source row of the row's
-// y-window it copies the row's byte span (16-byte aligned vector loads, every byte once) into an LDS
-// buffer (two, alternating: the next row's copy is issued before the current row is summed), and
-// every thread sums its x-window from there - the per-pixel form issued ~300 byte loads per thread
+// is 256 consecutive output pixels of one output row of one frame; the source rows of the row's
+// y-window stream through a 4-slot LDS ring by LDS-DMA (each row's byte span from a 16-byte boundary,
+// three rows in flight while one is summed), and every thread sums its x-window from there - the per-pixel form issued ~300 byte loads per thread
 // straight from memory and ran one 4K frame per launch at 0.03 of HBM. Requires
 // 16-byte aligned sources and row strides (every source byte the loads touch is then inside the
 // rows); the per-pixel kernel serves the rest. Bit-identical to it: same products, same order.
 struct AreaJob { const uint8_t* src; uint8_t* dst; };
 
+// LDS ring of the row kernel: AREA_RING row buffers of AREA_ROWB bytes, AREA_RING - 1 rows in flight
+constexpr int AREA_RING = 4, AREA_ROWB = 8192, AREA_PPW = AREA_ROWB / 1024 / 4;   // pieces per wave and row
+
 __global__ __launch_bounds__(256) void resize_area_rows_u8(const AreaJob* __restrict__ jobs, int row_stride,
                                                            const AreaTab* __restrict__ xtab,
                                                            const int* __restrict__ xtab_start,
                                                            const AreaTab* __restrict__ ytab,
-                                                           const int* __restrict__ ytab_start, int OH, int OW,
-                                                           int span_bytes) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t rowbuf[];   // 2 x span_bytes
+                                                           const int* __restrict__ ytab_start, int OH, int OW) {
+  __shared__ __attribute__((aligned(16))) uint8_t ring[AREA_RING * AREA_ROWB];
   const AreaJob job = jobs[blockIdx.z];
   const int dy = blockIdx.y, x0 = blockIdx.x * 256;
   const int dx = x0 + threadIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int xl = min(x0 + 255, OW - 1);
-  // the workgroup's source byte span, from a 16-byte boundary
+  // the workgroup's source byte span, from a 16-byte boundary (<= AREA_ROWB: checked on the host)
   const int c0 = xtab[xtab_start[x0]].si, c1 = xtab[xtab_start[xl + 1] - 1].si;
   const int b0 = (c0 * 3) & ~15, b1 = (c1 * 3 + 3 + 15) & ~15;
-  const int nchunk = (b1 - b0) >> 4;
   const int j0 = ytab_start[dy], j1 = ytab_start[dy + 1];
-  auto copy_row = [&](int j, int buf) {
-    const uint4* srow = reinterpret_cast<const uint4*>(job.src + (long long)ytab[j].si * row_stride + b0);
-    uint4* drow = reinterpret_cast<uint4*>(rowbuf + buf * span_bytes);
-    for (int k = threadIdx.x; k < nchunk; k += 256) drow[k] = srow[k];
+  // LDS-DMA of source row j into ring slot: piece q = wave + 4 i covers LDS bytes q KiB + 16 lane; a lane
+  // past the span re-reads the span's first chunk (every address it touches is inside the row)
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(job.src), (short)0, (int)0xffffffff, 0x00020000);
+  unsigned lofs[AREA_PPW];
+#pragma unroll
+  for (int i = 0; i < AREA_PPW; ++i) {
+    const int byte = (wave + 4 * i) * 1024 + lane * 16;
+    lofs[i] = (unsigned)(b0 + (byte < b1 - b0 ? byte : 0));
+  }
+  auto issue = [&](int j, int slot) __attribute__((always_inline)) {
+    const unsigned rbase = (unsigned)ytab[j].si * (unsigned)row_stride;
+#pragma unroll
+    for (int i = 0; i < AREA_PPW; ++i) {
+      unsigned off = lofs[i];
+      asm volatile("" : "+v"(off));
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(ring + slot * AREA_ROWB + (wave + 4 * i) * 1024), 16,
+                                               off, rbase, 0, 0);
+    }
   };
   const bool live = dx < OW;
   const int i0 = live ? xtab_start[dx] : 0, i1 = live ? xtab_start[dx + 1] : 0;
@@ -439,32 +455,40 @@ __global__ __launch_bounds__(256) void resize_area_rows_u8(const AreaJob* __rest
     xo[t] = tx.si * 3 - b0;
     xa[t] = tx.alpha;
   }
+  // prologue: rows j0 .. j0 + RING - 2 in flight (past the window: row j0 again into its slot's
+  // successor, so every wave always has the same number of DMAs younger than the row it waits for)
+#pragma unroll
+  for (int r = 0; r < AREA_RING - 1; ++r) issue(j0 + r < j1 ? j0 + r : j0, r);
   float acc[3] = {0.f, 0.f, 0.f};
-  copy_row(j0, 0);
   for (int j = j0; j < j1; ++j) {
-    __syncthreads();   // row j is in its buffer; every thread is done with the other one
-    if (j + 1 < j1) copy_row(j + 1, (j + 1 - j0) & 1);
-    const uint8_t* row = rowbuf + ((j - j0) & 1) * span_bytes;
+    const int k = j - j0;
+    // row j landed: the youngest (RING - 2) rows' DMAs may still be in flight
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((AREA_RING - 2) * AREA_PPW) : "memory");
+    __syncthreads();   // every wave's pieces of row j; every thread done with row j - 1's slot
+    const int jn = j + AREA_RING - 1;
+    issue(jn < j1 ? jn : j0, (k + AREA_RING - 1) % AREA_RING);
+    const uint8_t* row = ring + (k % AREA_RING) * AREA_ROWB;
     const AreaTab ty = ytab[j];
-    float rs[3] = {0.f, 0.f, 0.f};
+    float rsum[3] = {0.f, 0.f, 0.f};
     if (nt <= MAXT) {
 #pragma unroll
       for (int t = 0; t < MAXT; ++t) {
         if (t < nt) {
 #pragma unroll
-          for (int c = 0; c < 3; ++c) rs[c] += (float)row[xo[t] + c] * xa[t];
+          for (int c = 0; c < 3; ++c) rsum[c] += (float)row[xo[t] + c] * xa[t];
         }
       }
     } else {
       for (int i = i0; i < i1; ++i) {
         const AreaTab tx = xtab[i];
 #pragma unroll
-        for (int c = 0; c < 3; ++c) rs[c] += (float)row[tx.si * 3 - b0 + c] * tx.alpha;
+        for (int c = 0; c < 3; ++c) rsum[c] += (float)row[tx.si * 3 - b0 + c] * tx.alpha;
       }
     }
 #pragma unroll
-    for (int c = 0; c < 3; ++c) acc[c] += rs[c] * ty.alpha;
+    for (int c = 0; c < 3; ++c) acc[c] += rsum[c] * ty.alpha;
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the dummy tail DMAs, before the workgroup's LDS goes)
   if (!live) return;
   uint8_t* o = job.dst + ((long long)dy * OW + dx) * 3;
 #pragma unroll
@@ -551,9 +575,9 @@ hipError_t rotate_pad_launch(const uint8_t* src, int H, int W, int row_stride, i
 hipError_t resize_area_rows_launch(const void* jobs, int n, int row_stride, const AreaTab* xtab, const int* xstart,
                                   const AreaTab* ytab, const int* ystart, int OH, int OW, int span_bytes,
                                   hipStream_t s) {
-  if (n <= 0 || span_bytes <= 0 || span_bytes % 16 || 2 * span_bytes > 65536) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(resize_area_rows_u8, dim3((OW + 255) / 256, OH, n), dim3(256), 2 * span_bytes, s,
-                     (const AreaJob*)jobs, row_stride, xtab, xstart, ytab, ystart, OH, OW, span_bytes);
+  if (n <= 0 || span_bytes <= 0 || span_bytes > AREA_ROWB) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(resize_area_rows_u8, dim3((OW + 255) / 256, OH, n), dim3(256), 0, s, (const AreaJob*)jobs,
+                     row_stride, xtab, xstart, ytab, ystart, OH, OW);
   return hipGetLastError();
 }
 
