@@ -887,8 +887,9 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
     }
   }
   // f16x3 64 -> 64 channel 3x3 layers on the halo-staged split kernel (pc_conv_hx.hip: 160x160x64
-  // b64 524 vs 632 us on conv_fast's fused tile), every plan alike (the choice does not depend
-  // on the batch). PC_CONV_HX=0 disables; the tuning overrides of the other kernels too.
+  // b64 524 vs 632 us on conv_fast's fused tile) where its grid fills the CUs; it accumulates in the
+  // fused tiles' order (round 6), so plan classes choose freely. PC_CONV_HX=0 disables; the tuning
+  // overrides of the other kernels too.
   pl.hx = 0;
   if (!(getenv("PC_CONV_HX") && atoi(getenv("PC_CONV_HX")) == 0) && !getenv("PC_CONV_FAST") &&
       !getenv("PC_CONV_CFG") && !getenv("PC_CONV_HALO") && !getenv("PC_CONV_T2D") && !getenv("PC_T2D_SPLIT64") &&
@@ -897,7 +898,10 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
     if (X.split && !X.c8 && !Y.c8 && X.C == 128 && X.cs == 128 && Y.split && Y.C == 128 && npad == 64 && w[4] == 3 && w[5] == 3 &&
         w[6] == 1 && w[7] == 1 && X.H == Y.H && X.W == Y.W && w[15] == 9 * 192 &&
         !(w[21] >= 0 && (w[22] == RES_UP2 || !n->tens[w[21]].split || n->tens[w[21]].c8)) &&
-        (double)X.H * X.W * n->max_batch * X.cs * esz + kZeroTail < 4294967296.0) {
+        (double)X.H * X.W * n->max_batch * X.cs * esz + kZeroTail < 4294967296.0 &&
+        plan_batch * ((Y.H + 11) / 12) * ((Y.W + 15) / 16) >= 256) {
+      // (its 16x12 blocks at two per CU; a grid of fewer blocks - a per-frame extract()'s 40x40 maps -
+      // keeps the fused tiles: the same accumulation order, so the classes stay bit-identical)
       pl.hx = 1;
       pl.fast = pl.halo = pl.t2d = -1;
       pl.sx = 0;
@@ -909,7 +913,10 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
         w[5] == 3 && w[6] == 1 && w[7] == 1 && X.H == Y.H && X.W == Y.W && w[15] == 9 * 288 &&
         !(w[21] >= 0 && (w[22] == RES_UP2 || !n->tens[w[21]].split || n->tens[w[21]].c8)) &&
         (double)X.H * X.W * n->max_batch * X.cs * esz + kZeroTail < 4294967296.0 &&
+        plan_batch * ((Y.H + 19) / 20) * ((Y.W + 15) / 16) >= 128 &&
         !(getenv("PC_CONV_HXG") && atoi(getenv("PC_CONV_HXG")) == 0)) {
+      // (one 16x20 block per CU; smaller grids - a single frame's 80x80 map is 20 blocks - keep the
+      // fused tiles, bit-identical: conv_hxg walks K and the MFMA passes in their order)
       pl.hx = 2;
       pl.fast = pl.halo = pl.t2d = -1;
       pl.sx = 0;

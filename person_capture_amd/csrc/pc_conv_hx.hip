@@ -10,11 +10,12 @@
 // fragments come from the conv's fragment-ordered weight copy (pc_api.cpp pack_wfrag) straight into
 // registers, one k-step ahead: the K loop has no barrier, and two workgroups share a CU (round 4's
 // form staged 16x16 blocks and a 3-tap weight ring through the LDS, 131 KB: one workgroup per CU).
-// Per k-step and fragment the MFMAs are W_hi*x_hi, W_lo*x_hi, W_hi*x_lo, k-steps in (tap row, tap
-// column, 32-channel block) order. That is NOT conv_fast SX's accumulation order (channel-group-major
-// K, W_lo*x_hi first, round 5), so PC_CONV_HX=0 changes these layers' outputs in the last bits (both
-// f32 class); what the code guarantees is that every plan class of a net runs the same kernel on them
-// (plan_conv picks this one independently of the batch), so small and large batches stay bit-identical.
+// Per k-step and fragment the MFMAs are W_lo*x_hi, W_hi*x_hi, W_hi*x_lo, k-steps in (tap row, tap
+// column, 32-channel block) order: for 64 input channels (one channel group of 64) that is conv_fast
+// SX's accumulation order, pass order included (round 6; round 5 issued W_hi*x_hi first), and the
+// epilogue arithmetic is conv_epilogue_lds<SPLIT>'s - so a plan class may run these layers here or on
+// the fused tiles and small and large batches stay bit-identical (pc_api.cpp plan_conv takes this
+// kernel where its grid fills the CUs; tests/test_gpu_plan_classes.py).
 #include "pc_conv_common.h"
 
 namespace pc {
@@ -103,12 +104,12 @@ __global__ __launch_bounds__(256, 2) void conv_hx64(ConvParams p, int nby, int n
     for (int a = 0; a < TC; ++a)
 #pragma unroll
       for (int t = 0; t < TP; ++t)
-        acc[a][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wbh[q][a], bh[t], acc[a][t], 0, 0, 0);
+        acc[a][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wbl[q][a], bh[t], acc[a][t], 0, 0, 0);
 #pragma unroll
     for (int a = 0; a < TC; ++a)
 #pragma unroll
       for (int t = 0; t < TP; ++t)
-        acc[a][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wbl[q][a], bh[t], acc[a][t], 0, 0, 0);
+        acc[a][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wbh[q][a], bh[t], acc[a][t], 0, 0, 0);
 #pragma unroll
     for (int a = 0; a < TC; ++a)
 #pragma unroll
@@ -213,9 +214,10 @@ __global__ __launch_bounds__(256, 2) void conv_hx64(ConvParams p, int nby, int n
 //    group g + 1's LDS-DMA is issued right after the barrier that opens group g, so it lands while
 //    group g's 9 taps run; one barrier per group, none inside it;
 //  * K walks (32-channel group, tap row, tap column) - the packed fragment copy's order for channel
-//    counts that are not a multiple of 64 (pc_api.cpp pack_wfrag, gt 1) - with the weight fragments of
-//    the next k-step loaded into registers under the current one; per k-step and fragment the MFMAs
-//    are conv_hx64's: W_hi*x_hi, W_lo*x_hi, W_hi*x_lo;
+//    counts that are not a multiple of 64 (pc_api.cpp pack_wfrag, gt 1), which is conv_fast SX's K order
+//    there - with the weight fragments of the next k-step loaded into registers under the current one;
+//    per k-step and fragment the MFMAs are SX's: W_lo*x_hi, W_hi*x_hi, W_hi*x_lo (so a plan class may
+//    take the fused tiles instead: same accumulators);
 //  * epilogue: conv_hx64's (f32 image over the LDS, 16-byte hi and lo stores per pixel and 8 channels).
 template <int CIN, int COUT, int TP>
 __global__ __launch_bounds__(256, 1) void conv_hxg(ConvParams p, int nby, int nbx) {
@@ -316,12 +318,12 @@ __global__ __launch_bounds__(256, 1) void conv_hxg(ConvParams p, int nby, int nb
       for (int a = 0; a < TC; ++a)
 #pragma unroll
         for (int t = 0; t < TP; ++t)
-          acc[a][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wbh[q][a], bh[t], acc[a][t], 0, 0, 0);
+          acc[a][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wbl[q][a], bh[t], acc[a][t], 0, 0, 0);
 #pragma unroll
       for (int a = 0; a < TC; ++a)
 #pragma unroll
         for (int t = 0; t < TP; ++t)
-          acc[a][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wbl[q][a], bh[t], acc[a][t], 0, 0, 0);
+          acc[a][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wbh[q][a], bh[t], acc[a][t], 0, 0, 0);
 #pragma unroll
       for (int a = 0; a < TC; ++a)
 #pragma unroll

@@ -132,16 +132,17 @@ def test_split_detections_match_f32(gpu_ctx, s10g, seed):
 
 @pytest.mark.parametrize("hx", ["default", "off"])
 def test_split_hx_ran(gpu_ctx, s10g, hx, monkeypatch):
-    """The planner sends the f16x3 64 -> 64 channel 3x3 layers to the halo-staged kernel (profile
-    code 500): at D=640 the 160x160, 80x80 and 40x40 ones (40 is not a multiple of its 16-pixel
-    blocks: partial blocks), and never under PC_CONV_HX=0."""
+    """The planner sends the f16x3 64 -> 64 channel 3x3 layers of a C3 detection chunk (32 frames) to
+    the halo-staged kernel (profile code 500): at D=640 the 160x160, 80x80 and 40x40 ones (40 is not a
+    multiple of its 16-pixel blocks: partial blocks), and never under PC_CONV_HX=0. (A single frame's
+    grids are too small for it: its plan keeps the fused tiles, bit-identically - test_gpu_plan_classes.)"""
     if hx == "off":
         monkeypatch.setenv("PC_CONV_HX", "0")
-    eng = ScrfdEngine(gpu_ctx, s10g, "10g", D=640, precision=PC_PREC_F16X3, max_batch=1)
+    eng = ScrfdEngine(gpu_ctx, s10g, "10g", D=640, precision=PC_PREC_F16X3, max_batch=32)
     f = _frame(7)
     d = gpu_ctx.upload(f)
     eng.net.profile(True)
-    eng.detect_frames([(d.ptr, f.shape[0], f.shape[1], f.strides[0])], thresh=0.5)
+    eng.detect_frames([(d.ptr, f.shape[0], f.shape[1], f.strides[0])] * 32, thresh=0.5)
     recs = eng.net.profile_ops()
     eng.net.profile(False)
     hx_ops = [int(r[0]) for r in recs if int(r[4]) == 500]
@@ -162,15 +163,17 @@ def test_split_net_parity_d640_hxg(gpu_ctx, s10g, monkeypatch):
 
 @pytest.mark.parametrize("hxg", ["default", "off"])
 def test_split_hxg_ran(gpu_ctx, s10g, hxg, monkeypatch):
-    """The planner sends the f16x3 96 -> 96 channel 3x3 layers to conv_hxg (profile code 501) at every
-    map size of D=640, and never under PC_CONV_HXG=0 (conv_hx64 keeps the 64-channel ones)."""
+    """The planner sends the f16x3 96 -> 96 channel 3x3 layers of a C3 detection chunk (32 frames) to
+    conv_hxg (profile code 501) where its grid fills the CUs - the 80x80 and 40x40 maps of D=640 - and
+    never under PC_CONV_HXG=0 (conv_hx64 keeps the 64-channel ones); a single frame keeps the fused
+    tiles on all of them."""
     if hxg == "off":
         monkeypatch.setenv("PC_CONV_HXG", "0")
-    eng = ScrfdEngine(gpu_ctx, s10g, "10g", D=640, precision=PC_PREC_F16X3, max_batch=1)
+    eng = ScrfdEngine(gpu_ctx, s10g, "10g", D=640, precision=PC_PREC_F16X3, max_batch=32)
     f = _frame(9)
     d = gpu_ctx.upload(f)
     eng.net.profile(True)
-    eng.detect_frames([(d.ptr, f.shape[0], f.shape[1], f.strides[0])], thresh=0.5)
+    eng.detect_frames([(d.ptr, f.shape[0], f.shape[1], f.strides[0])] * 32, thresh=0.5)
     recs = eng.net.profile_ops()
     eng.net.profile(False)
     codes = [int(r[4]) for r in recs]
@@ -180,4 +183,8 @@ def test_split_hxg_ran(gpu_ctx, s10g, hxg, monkeypatch):
         assert not hxg_ops
         return
     sizes = {eng.program.tensors[eng.program.ops[o][1]][1] for o in hxg_ops}
-    assert {80, 40, 20} <= sizes, sorted(sizes)
+    assert {80, 40} <= sizes, sorted(sizes)
+    eng.net.profile(True)
+    eng.detect_frames([(d.ptr, f.shape[0], f.shape[1], f.strides[0])], thresh=0.5)
+    assert not any(int(r[4]) in (500, 501) for r in eng.net.profile_ops())   # one frame: the fused tiles
+    eng.net.profile(False)
