@@ -930,6 +930,18 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
     // faces (256 rows = one round of one-image workgroups; at 383 rows, 1.5 rounds, 876: the quantum
     // follows, face_embedder.py), profiles/r06e_*
     const int hxi_mask = getenv("PC_CONV_HXI") ? atoi(getenv("PC_CONV_HXI")) : 3;
+    // plain f16 nets (BASELINE C2's fp16 ArcFace): bits 2 / 3 = 14x14x256 / 28x28x128 (tap-major K: the
+    // plain tiles' and the resident chain's order, bit-identical)
+    if (!X.split && !X.c8 && !X.is_f32 && !Y.split && !Y.is_f32 && !Y.c8 && X.cs == X.C && Y.cs == Y.C && Y.C == X.C &&
+        npad == X.C && w[4] == 3 && w[5] == 3 && w[6] == 1 && w[7] == 1 && X.W == X.H && Y.H == X.H && Y.W == X.W &&
+        w[15] == 9 * X.C && !(w[21] >= 0 && (w[22] == RES_UP2 || n->tens[w[21]].split || n->tens[w[21]].is_f32)) &&
+        (((hxi_mask & 4) && X.C == 256 && X.H == 14 && plan_batch >= 192) ||
+         ((hxi_mask & 8) && X.C == 128 && X.H == 28 && plan_batch >= 64)) &&
+        (double)X.H * X.W * n->max_batch * X.cs * esz + kZeroTail < 4294967296.0) {
+      pl.hx = X.C == 256 ? 3 : 4;
+      pl.fast = pl.halo = pl.t2d = -1;
+      pl.sx = 0;
+    }
     const int hc = X.C / 2;
     const bool hxi_shape = ((hxi_mask & 1) && hc == 256 && X.H == 14 && plan_batch >= 192) ||
                            ((hxi_mask & 2) && hc == 128 && X.H == 28 && plan_batch >= 64);
@@ -1192,6 +1204,26 @@ static int pack_wfrag(pc_net* n, const NetOp& op, const float* wf, void** out) {
   const int* w = op.w;
   const int npad = w[14];
   const long long ktot = w[15];
+  if (w[2] == 1 && !n->tens[w[3]].split) {
+    // plain f16 (conv_hxi's plain form): K tiles of 32 channels tap-major (tap row, tap column,
+    // 32-channel block: conv_fast's plain K order), per tile npad / 16 row blocks of W fragments
+    const NetTensor& X = n->tens[w[3]];
+    const int C = X.C, KH = w[4], KW = w[5];
+    if (C % 32 || (long long)KH * KW * C != ktot || npad % 16) return fail(n->ctx, PC_ERR_FORMAT, "wfrag: plain K layout");
+    const long long nkt = (long long)KH * KW * (C / 32), tile_elems = (long long)(npad / 16) * 512;
+    std::vector<_Float16> h((size_t)(nkt * tile_elems));
+    for (long long kt = 0; kt < nkt; ++kt)
+      for (int rb = 0; rb < npad / 16; ++rb)
+        for (int l = 0; l < 64; ++l)
+          for (int j = 0; j < 8; ++j) {
+            const long long row = rb * 16 + (l & 15), k = kt * 32 + (l >> 4) * 8 + j;
+            h[(size_t)(kt * tile_elems + ((long long)rb * 64 + l) * 8 + j)] = (_Float16)wf[row * ktot + k];
+          }
+    if (hipMalloc(out, h.size() * 2) != hipSuccess ||
+        hipMemcpy(*out, h.data(), h.size() * 2, hipMemcpyHostToDevice) != hipSuccess)
+      return fail(n->ctx, PC_ERR_HIP, "wfrag upload failed");
+    return PC_OK;
+  }
   long long nkt = 0, k0 = 0;
   for (int sg = 0; sg < w[2]; ++sg) {
     const NetTensor& X = n->tens[w[3 + 5 * sg]];

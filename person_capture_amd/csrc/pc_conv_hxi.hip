@@ -31,37 +31,46 @@
 
 namespace pc {
 
-constexpr int HXI_SB = 256;   // halo slot: 64 hi + 64 lo f16 channels
-
-template <int HW, int PITCH, int ROWS, int CIN, int COUT, int WCH, int WPX>
+// SPLIT (f16x3): a halo slot holds one 64-channel group's hi and lo halves (256 bytes), staged group by
+// group in a 2-stage ring; K = (group, tap, 32-channel block), 3 MFMA passes per k-step (the fused
+// tiles' order). Plain f16 (the BASELINE C2 fp16 net): a slot holds every input channel (CIN * 2 bytes),
+// staged once; K = (tap, 32-channel block), tap-major like conv_fast's plain tiles and the resident
+// chain, one MFMA per fragment pair - so it is bit-identical to them as well.
+template <int HW, int PITCH, int ROWS, int CIN, int COUT, int WCH, int WPX, bool SPLIT, int OCC>
 struct HxiGeom {
   static constexpr int NW = WCH * WPX, NT = 64 * NW;
   static constexpr int NF = ROWS * PITCH / 16;              // pixel fragments per workgroup
   static constexpr int TP = NF / WPX, TC = COUT / WCH / 16;
-  static constexpr int TPG = TP > 7 ? (TP % 2 == 0 ? TP / 2 : TP) : TP;   // fragments per read group
-  static constexpr int NG = CIN / 64, NKS = NG * 18;
+  // fragments per read group (two workgroups per CU: one at a time, their 4 waves per SIMD hide the reads)
+  static constexpr int TPG = OCC > 1 ? 1 : (TP > 7 ? (TP % 2 == 0 ? TP / 2 : TP) : TP);
+  static constexpr int SB = SPLIT ? 256 : CIN * 2;           // halo slot bytes
+  static constexpr int NB = SPLIT ? 2 : CIN / 32;            // 32-channel blocks per staged group
+  static constexpr int NG = SPLIT ? CIN / 64 : 1, KPG = 9 * NB, NKS = NG * KPG;
+  static constexpr int NSTAGE = NG > 1 ? 2 : 1;
   static constexpr int SLOTS = (ROWS + 2) * PITCH + 2;       // + the 2 slots discarded columns reach
-  static constexpr int PIECES = (SLOTS * HXI_SB + 1023) / 1024;
+  static constexpr int PIECES = (SLOTS * SB + 1023) / 1024;
   static constexpr int STAGE = PIECES * 1024;
   static constexpr int NPIX = ROWS * HW;
-  static constexpr int PC = COUT * NPIX * 4 <= 131072 ? COUT : COUT / 2;   // channels per epilogue pass
+  static constexpr int PC = COUT * NPIX * 4 <= 131072 / OCC ? COUT : COUT / 2;   // channels per epilogue pass
   static constexpr int NPASS = COUT / PC;
   static constexpr int RS = PC + 4;
   static constexpr int EPI = NPIX * RS * 4;
-  static constexpr int SMEM = 2 * STAGE > EPI ? 2 * STAGE : EPI;
+  static constexpr int SMEM = NSTAGE * STAGE > EPI ? NSTAGE * STAGE : EPI;
+  static constexpr int WTILE = SPLIT ? 2048 : 1024;          // packed weight bytes per K tile and 16-row block
   static constexpr int CGN = PC / 8;                         // 8-channel items per pixel and pass
   static constexpr int IT = (NPIX + NT / CGN - 1) / (NT / CGN);   // items (pixels) per thread and pass
   static_assert(PITCH % 16 == 0 && PITCH >= HW + 2 && NF % WPX == 0 && TP % TPG == 0, "pixel fragments");
-  static_assert(COUT % (16 * WCH) == 0 && CIN % 64 == 0 && HW % ROWS == 0, "tiling");
+  static_assert(COUT % (16 * WCH) == 0 && CIN % 64 == 0 && HW % ROWS == 0 && SB % 256 == 0, "tiling");
   static_assert(SMEM <= 163840, "LDS");
   static_assert(NPASS == 1 || WCH % 2 == 0, "epilogue passes split the channel waves");
 };
 
-template <int HW, int PITCH, int ROWS, int CIN, int COUT, int WCH, int WPX>
-__global__ __launch_bounds__(512, 2) void conv_hxi(ConvParams p) {
-  using G = HxiGeom<HW, PITCH, ROWS, CIN, COUT, WCH, WPX>;
+template <int HW, int PITCH, int ROWS, int CIN, int COUT, int WCH, int WPX, bool SPLIT = true, int OCC = 1>
+__global__ __launch_bounds__(512, 2 * OCC) void conv_hxi(ConvParams p) {
+  using G = HxiGeom<HW, PITCH, ROWS, CIN, COUT, WCH, WPX, SPLIT, OCC>;
   constexpr int NW = G::NW, NT = G::NT, TC = G::TC, TP = G::TP, TPG = G::TPG, NG = G::NG, NKS = G::NKS;
-  constexpr int STAGE = G::STAGE, PIECES = G::PIECES;
+  constexpr int STAGE = G::STAGE, PIECES = G::PIECES, SB = G::SB, NB = G::NB, KPG = G::KPG;
+  static_assert(G::SMEM * OCC <= 163840, "LDS for OCC workgroups per CU");
   static_assert(NW == 8, "8 waves");
   __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
   const ConvSeg& S = p.seg[0];
@@ -79,41 +88,42 @@ __global__ __launch_bounds__(512, 2) void conv_hxi(ConvParams p) {
   const __amdgpu_buffer_rsrc_t xrs = rsrc(S.x);
   const __amdgpu_buffer_rsrc_t wrs = rsrc(p.wfrag);
 
-  // this wave's halo pieces i = wave + 8 j: LDS byte i * 1024 + lane * 16 = slot h = 4 i + lane / 16,
-  // chunk position q = lane % 16, holding source chunk c = q ^ ((h & 7) << 1): channels 8 (c & 7) .. of
-  // the group's hi (c < 8) or lo half of input pixel (r0 - 1 + h / PITCH, h % PITCH - 1); zeros outside
+  // this wave's halo pieces i = wave + 8 j: LDS byte i * 1024 + lane * 16 = slot h, chunk position q,
+  // holding source chunk c = q ^ ((h & 7) << 1) (the XOR touches the low 4 bits only): split: channels
+  // 8 (c & 7) .. of the group's hi (c < 8) or lo half; plain: channels 8 c .. - of input pixel
+  // (r0 - 1 + h / PITCH, h % PITCH - 1); zeros outside
   constexpr int PPW = (PIECES + NW - 1) / NW;
-  unsigned src[PPW];
-#pragma unroll
-  for (int j = 0; j < PPW; ++j) {
-    const int h = (wave + NW * j) * 4 + kg, q = fr;
-    const int c = q ^ ((h & 7) << 1);
-    const int iy = r0 - 1 + h / PITCH, ix = h % PITCH - 1;
-    const bool ok = h < (ROWS + 2) * PITCH && (unsigned)iy < (unsigned)HW && (unsigned)ix < (unsigned)HW;
-    src[j] = ok ? (unsigned)((n * HW + iy) * HW + ix) * (unsigned)(S.cs * 2) + (unsigned)(((c & 7) * 8 + (c >> 3) * CIN) * 2)
-                : S.zero_off + (unsigned)(q << 4);
-  }
+  // (offsets computed at each issue: kept in registers for all pieces they spilled the 256-register
+  // plain 14x14 form, 17 pieces per wave)
   auto stage = [&](int g, int st) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < PPW; ++j) {
       if (wave + NW * j < PIECES) {   // (wave-uniform)
-        unsigned off = src[j];
+        const int byte = (wave + NW * j) * 1024 + lane * 16;
+        const int h = byte / SB, q = (byte % SB) >> 4;
+        const int c = q ^ ((h & 7) << 1);
+        const int iy = r0 - 1 + h / PITCH, ix = h % PITCH - 1;
+        const bool ok = h < (ROWS + 2) * PITCH && (unsigned)iy < (unsigned)HW && (unsigned)ix < (unsigned)HW;
+        const int cb = SPLIT ? ((c & 7) * 8 + (c >> 3) * CIN) * 2 : c * 16;
+        unsigned off = ok ? (unsigned)((n * HW + iy) * HW + ix) * (unsigned)(S.cs * 2) + (unsigned)cb
+                          : S.zero_off + (unsigned)((q & 15) << 4);
         asm volatile("" : "+v"(off));
-        // the group's 64 channels ride in the scalar offset (128 bytes per group of each half)
+        // split: the group's 64 channels ride in the scalar offset (128 bytes per group of each half)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)(smem + st * STAGE + (wave + NW * j) * 1024), 16, off,
                                                  g * 128, 0, 0);
       }
     }
   };
-  // weight fragments of k-step s (packed K tile s: group s / 18, tap (s % 18) / 2, block s % 2): row
-  // blocks TC wch .. TC wch + TC - 1 of npad / 16, each [W_hi, W_lo] x 1 KiB
-  const int tile = (p.npad / 16) * 2048;
+  // weight fragments of k-step s (packed K tile s; split: group s / 18, tap (s % 18) / 2, block s % 2,
+  // plain: tap s / NB, block s % NB): row blocks TC wch .. TC wch + TC - 1 of npad / 16, each
+  // [W_hi, W_lo] (split) or W (plain) x 1 KiB
+  const int tile = (p.npad / 16) * G::WTILE;
   auto wload = [&](f16x8* wh, f16x8* wl, int s) __attribute__((always_inline)) {
 #pragma unroll
     for (int a = 0; a < TC; ++a) {
-      const int o = ((TC * wch + a) * 2) * 1024 + lane * 16;
+      const int o = (TC * wch + a) * G::WTILE + lane * 16;
       wh[a] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, o, s * tile, 0));
-      wl[a] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, o + 1024, s * tile, 0));
+      if constexpr (SPLIT) wl[a] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, o + 1024, s * tile, 0));
     }
   };
   f16x8 wbh[2][TC], wbl[2][TC];
@@ -128,9 +138,13 @@ __global__ __launch_bounds__(512, 2) void conv_hxi(ConvParams p) {
   if (p.dbg & 8) return;   // tuning only (PC_CONV_DBG): prologue only
 
   // per-lane LDS byte of (tap column dx, chunk kind) for slot fr + dx of halo row 0
+  // (recomputed at each k-step - the asm keeps the compiler from hoisting all (dx, block) offsets of
+  // the unrolled loop into registers at once: 24 of them in the plain 256-channel form)
   auto boff = [&](int dx, int chunk) __attribute__((always_inline)) {
     const int h = fr + dx;
-    return (unsigned)(h * HXI_SB + ((chunk ^ ((h & 7) << 1)) << 4));
+    unsigned v = (unsigned)(h * SB + ((chunk ^ ((h & 7) << 1)) << 4));
+    asm volatile("" : "+v"(v));
+    return v;
   };
   // halo slot of fragment t's first slot at tap (0, 0): fragment f = wpx * TP + t covers output row
   // f / (PITCH / 16), columns 16 (f % (PITCH / 16)) .. +16
@@ -140,23 +154,32 @@ __global__ __launch_bounds__(512, 2) void conv_hxi(ConvParams p) {
   };
   static_for<NG>([&](auto gc) __attribute__((always_inline)) {
     constexpr int g = decltype(gc)::value, st = g & 1;
-    // group g's halo: every VMEM op but the youngest 2 TC (the next k-step's weights) has landed
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * TC) : "memory");
+    // group g's halo: every VMEM op but the youngest (the next k-step's weights) has landed
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SPLIT ? 2 * TC : TC) : "memory");
     __syncthreads();   // every wave's pieces of group g; every wave done reading group g - 1's stage
     if constexpr (g + 1 < NG) stage(g + 1, st ^ 1);
     const char* base = smem + st * STAGE;
-    static_for<18>([&](auto kc) __attribute__((always_inline)) {
-      constexpr int k = decltype(kc)::value, tap = k / 2, blk = k % 2, s = g * 18 + k, q = s & 1;
+    static_for<KPG>([&](auto kc) __attribute__((always_inline)) {
+      constexpr int k = decltype(kc)::value, tap = k / NB, blk = k % NB, s = g * KPG + k, q = s & 1;
       constexpr int dy = tap / 3, dx = tap % 3;
       if constexpr (s + 1 < NKS) wload(wbh[q ^ 1], wbl[q ^ 1], s + 1);
-      const unsigned oh = boff(dx, blk * 4 + kg), ol = boff(dx, 8 + blk * 4 + kg);
+      const unsigned oh = boff(dx, blk * 4 + kg), ol = SPLIT ? boff(dx, 8 + blk * 4 + kg) : 0u;
       if (p.dbg & 2) return;   // tuning only: no MFMAs
       static_for<TP / TPG>([&](auto pc) __attribute__((always_inline)) {
         constexpr int t0 = decltype(pc)::value * TPG;
-        f16x8 bh[TPG], bl[TPG];
+        f16x8 bh[TPG], bl[SPLIT ? TPG : 1];
 #pragma unroll
         for (int t = 0; t < TPG; ++t)
-          bh[t] = *reinterpret_cast<const f16x8*>(base + oh + (fslot(t0 + t) + dy * PITCH) * HXI_SB);
+          bh[t] = *reinterpret_cast<const f16x8*>(base + oh + (fslot(t0 + t) + dy * PITCH) * SB);
+        if constexpr (!SPLIT) {   // plain f16: one MFMA per fragment pair
+#pragma unroll
+          for (int a = 0; a < TC; ++a)
+#pragma unroll
+            for (int t = 0; t < TPG; ++t)
+              acc[a][t0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wbh[q][a], bh[t], acc[a][t0 + t], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          return;
+        }
 #pragma unroll
         for (int a = 0; a < TC; ++a)
 #pragma unroll
@@ -165,7 +188,7 @@ __global__ __launch_bounds__(512, 2) void conv_hxi(ConvParams p) {
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int t = 0; t < TPG; ++t)
-          bl[t] = *reinterpret_cast<const f16x8*>(base + ol + (fslot(t0 + t) + dy * PITCH) * HXI_SB);
+          bl[t] = *reinterpret_cast<const f16x8*>(base + ol + (fslot(t0 + t) + dy * PITCH) * SB);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int a = 0; a < TC; ++a)
@@ -212,28 +235,39 @@ __global__ __launch_bounds__(512, 2) void conv_hxi(ConvParams p) {
     }
     // the per-pixel term of each of the thread's items, requested before anything waits on it: the
     // residual hi + lo (its f32 value), or the border-class bias of a folded pre-BN conv
-    float pre[IT][8];
-#pragma unroll
-    for (int k = 0; k < IT; ++k) {
+    // (two workgroups per CU: loaded at the item instead - the other workgroup covers the latency, and
+    // the registers are not there)
+    constexpr bool PREF = OCC == 1;
+    float pre[PREF ? IT : 1][8];
+    auto load_pre = [&](int k, float* dst) __attribute__((always_inline)) {
       const int pl = pl0 + PSTEP * k;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) pre[k][j] = 0.f;
-      if (pl >= NPIX) continue;
+      for (int j = 0; j < 8; ++j) dst[j] = 0.f;
+      if (pl >= NPIX) return;
       if (has_res) {
         const f16* rp = reinterpret_cast<const f16*>(p.res) + (pix0 + pl) * p.rcs + ch;
         const f16x8 rh = *reinterpret_cast<const f16x8*>(rp);
-        const f16x8 rl = *reinterpret_cast<const f16x8*>(rp + p.rsplit);
+        if constexpr (SPLIT) {
+          const f16x8 rl = *reinterpret_cast<const f16x8*>(rp + p.rsplit);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) pre[k][j] = (float)rh[j] + (float)rl[j];
+          for (int j = 0; j < 8; ++j) dst[j] = (float)rh[j] + (float)rl[j];
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) dst[j] = (float)rh[j];
+        }
       } else if (border) {
         const int oy = r0 + pl / HW, ox = pl % HW;
         const int rc = oy - 1 < 0 ? 0 : (oy + 1 >= HW ? 2 : 1);
         const int cc = ox - 1 < 0 ? 0 : (ox + 1 >= HW ? 2 : 1);
         const f32x4* bp = reinterpret_cast<const f32x4*>(p.bias + (rc * 3 + cc) * p.npad + ch);
         const f32x4 b0 = bp[0], b1 = bp[1];
-        pre[k][0] = b0[0]; pre[k][1] = b0[1]; pre[k][2] = b0[2]; pre[k][3] = b0[3];
-        pre[k][4] = b1[0]; pre[k][5] = b1[1]; pre[k][6] = b1[2]; pre[k][7] = b1[3];
+        dst[0] = b0[0]; dst[1] = b0[1]; dst[2] = b0[2]; dst[3] = b0[3];
+        dst[4] = b1[0]; dst[5] = b1[1]; dst[6] = b1[2]; dst[7] = b1[3];
       }
+    };
+    if constexpr (PREF) {
+#pragma unroll
+      for (int k = 0; k < IT; ++k) load_pre(k, pre[k]);
     }
     __syncthreads();   // the stages (pass 0) / the previous pass's image are no longer read
     if (NPASS == 1 || wch / (WCH / 2) == pass) {
@@ -255,6 +289,13 @@ __global__ __launch_bounds__(512, 2) void conv_hxi(ConvParams p) {
     for (int k = 0; k < IT; ++k) {
       const int pl = pl0 + PSTEP * k;
       if (pl >= NPIX) continue;
+      float pk[8];
+      if constexpr (PREF) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pk[j] = pre[k][j];
+      } else {
+        load_pre(k, pk);
+      }
       const long long pix = pix0 + pl;
       const f32x4 lo4 = *reinterpret_cast<const f32x4*>(im + pl * RS + cg * 8);
       const f32x4 hi4 = *reinterpret_cast<const f32x4*>(im + pl * RS + cg * 8 + 4);
@@ -270,12 +311,12 @@ __global__ __launch_bounds__(512, 2) void conv_hxi(ConvParams p) {
           for (int j = 0; j < 8; ++j) v[j] += bp[j];
         } else {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] += pre[k][j];
+          for (int j = 0; j < 8; ++j) v[j] += pk[j];
         }
       }
       if (has_res && !pre_act) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] += pre[k][j];
+        for (int j = 0; j < 8; ++j) v[j] += pk[j];
       }
       if (smooth) {
 #pragma unroll
@@ -286,7 +327,7 @@ __global__ __launch_bounds__(512, 2) void conv_hxi(ConvParams p) {
       }
       if (has_res && pre_act) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] += pre[k][j];
+        for (int j = 0; j < 8; ++j) v[j] += pk[j];
       }
       f16x8 yh, yl;
 #pragma unroll
@@ -298,35 +339,42 @@ __global__ __launch_bounds__(512, 2) void conv_hxi(ConvParams p) {
       if (p.dbg & 16) continue;   // tuning only: no stores
       f16* yp = reinterpret_cast<f16*>(p.y) + pix * p.ycs + ch;
       *reinterpret_cast<f16x8*>(yp) = yh;
-      *reinterpret_cast<f16x8*>(yp + p.ysplit) = yl;
+      if constexpr (SPLIT) *reinterpret_cast<f16x8*>(yp + p.ysplit) = yl;
     }
   }
 }
 
 // the instantiated shapes: IResNet's 14x14x256 (one image per workgroup, 8 x 1 waves of 32 channels x
-// 14 rows) and 28x28x128 (7 rows per workgroup, 4 x 2 waves of 32 channels x 7 fragments)
+// 14 rows) and 28x28x128 (7 rows per workgroup, 4 x 2 waves of 32 channels x 7 fragments); plain f16
+// 28x28x128 at two workgroups per CU (its halo stage is 73 KB)
 #define PC_HXI_14 14, 16, 14, 256, 256, 8, 1
 #define PC_HXI_28 28, 32, 7, 128, 128, 4, 2
 
-// can a conv run here: one split segment of C channels (X.C 2 C = [hi | lo], dense) on an HW x HW map
-// of an instantiated shape, C output channels written split (dense), 3x3 stride 1 pad 1, plain or
-// same-size split residual
+// can a conv run here: one segment of C channels (split: X.C 2 C = [hi | lo]; plain f16: X.C C), dense,
+// on an HW x HW map of an instantiated shape, C output channels written in the same form (dense), 3x3
+// stride 1 pad 1, plain or same-size residual in the same form
 int conv_hxi_ok(const ConvParams& p) {
   const ConvSeg& S = p.seg[0];
-  const int C = S.C / 2;
+  const bool split = p.ysplit != 0;
+  const int C = split ? S.C / 2 : S.C, w = split ? 2 : 1;
   const bool shape = (S.H == 14 && C == 256) || (S.H == 28 && C == 128);
-  return shape && p.nseg == 1 && S.cs == 2 * C && S.W == S.H && S.KH == 3 && S.KW == 3 && S.stride == 1 && S.pad == 1 &&
-         p.OH == S.H && p.OW == S.H && p.npad == C && p.ysplit == C && p.ycs == 2 * C && p.splitk == 1 && !p.out_f32 &&
-         !p.yc8 && !p.rc8 && p.ktot == 9 * 3 * C && p.res_mode != RES_UP2 &&
-         (p.res_mode == RES_NONE || (p.rsplit == C && p.rcs % 8 == 0)) && p.cwrite == C && p.wfrag != nullptr;
+  return shape && p.nseg == 1 && S.cs == w * C && S.W == S.H && S.KH == 3 && S.KW == 3 && S.stride == 1 &&
+         S.pad == 1 && p.OH == S.H && p.OW == S.H && p.npad == C && p.ycs == w * C && p.splitk == 1 && !p.out_f32 &&
+         !p.yc8 && !p.rc8 && p.ktot == 9 * (split ? 3 : 1) * C && p.res_mode != RES_UP2 &&
+         (p.res_mode == RES_NONE || (p.rsplit == (split ? C : 0) && p.rcs % 8 == 0)) && p.cwrite == C &&
+         p.wfrag != nullptr && (!split || p.ysplit == C);
 }
 
 hipError_t conv_hxi_launch(const ConvParams& p, hipStream_t s) {
   if (!conv_hxi_ok(p)) return hipErrorInvalidValue;
-  if (p.OH == 14)
-    hipLaunchKernelGGL((conv_hxi<PC_HXI_14>), dim3(p.N), dim3(512), 0, s, p);
-  else
-    hipLaunchKernelGGL((conv_hxi<PC_HXI_28>), dim3(p.N * 4), dim3(512), 0, s, p);
+  const bool split = p.ysplit != 0;
+  if (p.OH == 14) {
+    if (split) hipLaunchKernelGGL((conv_hxi<PC_HXI_14, true, 1>), dim3(p.N), dim3(512), 0, s, p);
+    else hipLaunchKernelGGL((conv_hxi<PC_HXI_14, false, 1>), dim3(p.N), dim3(512), 0, s, p);
+  } else {
+    if (split) hipLaunchKernelGGL((conv_hxi<PC_HXI_28, true, 1>), dim3(p.N * 4), dim3(512), 0, s, p);
+    else hipLaunchKernelGGL((conv_hxi<PC_HXI_28, false, 2>), dim3(p.N * 4), dim3(512), 0, s, p);
+  }
   return hipGetLastError();
 }
 

@@ -201,3 +201,35 @@ def test_arcface_f16x3_hxi_bit_identical(gpu_ctx, monkeypatch, batch):
     assert sum(1 for c in codes[0] if c == 502) == 58 and sum(1 for c in codes[0] if c == 503) == 24, codes[0]
     assert 502 not in codes[1] and 503 not in codes[1]
     assert np.array_equal(outs[0].view(np.uint8), outs[1].view(np.uint8))
+
+
+def test_arcface_f16_hxi_bit_identical(gpu_ctx, monkeypatch):
+    """The plain f16 form of conv_hxi (BASELINE C2's fp16 net: the halo holds every input channel, K walks
+    taps then 32-channel blocks - the plain tiles' and the resident chain's order) on the 14x14x256 and
+    28x28x128 layers (PC_CONV_HXI bits 2 / 3, chains off) gives the default plan's bits (resident chains
+    on the 14x14 stage, conv_fast tiles on 28x28)."""
+    from person_capture_amd.runtime import Net
+    P = models.compile_iresnet(models.synth_iresnet(100, seed=10), 100, split=False)
+    x = np.zeros((256, 112, 112, 4), np.float16)
+    x[..., :3] = np.random.default_rng(11).uniform(-1, 1, (256, 112, 112, 3))
+    d = gpu_ctx.upload(x)
+    outs, codes = [], []
+    try:
+        for env in ({"PC_CONV_HXI": "12", "PC_CHAIN_MIN": "100000"}, {"PC_CONV_HXI": "0"}):
+            for k, v in env.items():
+                monkeypatch.setenv(k, v)
+            net = Net(gpu_ctx, P.serialize(), PC_PREC_F16, max_batch=256)
+            try:
+                net.profile(True)
+                net.run(d.ptr, 256)
+                codes.append([int(r[4]) for r in net.profile_ops()])
+                net.profile(False)
+                outs.append(net.read_output(0, 256).copy())
+            finally:
+                net.close()
+            monkeypatch.delenv("PC_CHAIN_MIN", raising=False)
+    finally:
+        d.free()
+    assert sum(1 for c in codes[0] if c == 502) == 58 and sum(1 for c in codes[0] if c == 503) == 24, codes[0]
+    assert 300 in codes[1] and 502 not in codes[1]   # (300: a resident chain launch)
+    assert np.array_equal(outs[0].view(np.uint8), outs[1].view(np.uint8))
