@@ -924,14 +924,17 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
     // IResNet's 14x14x256 and 28x28x128 layers on the image-resident conv_hxi (pc_conv_hxi.hip) at
     // batches that give every CU a workgroup (plans for >= 192 / 64 images): bit-identical to the fused
     // tiles the smaller plan classes run (same K order, MFMA order and epilogue arithmetic).
-    // PC_CONV_HXI is a mask of the shapes it takes: bit 0 14x14x256, bit 1 28x28x128 (default 3). ArcFace-x3
+    // PC_CONV_HXI is a mask of the shapes it takes: bit 0 14x14x256, bit 1 28x28x128 (f16x3), bits 2 / 3 the
+    // same shapes of plain f16 nets (default 11: all but plain 14x14x256, which the resident chain beats). ArcFace-x3
     // b256 per layer, interleaved on one box: 28x28x128 187.5 vs 224.2 us on the 128x256 WG tile,
     // 14x14x256 149.3 vs 151.5 on the 256x224 one; C3 962 vs 930 frames/s with the embed quantum at 128
     // faces (256 rows = one round of one-image workgroups; at 383 rows, 1.5 rounds, 876: the quantum
     // follows, face_embedder.py), profiles/r06e_*
-    const int hxi_mask = getenv("PC_CONV_HXI") ? atoi(getenv("PC_CONV_HXI")) : 3;
+    const int hxi_mask = getenv("PC_CONV_HXI") ? atoi(getenv("PC_CONV_HXI")) : 11;
     // plain f16 nets (BASELINE C2's fp16 ArcFace): bits 2 / 3 = 14x14x256 / 28x28x128 (tap-major K: the
-    // plain tiles' and the resident chain's order, bit-identical)
+    // plain tiles' and the resident chain's order, bit-identical). f16 ArcFace b256, one box (r06m):
+    // 28x28x128 72.8 us/launch vs 94.0 on tile cfg 14 (C2 f16 7.64 vs 8.17 ms); 14x14x256 65 us x 58 =
+    // 3.77 ms vs 3.34 for the resident chain, so bit 2 stays opt-in (profiles/r06m_*)
     if (!X.split && !X.c8 && !X.is_f32 && !Y.split && !Y.is_f32 && !Y.c8 && X.cs == X.C && Y.cs == Y.C && Y.C == X.C &&
         npad == X.C && w[4] == 3 && w[5] == 3 && w[6] == 1 && w[7] == 1 && X.W == X.H && Y.H == X.H && Y.W == X.W &&
         w[15] == 9 * X.C && !(w[21] >= 0 && (w[22] == RES_UP2 || n->tens[w[21]].split || n->tens[w[21]].is_f32)) &&
