@@ -808,7 +808,9 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
       static_assert(sizeof(cost) / sizeof(cost[0]) == sizeof(occ) / sizeof(occ[0]), "tile tables");
       // fused split tiles: the 128x512 tile (8 waves of 64x128) ran ArcFace-x3's 28x28x128 at 464 us
       // against 233 for the 128x256 tile at the same estimate (profiles/r05n_sx_tile_sweep.txt)
-      auto sxcost = [&](int k) { return k == 9 ? 2.2 : cost[k]; };
+      // (and the 64x128 small tile: ArcFace-x3's 28x28x128 at 12 rows 28.0 us against 34.5 for the 32x256
+      // tile the plain factor picks, profiles/r06n_small_tile_sweep.txt)
+      auto sxcost = [&](int k) { return k == 9 ? 2.2 : k == 16 ? 1.4 : cost[k]; };
       int best = -1, best_rowb = rowb;
       double best_t = 0;
       bool rows256 = small && !n->f32 && !any_split && rowb == 128 && !getenv("PC_CONV_ROWB");

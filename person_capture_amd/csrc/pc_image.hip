@@ -265,15 +265,26 @@ __global__ void warp_affine_u8(const WarpDesc* __restrict__ descs, int gx, int n
 // quality = var(Laplacian(BGR2GRAY(chip), CV_64F)), ksize=1, BORDER_REFLECT_101.
 // The Laplacian values are small integers, so sum and sum of squares are exact in
 // int64; var = (S2 - S1^2/N)/N in f64 (numpy's two-pass var agrees to ~1e-15).
-// One 256-thread workgroup per chip.
+// One 1024-thread workgroup per chip: the chip's bytes come in as 16-byte loads (a per-frame
+// extract() has ~6 chips, so the old 256-thread byte-load loop ran ~40 us on 6 CUs), the gray
+// image and the Laplacian sums come from the LDS.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void face_quality(const uint8_t* __restrict__ chips, int side, double* __restrict__ out) {
+__global__ __launch_bounds__(1024) void face_quality(const uint8_t* __restrict__ chips, int side, double* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t raw[128 * 128 * 3];
   __shared__ uint8_t g[128 * 128];
-  __shared__ long long red[2][4];
+  __shared__ long long red[2][16];
   const uint8_t* c = chips + (long long)blockIdx.x * side * side * 3;
   const int n = side * side;
+  const int nb = n * 3;
+  if ((nb & 15) == 0 && ((uintptr_t)c & 15) == 0) {
+    for (int i = threadIdx.x; i < nb / 16; i += blockDim.x)
+      reinterpret_cast<uint4*>(raw)[i] = reinterpret_cast<const uint4*>(c)[i];
+  } else {
+    for (int i = threadIdx.x; i < nb; i += blockDim.x) raw[i] = c[i];
+  }
+  __syncthreads();
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    const int b = c[i * 3 + 0], gg = c[i * 3 + 1], r = c[i * 3 + 2];
+    const int b = raw[i * 3 + 0], gg = raw[i * 3 + 1], r = raw[i * 3 + 2];
     g[i] = (uint8_t)((b * 1868 + gg * 9617 + r * 4899 + (1 << 13)) >> 14);
   }
   __syncthreads();
@@ -295,7 +306,7 @@ __global__ __launch_bounds__(256) void face_quality(const uint8_t* __restrict__ 
   __syncthreads();
   if (threadIdx.x == 0) {
     long long t1 = 0, t2 = 0;
-    for (int k = 0; k < 4; ++k) { t1 += red[0][k]; t2 += red[1][k]; }
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) { t1 += red[0][k]; t2 += red[1][k]; }
     const double N = (double)n;
     const double mean = (double)t1 / N;
     // sum (l - mean)^2 = S2 - 2*mean*S1 + N*mean^2 = S2 - S1*mean (exact algebra)
@@ -551,7 +562,7 @@ hipError_t warp_launch(const WarpDesc* d_descs, int N, int max_pixels, hipStream
 
 hipError_t quality_launch(const uint8_t* chips, int N, int side, double* out, hipStream_t s) {
   if (side > 128) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(face_quality, dim3(N), dim3(256), 0, s, chips, side, out);
+  hipLaunchKernelGGL(face_quality, dim3(N), dim3(1024), 0, s, chips, side, out);
   return hipGetLastError();
 }
 

@@ -88,6 +88,20 @@ def test_face_quality(gpu_ctx):
     assert got[3] == 0.0
 
 
+@pytest.mark.parametrize("side", [5, 37, 128])
+def test_face_quality_other_sides(gpu_ctx, side):
+    """Chip sizes whose bytes are not whole 16-byte words (the byte-load path) and the largest side."""
+    rng = np.random.default_rng(side)
+    chips = rng.integers(0, 256, size=(3, side, side, 3), dtype=np.uint8)
+    d = gpu_ctx.upload(chips)
+    out = gpu_ctx.alloc(3 * 8)
+    check(gpu_ctx.lib.pc_face_quality(gpu_ctx.handle, C.c_void_p(d.ptr), 3, side, C.c_void_p(out.ptr)),
+          gpu_ctx.handle)
+    got = gpu_ctx.download(out.ptr, (3,), np.float64)
+    ref = np.array([cv_ops.face_quality(c) for c in chips])
+    assert np.allclose(got, ref, rtol=1e-12, atol=1e-9)
+
+
 def test_arcface_prep_and_flip(gpu_ctx):
     rng = np.random.default_rng(10)
     chips = rng.integers(0, 256, size=(3, 112, 112, 3), dtype=np.uint8)
