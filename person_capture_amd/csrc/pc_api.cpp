@@ -2134,7 +2134,8 @@ extern "C" int pc_resize_area_batch(pc_ctx* c, const uint8_t* const* srcs, uint8
   if ((rc = stage_copy(c, xs, sizeof(int32_t) * (OW + 1), &dxs))) return rc;
   if ((rc = stage_copy(c, yt, sizeof(pc_area_tab) * n_y, &dyt))) return rc;
   if ((rc = stage_copy(c, ys, sizeof(int32_t) * (OH + 1), &dys))) return rc;
-  if (aligned && span <= 8192) {   // (pc_image.hip AREA_ROWB: 4K -> 416 spans ~7.1 KB)
+  const bool direct = getenv("PC_AREA_DIRECT") && atoi(getenv("PC_AREA_DIRECT")) != 0;   // (A/B: per-pixel kernel)
+  if (aligned && span <= 8192 && !direct) {   // (pc_image.hip AREA_ROWB: 4K -> 416 spans ~7.1 KB)
     std::vector<const void*> jobs(2 * (size_t)n);
     for (int i = 0; i < n; ++i) { jobs[2 * i] = srcs[i]; jobs[2 * i + 1] = dsts[i]; }
     void* dj;

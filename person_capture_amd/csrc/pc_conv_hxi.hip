@@ -29,6 +29,8 @@
 //    28x28x128, profiles/r06f_hxi28_phase_split.txt).
 #include "pc_conv_common.h"
 
+#include <cstdlib>
+
 namespace pc {
 
 // SPLIT (f16x3): a halo slot holds one 64-channel group's hi and lo halves (256 bytes), staged group by
@@ -46,7 +48,9 @@ struct HxiGeom {
   static constexpr int SB = SPLIT ? 256 : CIN * 2;           // halo slot bytes
   static constexpr int NB = SPLIT ? 2 : CIN / 32;            // 32-channel blocks per staged group
   static constexpr int NG = SPLIT ? CIN / 64 : 1, KPG = 9 * NB, NKS = NG * KPG;
-  static constexpr int NSTAGE = NG > 1 ? 2 : 1;
+  // a 2-stage ring where the groups are several; at two workgroups per CU one stage (the other
+  // workgroup's MFMAs cover the exposed staging)
+  static constexpr int NSTAGE = NG > 1 && OCC == 1 ? 2 : 1;
   static constexpr int SLOTS = (ROWS + 2) * PITCH + 2;       // + the 2 slots discarded columns reach
   static constexpr int PIECES = (SLOTS * SB + 1023) / 1024;
   static constexpr int STAGE = PIECES * 1024;
@@ -153,11 +157,17 @@ __global__ __launch_bounds__(512, 2 * OCC) void conv_hxi(ConvParams p) {
     return (f / (PITCH / 16)) * PITCH + (f % (PITCH / 16)) * 16;
   };
   static_for<NG>([&](auto gc) __attribute__((always_inline)) {
-    constexpr int g = decltype(gc)::value, st = g & 1;
-    // group g's halo: every VMEM op but the youngest (the next k-step's weights) has landed
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SPLIT ? 2 * TC : TC) : "memory");
+    constexpr int g = decltype(gc)::value, st = G::NSTAGE == 2 ? (g & 1) : 0;
+    if constexpr (G::NSTAGE == 1 && g > 0) {   // one stage: group g replaces g - 1 once every wave is done
+      __syncthreads();
+      stage(g, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      // group g's halo: every VMEM op but the youngest (the next k-step's weights) has landed
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SPLIT ? 2 * TC : TC) : "memory");
+    }
     __syncthreads();   // every wave's pieces of group g; every wave done reading group g - 1's stage
-    if constexpr (g + 1 < NG) stage(g + 1, st ^ 1);
+    if constexpr (G::NSTAGE == 2 && g + 1 < NG) stage(g + 1, st ^ 1);
     const char* base = smem + st * STAGE;
     static_for<KPG>([&](auto kc) __attribute__((always_inline)) {
       constexpr int k = decltype(kc)::value, tap = k / NB, blk = k % NB, s = g * KPG + k, q = s & 1;
@@ -372,7 +382,11 @@ hipError_t conv_hxi_launch(const ConvParams& p, hipStream_t s) {
     if (split) hipLaunchKernelGGL((conv_hxi<PC_HXI_14, true, 1>), dim3(p.N), dim3(512), 0, s, p);
     else hipLaunchKernelGGL((conv_hxi<PC_HXI_14, false, 1>), dim3(p.N), dim3(512), 0, s, p);
   } else {
-    if (split) hipLaunchKernelGGL((conv_hxi<PC_HXI_28, true, 1>), dim3(p.N * 4), dim3(512), 0, s, p);
+    // (split: two workgroups per CU, one halo stage each, so one's epilogue runs under the other's MFMAs;
+    // PC_HXI28_OCC=1 the 2-stage form)
+    const bool occ1 = getenv("PC_HXI28_OCC") && atoi(getenv("PC_HXI28_OCC")) == 1;   // (per launch: A/B in one process)
+    if (split && occ1) hipLaunchKernelGGL((conv_hxi<PC_HXI_28, true, 1>), dim3(p.N * 4), dim3(512), 0, s, p);
+    else if (split) hipLaunchKernelGGL((conv_hxi<PC_HXI_28, true, 2>), dim3(p.N * 4), dim3(512), 0, s, p);
     else hipLaunchKernelGGL((conv_hxi<PC_HXI_28, false, 2>), dim3(p.N * 4), dim3(512), 0, s, p);
   }
   return hipGetLastError();

@@ -429,10 +429,15 @@ __global__ __launch_bounds__(256) void resize_area_rows_u8(const AreaJob* __rest
   const int dx = x0 + threadIdx.x;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int xl = min(x0 + 255, OW - 1);
+  // the pixel's x-window bounds, loaded with the span's (before the DMAs: a wait on a later load would
+  // wait for them too)
+  const bool live = dx < OW;
+  int i0 = live ? xtab_start[dx] : 0, i1 = live ? xtab_start[dx + 1] : 0;
   // the workgroup's source byte span, from a 16-byte boundary (<= AREA_ROWB: checked on the host)
   const int c0 = xtab[xtab_start[x0]].si, c1 = xtab[xtab_start[xl + 1] - 1].si;
   const int b0 = (c0 * 3) & ~15, b1 = (c1 * 3 + 3 + 15) & ~15;
   const int j0 = ytab_start[dy], j1 = ytab_start[dy + 1];
+  asm volatile("" : "+v"(i0), "+v"(i1));
   // LDS-DMA of source row j into ring slot: piece q = wave + 4 i covers LDS bytes q KiB + 16 lane; a lane
   // past the span re-reads the span's first chunk (every address it touches is inside the row)
   const __amdgpu_buffer_rsrc_t rs =
@@ -443,7 +448,8 @@ __global__ __launch_bounds__(256) void resize_area_rows_u8(const AreaJob* __rest
     const int byte = (wave + 4 * i) * 1024 + lane * 16;
     lofs[i] = (unsigned)(b0 + (byte < b1 - b0 ? byte : 0));
   }
-  auto issue = [&](int j, int slot) __attribute__((always_inline)) {
+  auto issue = [&](int j, auto slotc) __attribute__((always_inline)) {
+    constexpr int slot = decltype(slotc)::value;
     const unsigned rbase = (unsigned)ytab[j].si * (unsigned)row_stride;
 #pragma unroll
     for (int i = 0; i < AREA_PPW; ++i) {
@@ -453,32 +459,47 @@ __global__ __launch_bounds__(256) void resize_area_rows_u8(const AreaJob* __rest
                                                off, rbase, 0, 0);
     }
   };
-  const bool live = dx < OW;
-  const int i0 = live ? xtab_start[dx] : 0, i1 = live ? xtab_start[dx + 1] : 0;
+  // prologue: rows j0 .. j0 + RING - 2 in flight, issued before the x-window loads so both latencies
+  // overlap (past the window: row j0 again into its slot's successor, so every wave always has the
+  // same number of DMAs younger than the row it waits for)
+  static_for<AREA_RING - 1>([&](auto rc) __attribute__((always_inline)) {
+    constexpr int r = decltype(rc)::value;
+    issue(j0 + r < j1 ? j0 + r : j0, rc);
+  });
   // the pixel's x-window in registers (<= MAXT taps: scale < MAXT - 1; wider windows re-read the table)
   constexpr int MAXT = 16;
   const int nt = i1 - i0;
   int xo[MAXT];
   float xa[MAXT];
+  // (every entry loaded unconditionally - an in-window index or the window's first - so the 16 loads go
+  // out together: guarded loads were issued one round trip after another)
+  int tsi[MAXT];
+  float tal[MAXT];
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) {
-    const AreaTab tx = t < nt ? xtab[i0 + t] : AreaTab{0, 0, 0.f};
-    xo[t] = tx.si * 3 - b0;
-    xa[t] = tx.alpha;
+    const AreaTab tx = xtab[t < nt ? i0 + t : i0];
+    tsi[t] = tx.si;
+    tal[t] = tx.alpha;
   }
-  // prologue: rows j0 .. j0 + RING - 2 in flight (past the window: row j0 again into its slot's
-  // successor, so every wave always has the same number of DMAs younger than the row it waits for)
 #pragma unroll
-  for (int r = 0; r < AREA_RING - 1; ++r) issue(j0 + r < j1 ? j0 + r : j0, r);
+  for (int t = 0; t < MAXT; ++t) asm volatile("" : "+v"(tsi[t]), "+v"(tal[t]));   // (no sinking into branches)
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t) {
+    xo[t] = t < nt ? tsi[t] * 3 - b0 : 0;
+    xa[t] = t < nt ? tal[t] : 0.f;
+  }
   float acc[3] = {0.f, 0.f, 0.f};
-  for (int j = j0; j < j1; ++j) {
-    const int k = j - j0;
+  // one source row per step, unrolled by the ring depth so every ring slot is a compile-time offset: with
+  // a run-time slot the compiler cannot tell which LDS-DMA a row read depends on and waited vmcnt(0) at
+  // every step (one row in flight instead of RING - 1)
+  auto step = [&](int j, auto slotc) __attribute__((always_inline)) {
+    constexpr int slot = decltype(slotc)::value;
     // row j landed: the youngest (RING - 2) rows' DMAs may still be in flight
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"((AREA_RING - 2) * AREA_PPW) : "memory");
-    __syncthreads();   // every wave's pieces of row j; every thread done with row j - 1's slot
+    __builtin_amdgcn_s_barrier();   // every wave's pieces of row j; every thread done with row j - 1's slot
     const int jn = j + AREA_RING - 1;
-    issue(jn < j1 ? jn : j0, (k + AREA_RING - 1) % AREA_RING);
-    const uint8_t* row = ring + (k % AREA_RING) * AREA_ROWB;
+    issue(jn < j1 ? jn : j0, std::integral_constant<int, (slot + AREA_RING - 1) % AREA_RING>{});
+    const uint8_t* row = ring + slot * AREA_ROWB;
     const AreaTab ty = ytab[j];
     float rsum[3] = {0.f, 0.f, 0.f};
     if (nt <= MAXT) {
@@ -498,6 +519,11 @@ __global__ __launch_bounds__(256) void resize_area_rows_u8(const AreaJob* __rest
     }
 #pragma unroll
     for (int c = 0; c < 3; ++c) acc[c] += rsum[c] * ty.alpha;
+  };
+  for (int j = j0; j < j1; j += AREA_RING) {
+    static_for<AREA_RING>([&](auto rc) __attribute__((always_inline)) {
+      if (j + decltype(rc)::value < j1) step(j + decltype(rc)::value, rc);
+    });
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the dummy tail DMAs, before the workgroup's LDS goes)
   if (!live) return;

@@ -177,7 +177,8 @@ def test_arcface_f16x3_hxi_bit_identical(gpu_ctx, monkeypatch, batch):
     halo staged per group of 64 input channels) runs the 58 14x14x256 and 24 28x28x128
     layers of a large batch (profile codes 502 / 503, PC_CONV_HXI=3: both shapes) and gives the fused tiles'
     bits (PC_CONV_HXI=0): same K order (64-channel groups, taps, 32-channel blocks), same MFMA order per
-    k-step, conv_epilogue_lds's arithmetic (with and without residual)."""
+    k-step, conv_epilogue_lds's arithmetic (with and without residual). The 28x28 form runs at two
+    workgroups per CU with one halo stage (default) or one per CU with two (PC_HXI28_OCC=1): same bits."""
     from person_capture_amd.runtime import Net
     P = models.compile_iresnet(models.synth_iresnet(100, seed=8), 100, split=True)
     x = np.zeros((batch, 112, 112, 4), np.float16)
@@ -185,8 +186,10 @@ def test_arcface_f16x3_hxi_bit_identical(gpu_ctx, monkeypatch, batch):
     d = gpu_ctx.upload(x)
     outs, codes = [], []
     try:
-        for hxi in ("3", "0"):
+        for hxi, occ in (("3", None), ("0", None), ("3", "1")):
             monkeypatch.setenv("PC_CONV_HXI", hxi)
+            if occ:
+                monkeypatch.setenv("PC_HXI28_OCC", occ)
             net = Net(gpu_ctx, P.serialize(), PC_PREC_F16, max_batch=batch)
             try:
                 net.profile(True)
@@ -200,7 +203,9 @@ def test_arcface_f16x3_hxi_bit_identical(gpu_ctx, monkeypatch, batch):
         d.free()
     assert sum(1 for c in codes[0] if c == 502) == 58 and sum(1 for c in codes[0] if c == 503) == 24, codes[0]
     assert 502 not in codes[1] and 503 not in codes[1]
+    assert codes[2] == codes[0]
     assert np.array_equal(outs[0].view(np.uint8), outs[1].view(np.uint8))
+    assert np.array_equal(outs[0].view(np.uint8), outs[2].view(np.uint8))
 
 
 def test_arcface_f16_hxi_bit_identical(gpu_ctx, monkeypatch):

@@ -7,7 +7,7 @@ T=$1; OUT=$2; CMD=$3
 for attempt in $(seq 1 30); do
   /usr/local/graft/bin/gpurun --timeout "$T" -- "$CMD" > "$OUT" 2>&1
   rc=$?
-  if grep -q "status=transient" "$OUT" && ! grep -q "status=ok\|status=fail" "$OUT"; then
+  if grep -q "status=transient\|slot(s) on this pod are busy\|no free box" "$OUT" && ! grep -q "status=ok\|status=fail" "$OUT"; then
     sleep 60
     continue
   fi
