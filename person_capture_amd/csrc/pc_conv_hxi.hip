@@ -48,12 +48,12 @@ struct HxiGeom {
   static constexpr int SB = SPLIT ? 256 : CIN * 2;           // halo slot bytes
   static constexpr int NB = SPLIT ? 2 : CIN / 32;            // 32-channel blocks per staged group
   static constexpr int NG = SPLIT ? CIN / 64 : 1, KPG = 9 * NB, NKS = NG * KPG;
-  // a 2-stage ring where the groups are several; at two workgroups per CU one stage (the other
-  // workgroup's MFMAs cover the exposed staging)
-  static constexpr int NSTAGE = NG > 1 && OCC == 1 ? 2 : 1;
   static constexpr int SLOTS = (ROWS + 2) * PITCH + 2;       // + the 2 slots discarded columns reach
   static constexpr int PIECES = (SLOTS * SB + 1023) / 1024;
   static constexpr int STAGE = PIECES * 1024;
+  // a 2-stage ring where the groups are several and two stages fit the workgroup's LDS share; else one
+  // stage (at two workgroups per CU the other workgroup's MFMAs cover the exposed staging)
+  static constexpr int NSTAGE = NG > 1 && 2 * STAGE * OCC <= 163840 ? 2 : 1;
   static constexpr int NPIX = ROWS * HW;
   static constexpr int PC = COUT * NPIX * 4 <= 131072 / OCC ? COUT : COUT / 2;   // channels per epilogue pass
   static constexpr int NPASS = COUT / PC;
@@ -379,6 +379,7 @@ hipError_t conv_hxi_launch(const ConvParams& p, hipStream_t s) {
   if (!conv_hxi_ok(p)) return hipErrorInvalidValue;
   const bool split = p.ysplit != 0;
   if (p.OH == 14) {
+    // (half an image per workgroup at two per CU, 7 rows: 147.7 vs 145.3 us, profiles/r06t_hxi14_half_ab.txt)
     if (split) hipLaunchKernelGGL((conv_hxi<PC_HXI_14, true, 1>), dim3(p.N), dim3(512), 0, s, p);
     else hipLaunchKernelGGL((conv_hxi<PC_HXI_14, false, 1>), dim3(p.N), dim3(512), 0, s, p);
   } else {

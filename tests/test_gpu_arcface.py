@@ -186,10 +186,10 @@ def test_arcface_f16x3_hxi_bit_identical(gpu_ctx, monkeypatch, batch):
     d = gpu_ctx.upload(x)
     outs, codes = [], []
     try:
-        for hxi, occ in (("3", None), ("0", None), ("3", "1")):
+        for hxi, env in (("3", {}), ("0", {}), ("3", {"PC_HXI28_OCC": "1"})):
             monkeypatch.setenv("PC_CONV_HXI", hxi)
-            if occ:
-                monkeypatch.setenv("PC_HXI28_OCC", occ)
+            for k, v in env.items():
+                monkeypatch.setenv(k, v)
             net = Net(gpu_ctx, P.serialize(), PC_PREC_F16, max_batch=batch)
             try:
                 net.profile(True)
