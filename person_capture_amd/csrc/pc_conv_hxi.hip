@@ -41,14 +41,15 @@ namespace pc {
 template <int HW, int PITCH, int ROWS, int CIN, int COUT, int WCH, int WPX, bool SPLIT, int OCC>
 struct HxiGeom {
   static constexpr int NW = WCH * WPX, NT = 64 * NW;
-  static constexpr int NF = ROWS * PITCH / 16;              // pixel fragments per workgroup
+  static constexpr int NF = (ROWS * PITCH + 15) / 16;       // pixel fragments per workgroup (16 slots each)
   static constexpr int TP = NF / WPX, TC = COUT / WCH / 16;
   // fragments per read group (two workgroups per CU: one at a time, their 4 waves per SIMD hide the reads)
   static constexpr int TPG = OCC > 1 ? 1 : (TP > 7 ? (TP % 2 == 0 ? TP / 2 : TP) : TP);
   static constexpr int SB = SPLIT ? 256 : CIN * 2;           // halo slot bytes
   static constexpr int NB = SPLIT ? 2 : CIN / 32;            // 32-channel blocks per staged group
   static constexpr int NG = SPLIT ? CIN / 64 : 1, KPG = 9 * NB, NKS = NG * KPG;
-  static constexpr int SLOTS = (ROWS + 2) * PITCH + 2;       // + the 2 slots discarded columns reach
+  // halo slots: the padded rows, + what the taps of the last fragment's discarded slots reach
+  static constexpr int SLOTS = (NF * 16 > ROWS * PITCH ? NF * 16 - ROWS * PITCH : 0) + (ROWS + 2) * PITCH + 2;
   static constexpr int PIECES = (SLOTS * SB + 1023) / 1024;
   static constexpr int STAGE = PIECES * 1024;
   // a 2-stage ring where the groups are several and two stages fit the workgroup's LDS share; else one
@@ -63,7 +64,7 @@ struct HxiGeom {
   static constexpr int WTILE = SPLIT ? 2048 : 1024;          // packed weight bytes per K tile and 16-row block
   static constexpr int CGN = PC / 8;                         // 8-channel items per pixel and pass
   static constexpr int IT = (NPIX + NT / CGN - 1) / (NT / CGN);   // items (pixels) per thread and pass
-  static_assert(PITCH % 16 == 0 && PITCH >= HW + 2 && NF % WPX == 0 && TP % TPG == 0, "pixel fragments");
+  static_assert(PITCH >= HW + 2 && NF % WPX == 0 && TP % TPG == 0, "pixel fragments");
   static_assert(COUT % (16 * WCH) == 0 && CIN % 64 == 0 && HW % ROWS == 0 && SB % 256 == 0, "tiling");
   static_assert(SMEM <= 163840, "LDS");
   static_assert(NPASS == 1 || WCH % 2 == 0, "epilogue passes split the channel waves");
@@ -141,21 +142,20 @@ __global__ __launch_bounds__(512, 2 * OCC) void conv_hxi(ConvParams p) {
     for (int t = 0; t < TP; ++t) acc[a][t] = f32x4{0.f, 0.f, 0.f, 0.f};
   if (p.dbg & 8) return;   // tuning only (PC_CONV_DBG): prologue only
 
-  // per-lane LDS byte of (tap column dx, chunk kind) for slot fr + dx of halo row 0
-  // (recomputed at each k-step - the asm keeps the compiler from hoisting all (dx, block) offsets of
+  // per-lane LDS byte of (tap, chunk kind) for slot fr + sh, sh = dy PITCH + dx the tap's slot shift (the
+  // swizzle key is the slot's low bits: at a pitch that is not a multiple of 8 the row shift changes them)
+  // (recomputed at each k-step - the asm keeps the compiler from hoisting all (tap, block) offsets of
   // the unrolled loop into registers at once: 24 of them in the plain 256-channel form)
-  auto boff = [&](int dx, int chunk) __attribute__((always_inline)) {
-    const int h = fr + dx;
+  auto boff = [&](int sh, int chunk) __attribute__((always_inline)) {
+    const int h = fr + sh;
     unsigned v = (unsigned)(h * SB + ((chunk ^ ((h & 7) << 1)) << 4));
     asm volatile("" : "+v"(v));
     return v;
   };
-  // halo slot of fragment t's first slot at tap (0, 0): fragment f = wpx * TP + t covers output row
-  // f / (PITCH / 16), columns 16 (f % (PITCH / 16)) .. +16
-  auto fslot = [&](int t) __attribute__((always_inline)) {
-    const int f = wpx * TP + t;
-    return (f / (PITCH / 16)) * PITCH + (f % (PITCH / 16)) * 16;
-  };
+  // halo slot of fragment t's first slot at tap (0, 0): fragment f = wpx * TP + t covers output slots
+  // 16 f .. 16 f + 15 (slot o = output row o / PITCH, column o % PITCH; columns >= HW and rows >= ROWS are
+  // discarded - a pitch that is not a multiple of 16 lets a fragment span two rows: the 7x7 form's 9)
+  auto fslot = [&](int t) __attribute__((always_inline)) { return (wpx * TP + t) * 16; };
   static_for<NG>([&](auto gc) __attribute__((always_inline)) {
     constexpr int g = decltype(gc)::value, st = G::NSTAGE == 2 ? (g & 1) : 0;
     if constexpr (G::NSTAGE == 1 && g > 0) {   // one stage: group g replaces g - 1 once every wave is done
@@ -173,14 +173,17 @@ __global__ __launch_bounds__(512, 2 * OCC) void conv_hxi(ConvParams p) {
       constexpr int k = decltype(kc)::value, tap = k / NB, blk = k % NB, s = g * KPG + k, q = s & 1;
       constexpr int dy = tap / 3, dx = tap % 3;
       if constexpr (s + 1 < NKS) wload(wbh[q ^ 1], wbl[q ^ 1], s + 1);
-      const unsigned oh = boff(dx, blk * 4 + kg), ol = SPLIT ? boff(dx, 8 + blk * 4 + kg) : 0u;
+      // (pitches that are multiples of 8 keep the row shift out of the swizzled offset: fewer live offsets -
+      // folding it in spilled the two-workgroup 28x28 form)
+      constexpr int sh = PITCH % 8 == 0 ? dx : dy * PITCH + dx, rsh = PITCH % 8 == 0 ? dy * PITCH : 0;
+      const unsigned oh = boff(sh, blk * 4 + kg), ol = SPLIT ? boff(sh, 8 + blk * 4 + kg) : 0u;
       if (p.dbg & 2) return;   // tuning only: no MFMAs
       static_for<TP / TPG>([&](auto pc) __attribute__((always_inline)) {
         constexpr int t0 = decltype(pc)::value * TPG;
         f16x8 bh[TPG], bl[SPLIT ? TPG : 1];
 #pragma unroll
         for (int t = 0; t < TPG; ++t)
-          bh[t] = *reinterpret_cast<const f16x8*>(base + oh + (fslot(t0 + t) + dy * PITCH) * SB);
+          bh[t] = *reinterpret_cast<const f16x8*>(base + oh + (fslot(t0 + t) + rsh) * SB);
         if constexpr (!SPLIT) {   // plain f16: one MFMA per fragment pair
 #pragma unroll
           for (int a = 0; a < TC; ++a)
@@ -198,7 +201,7 @@ __global__ __launch_bounds__(512, 2 * OCC) void conv_hxi(ConvParams p) {
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int t = 0; t < TPG; ++t)
-          bl[t] = *reinterpret_cast<const f16x8*>(base + ol + (fslot(t0 + t) + dy * PITCH) * SB);
+          bl[t] = *reinterpret_cast<const f16x8*>(base + ol + (fslot(t0 + t) + rsh) * SB);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int a = 0; a < TC; ++a)
@@ -285,9 +288,9 @@ __global__ __launch_bounds__(512, 2 * OCC) void conv_hxi(ConvParams p) {
       for (int a = 0; a < TC; ++a)
 #pragma unroll
         for (int t = 0; t < TP; ++t) {
-          const int f = wpx * TP + t;
-          const int orow = f / (PITCH / 16), ocol = (f % (PITCH / 16)) * 16 + fr;
-          if (ocol < HW) {
+          const int o = (wpx * TP + t) * 16 + fr;
+          const int orow = o / PITCH, ocol = o % PITCH;
+          if (ocol < HW && orow < ROWS) {
             const int pl = orow * HW + ocol;
             const int cl = (NPASS == 1 ? wch : wch % (WCH / 2)) * TC * 16 + a * 16 + kg * 4;
             *reinterpret_cast<f32x4*>(im + pl * RS + cl) = acc[a][t];
@@ -359,6 +362,9 @@ __global__ __launch_bounds__(512, 2 * OCC) void conv_hxi(ConvParams p) {
 // 28x28x128 at two workgroups per CU (its halo stage is 73 KB)
 #define PC_HXI_14 14, 16, 14, 256, 256, 8, 1
 #define PC_HXI_28 28, 32, 7, 128, 128, 4, 2
+// 7x7x512 (the last stage, split only): one image per workgroup at pitch 9 - 63 slots in 4 fragments
+// (77 % kept; a pitch of 16 would keep 44 %), 8 x 1 waves of 64 channels x 4 fragments
+#define PC_HXI_7 7, 9, 7, 512, 512, 8, 1
 
 // can a conv run here: one segment of C channels (split: X.C 2 C = [hi | lo]; plain f16: X.C C), dense,
 // on an HW x HW map of an instantiated shape, C output channels written in the same form (dense), 3x3
@@ -367,7 +373,7 @@ int conv_hxi_ok(const ConvParams& p) {
   const ConvSeg& S = p.seg[0];
   const bool split = p.ysplit != 0;
   const int C = split ? S.C / 2 : S.C, w = split ? 2 : 1;
-  const bool shape = (S.H == 14 && C == 256) || (S.H == 28 && C == 128);
+  const bool shape = (S.H == 14 && C == 256) || (S.H == 28 && C == 128) || (split && S.H == 7 && C == 512);
   return shape && p.nseg == 1 && S.cs == w * C && S.W == S.H && S.KH == 3 && S.KW == 3 && S.stride == 1 &&
          S.pad == 1 && p.OH == S.H && p.OW == S.H && p.npad == C && p.ycs == w * C && p.splitk == 1 && !p.out_f32 &&
          !p.yc8 && !p.rc8 && p.ktot == 9 * (split ? 3 : 1) * C && p.res_mode != RES_UP2 &&
@@ -378,7 +384,9 @@ int conv_hxi_ok(const ConvParams& p) {
 hipError_t conv_hxi_launch(const ConvParams& p, hipStream_t s) {
   if (!conv_hxi_ok(p)) return hipErrorInvalidValue;
   const bool split = p.ysplit != 0;
-  if (p.OH == 14) {
+  if (p.OH == 7) {
+    hipLaunchKernelGGL((conv_hxi<PC_HXI_7, true, 1>), dim3(p.N), dim3(512), 0, s, p);
+  } else if (p.OH == 14) {
     // (half an image per workgroup at two per CU, 7 rows: 147.7 vs 145.3 us, profiles/r06t_hxi14_half_ab.txt)
     if (split) hipLaunchKernelGGL((conv_hxi<PC_HXI_14, true, 1>), dim3(p.N), dim3(512), 0, s, p);
     else hipLaunchKernelGGL((conv_hxi<PC_HXI_14, false, 1>), dim3(p.N), dim3(512), 0, s, p);

@@ -175,7 +175,8 @@ def test_arcface_f16x3_wg_layouts_bit_identical(gpu_ctx, monkeypatch):
 def test_arcface_f16x3_hxi_bit_identical(gpu_ctx, monkeypatch, batch):
     """conv_hxi (pc_conv_hxi.hip: a workgroup per 14x14 image / per 7 rows of a 28x28 image, the padded
     halo staged per group of 64 input channels) runs the 58 14x14x256 and 24 28x28x128
-    layers of a large batch (profile codes 502 / 503, PC_CONV_HXI=3: both shapes) and gives the fused tiles'
+    layers of a large batch (profile codes 502 / 503; PC_CONV_HXI=19: those and the 4 7x7x512 ones, code
+    505, at pitch 9 - fragments that span two rows) and gives the fused tiles'
     bits (PC_CONV_HXI=0): same K order (64-channel groups, taps, 32-channel blocks), same MFMA order per
     k-step, conv_epilogue_lds's arithmetic (with and without residual). The 28x28 form runs at two
     workgroups per CU with one halo stage (default) or one per CU with two (PC_HXI28_OCC=1): same bits."""
@@ -186,7 +187,7 @@ def test_arcface_f16x3_hxi_bit_identical(gpu_ctx, monkeypatch, batch):
     d = gpu_ctx.upload(x)
     outs, codes = [], []
     try:
-        for hxi, env in (("3", {}), ("0", {}), ("3", {"PC_HXI28_OCC": "1"})):
+        for hxi, env in (("19", {}), ("0", {}), ("19", {"PC_HXI28_OCC": "1"})):
             monkeypatch.setenv("PC_CONV_HXI", hxi)
             for k, v in env.items():
                 monkeypatch.setenv(k, v)
@@ -202,7 +203,8 @@ def test_arcface_f16x3_hxi_bit_identical(gpu_ctx, monkeypatch, batch):
     finally:
         d.free()
     assert sum(1 for c in codes[0] if c == 502) == 58 and sum(1 for c in codes[0] if c == 503) == 24, codes[0]
-    assert 502 not in codes[1] and 503 not in codes[1]
+    assert sum(1 for c in codes[0] if c == 505) == 4, codes[0]
+    assert not {502, 503, 505} & set(codes[1])
     assert codes[2] == codes[0]
     assert np.array_equal(outs[0].view(np.uint8), outs[1].view(np.uint8))
     assert np.array_equal(outs[0].view(np.uint8), outs[2].view(np.uint8))
