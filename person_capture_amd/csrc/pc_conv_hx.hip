@@ -18,6 +18,8 @@
 // kernel where its grid fills the CUs; tests/test_gpu_plan_classes.py).
 #include "pc_conv_common.h"
 
+#include <cstdlib>
+
 namespace pc {
 
 constexpr int HX_TW = 16, HX_TH = 12, HX_PW = HX_TW + 2, HX_SLOTS = (HX_TH + 2) * HX_PW;
@@ -26,9 +28,16 @@ constexpr int HX_BYTES = HX_SLOTS * HX_SB;        // 64512 = 63 x 1 KiB
 static_assert(HX_BYTES % 1024 == 0, "halo DMA pieces");
 static_assert(HX_TH * HX_TW * 68 * 4 <= HX_BYTES, "epilogue image over the halo");
 
+// WLDS: each k-step's weight tile (8 KB) comes into the LDS once per workgroup by LDS-DMA (a 2-slot ring
+// after the halo, 79 KB per workgroup: still two per CU) and the four waves read their fragments from
+// there, instead of every wave loading all 8 fragments from L2 into registers (8 KB per wave and k-step
+// through the TA / TD return path, which the 8 waves of a CU share with the halo DMA). Same fragments,
+// same MFMA order: the same bits.
+template <bool WLDS>
 __global__ __launch_bounds__(256, 2) void conv_hx64(ConvParams p, int nby, int nbx) {
   constexpr int TC = 4, TP = HX_TH / 4, NKS = 18;   // 64 channels, 3 rows per wave, 9 taps x 2 k-steps
-  __shared__ __attribute__((aligned(16))) char halo[HX_BYTES];
+  constexpr int WT = 8192;                          // packed weight bytes per k-step
+  __shared__ __attribute__((aligned(16))) char halo[HX_BYTES + (WLDS ? 2 * WT : 0)];
   const ConvSeg& S = p.seg[0];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -71,8 +80,18 @@ __global__ __launch_bounds__(256, 2) void conv_hx64(ConvParams p, int nby, int n
       wl[a] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16 + (a * 2 + 1) * 1024, kt * 8192, 0));
     }
   };
-  f16x8 wbh[2][TC], wbl[2][TC];
-  wload(wbh[0], wbl[0], 0);
+  // WLDS: k-step s's weight tile into ring slot: pieces 2 wave + j (1 KiB each) of the packed tile
+  auto wdma = [&](int s, int slot) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int piece = wave * 2 + j;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_ptr_t)(halo + HX_BYTES + slot * WT + piece * 1024), 16,
+                                               piece * 1024 + lane * 16, s * WT, 0, 0);
+    }
+  };
+  f16x8 wbh[WLDS ? 1 : 2][TC], wbl[WLDS ? 1 : 2][TC];
+  if constexpr (WLDS) wdma(0, 0);
+  else wload(wbh[0], wbl[0], 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the halo (and k-step 0's weights)
   __syncthreads();
   if (p.dbg & 8) return;   // tuning only (PC_CONV_DBG): staging only
@@ -88,9 +107,24 @@ __global__ __launch_bounds__(256, 2) void conv_hx64(ConvParams p, int nby, int n
   for (int t = 0; t < TP; ++t) bslot[t] = (wave * TP + t) * HX_PW + fr;
 
   static_for<NKS>([&](auto sc) __attribute__((always_inline)) {
-    constexpr int s = decltype(sc)::value, tap = s / 2, ks = s % 2, q = s & 1;
+    constexpr int s = decltype(sc)::value, tap = s / 2, ks = s % 2;
+    constexpr int q = WLDS ? 0 : (s & 1);
     constexpr int toff = (tap / 3) * HX_PW + (tap % 3);
-    if constexpr (s + 1 < NKS) wload(wbh[q ^ 1], wbl[q ^ 1], s + 1);
+    if constexpr (WLDS) {
+      if constexpr (s > 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's pieces of k-step s's tile
+        __builtin_amdgcn_s_barrier();                      // every wave's pieces; every wave done with slot s - 1
+      }
+      // the fragment reads go out before the next tile's DMA, so nothing has to wait for it
+      const char* wt = halo + HX_BYTES + (s & 1) * WT + lane * 16;
+#pragma unroll
+      for (int a = 0; a < TC; ++a) {
+        wbh[0][a] = *reinterpret_cast<const f16x8*>(wt + (a * 2) * 1024);
+        wbl[0][a] = *reinterpret_cast<const f16x8*>(wt + (a * 2 + 1) * 1024);
+      }
+    } else if constexpr (s + 1 < NKS) {
+      wload(wbh[q ^ 1], wbl[q ^ 1], s + 1);
+    }
     f16x8 bh[TP], bl[TP];
 #pragma unroll
     for (int t = 0; t < TP; ++t) {
@@ -99,6 +133,7 @@ __global__ __launch_bounds__(256, 2) void conv_hx64(ConvParams p, int nby, int n
       bh[t] = *reinterpret_cast<const f16x8*>(halo + sl * HX_SB + (((ks * 4 + g) ^ sw) << 4));
       bl[t] = *reinterpret_cast<const f16x8*>(halo + sl * HX_SB + (((8 + ks * 4 + g) ^ sw) << 4));
     }
+    if constexpr (WLDS && s + 1 < NKS) wdma(s + 1, (s + 1) & 1);
     if (p.dbg & 2) return;   // tuning only: no MFMAs
 #pragma unroll
     for (int a = 0; a < TC; ++a)
@@ -460,7 +495,11 @@ int conv_hx_ok(const ConvParams& p) {
 hipError_t conv_hx_launch(const ConvParams& p, hipStream_t s) {
   if (!conv_hx_ok(p)) return hipErrorInvalidValue;
   const int nby = (p.OH + HX_TH - 1) / HX_TH, nbx = (p.OW + HX_TW - 1) / HX_TW;
-  hipLaunchKernelGGL(conv_hx64, dim3(p.N * nby * nbx), dim3(256), 0, s, p, nby, nbx);
+  // (per launch: the A/B switches it in one process)
+  if (getenv("PC_HX64_WLDS") && atoi(getenv("PC_HX64_WLDS")) == 0)
+    hipLaunchKernelGGL(conv_hx64<false>, dim3(p.N * nby * nbx), dim3(256), 0, s, p, nby, nbx);
+  else
+    hipLaunchKernelGGL(conv_hx64<true>, dim3(p.N * nby * nbx), dim3(256), 0, s, p, nby, nbx);
   return hipGetLastError();
 }
 
