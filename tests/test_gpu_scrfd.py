@@ -55,8 +55,10 @@ def test_scrfd_net_parity(gpu_ctx, s10g, prec, tol):
             assert err < tol, f"level {lvl}: rel err {err}"
 
 
-@pytest.mark.parametrize("thresh", [0.5, 0.3, 0.2])
+@pytest.mark.parametrize("thresh", [0.5, 0.3, 0.2, 0.05])
 def test_scrfd_decode_nms_bit_exact(gpu_ctx, s10g, thresh):
+    """(0.05: thousands of candidates and hundreds of kept boxes per image - many 64-candidate blocks of
+    the LDS NMS, each resolved against a long kept list)"""
     D = 640
     eng = ScrfdEngine(gpu_ctx, s10g, "10g", D=D, precision=PC_PREC_F16, max_batch=3, max_det=4096)
     frames = [_frame(10), _frame(11, 1080, 1920), _frame(12, 480, 300)]

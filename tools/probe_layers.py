@@ -1,7 +1,8 @@
 """Per-layer profile of the two trunks (HIP events around every launch, pc_net_profile_ops).
 usage: python tools/probe_layers.py [arc|arcx3|scrfd|scrfdx3] [batch]   -> table grouped by conv shape.
 scrfdx3 / arcx3: the f16x3 split programs.
-PROBE_MAXB=N: create the net for N images (the small-batch plans then serve batch <= min(16, N/4))."""
+PROBE_MAXB=N: create the net for N images (the small-batch plans then serve batch <= min(16, N/4)).
+PROBE_D=D: the SCRFD det size (default 640)."""
 import sys
 from collections import defaultdict
 
@@ -35,8 +36,8 @@ def main():
     if which in ("arc", "arcx3"):
         P = models.compile_iresnet(models.synth_iresnet(100, seed=0, calibrate=False), 100, split=which == "arcx3")
     else:
-        P = models.compile_scrfd(models.synth_scrfd("10g", seed=0, calibrate=False), "10g", 640,
-                                 split=which == "scrfdx3")
+        P = models.compile_scrfd(models.synth_scrfd("10g", seed=0, calibrate=False), "10g",
+                                 int(os.environ.get("PROBE_D", 640)), split=which == "scrfdx3")
     prec = PC_PREC_F32 if os.environ.get('PROBE_F32') else PC_PREC_F16
     net = Net(ctx, P.serialize(), prec, max_batch=int(os.environ.get('PROBE_MAXB', B)))   # FaceEmbedder: 512 for arc
     H, W, Cc = P.dims(P.input)
