@@ -27,6 +27,7 @@ constexpr int HX_SB = 256;                        // slot bytes: 64 hi + 64 lo f
 constexpr int HX_BYTES = HX_SLOTS * HX_SB;        // 64512 = 63 x 1 KiB
 static_assert(HX_BYTES % 1024 == 0, "halo DMA pieces");
 static_assert(HX_TH * HX_TW * 68 * 4 <= HX_BYTES, "epilogue image over the halo");
+static_assert(HX_TH * HX_TW % 32 == 0, "epilogue: 32 pixels per round of 8-channel groups");
 
 // WLDS: each k-step's weight tile (8 KB) comes into the LDS once per workgroup by LDS-DMA (a 2-slot ring
 // after the halo, 79 KB per workgroup: still two per CU) and the four waves read their fragments from
@@ -160,6 +161,26 @@ __global__ __launch_bounds__(256, 2) void conv_hx64(ConvParams p, int nby, int n
   // or border class), the activation select, split residual hi + lo - and stores the hi and
   // lo halves as one 16-byte vector each (conv_epilogue_lds's arithmetic) ----
   constexpr int RS = 68;                 // padded image row (floats)
+  // a thread keeps one 8-channel group for NIT pixels; their residual rows are requested first, so
+  // the loads run under the image transposition (loaded per pixel, the epilogue took 89 of 232 us on
+  // 160x160x64, profiles/r06ad_hx_phase_split.txt)
+  constexpr int NIT = HX_TH * HX_TW / 32;
+  const int OW = p.OW, OH = p.OH;
+  const int cg = threadIdx.x & 7, ch = cg * 8;
+  const bool has_res = p.res_mode != RES_NONE;
+  f16x8 rh[NIT], rl[NIT];
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    rh[k] = f16x8{};
+    rl[k] = f16x8{};
+    const int pl = (threadIdx.x >> 3) + 32 * k;
+    const int oy = oy0 + (pl >> 4), ox = ox0 + (pl & 15);
+    if (has_res && oy < OH && ox < OW) {
+      const f16* rp = reinterpret_cast<const f16*>(p.res) + (((long long)n * OH + oy) * OW + ox) * p.rcs + ch;
+      rh[k] = *reinterpret_cast<const f16x8*>(rp);
+      rl[k] = *reinterpret_cast<const f16x8*>(rp + p.rsplit);
+    }
+  }
   __syncthreads();                       // every wave is done with the halo
   float* im = reinterpret_cast<float*>(halo);
 #pragma unroll
@@ -170,8 +191,6 @@ __global__ __launch_bounds__(256, 2) void conv_hx64(ConvParams p, int nby, int n
       *reinterpret_cast<f32x4*>(im + pl * RS + a * 16 + g * 4) = acc[a][t];
     }
   __syncthreads();
-  const int OW = p.OW, OH = p.OH;
-  const int cg = threadIdx.x & 7, ch = cg * 8;
   float bc[8], sl[8];
   bool keep[8];
 #pragma unroll
@@ -181,9 +200,10 @@ __global__ __launch_bounds__(256, 2) void conv_hx64(ConvParams p, int nby, int n
     keep[j] = ch + j < p.cout;
   }
   const bool smooth = p.act == ACT_SILU || p.act == ACT_GELU;
-  const bool has_res = p.res_mode != RES_NONE;
   const bool pre_act = !p.act_after_res;
-  for (int pl = threadIdx.x >> 3; pl < HX_TH * HX_TW; pl += 32) {
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    const int pl = (threadIdx.x >> 3) + 32 * k;
     const int oy = oy0 + (pl >> 4), ox = ox0 + (pl & 15);
     if (oy >= OH || ox >= OW) continue;
     const long long pix = ((long long)n * OH + oy) * OW + ox;
@@ -198,14 +218,9 @@ __global__ __launch_bounds__(256, 2) void conv_hx64(ConvParams p, int nby, int n
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] += bp[j];
     }
-    float r[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (has_res) {
-      const f16* rp = reinterpret_cast<const f16*>(p.res) + pix * p.rcs + ch;
-      const f16x8 rh = *reinterpret_cast<const f16x8*>(rp);
-      const f16x8 rl = *reinterpret_cast<const f16x8*>(rp + p.rsplit);
+    float r[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) r[j] = (float)rh[j] + (float)rl[j];
-    }
+    for (int j = 0; j < 8; ++j) r[j] = (float)rh[k][j] + (float)rl[k][j];
     if (has_res && !pre_act) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] += r[j];
