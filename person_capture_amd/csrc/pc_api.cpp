@@ -1947,7 +1947,8 @@ extern "C" int pc_net_run(pc_net* n, const void* d_in, int N) {
   pc_ctx* c = n->ctx;
   if (N <= 0 || N > n->max_batch) return fail(c, PC_ERR_ARG, "batch out of range");
   n->cur_input = d_in;
-  if (!n->use_graph || N > n->graph_max_batch) return run_ops(n, N, c->stream);
+  // (profiling runs eagerly: the per-op HIP events are the point of it)
+  if (!n->use_graph || N > n->graph_max_batch || n->prof) return run_ops(n, N, c->stream);
   // Graphs are captured on a stream private to the net, never on the context stream: a context
   // (and its stream) is shared by every FaceEmbedder of the process, and work another host thread
   // enqueued there during an open capture would be recorded into this graph (not run now, replayed
@@ -1958,6 +1959,12 @@ extern "C" int pc_net_run(pc_net* n, const void* d_in, int N) {
   auto key = std::make_pair(N, d_in);
   auto it = n->graphs.find(key);
   if (it == n->graphs.end()) {
+    // (bounded: a graph per (batch, input) pair; callers with many batch sizes start over at 256)
+    if (n->graphs.size() >= 256) {
+      HIPCHK(c, hipStreamSynchronize(c->stream));   // (launched graphs may still run)
+      for (auto& kv : n->graphs) hipGraphExecDestroy(kv.second);
+      n->graphs.clear();
+    }
     if (!n->cap_stream) HIPCHK(c, hipStreamCreateWithFlags(&n->cap_stream, hipStreamNonBlocking));
     hipGraph_t g = nullptr;
     HIPCHK(c, hipStreamBeginCapture(n->cap_stream, hipStreamCaptureModeThreadLocal));

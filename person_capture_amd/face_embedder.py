@@ -357,11 +357,12 @@ class FaceEmbedder(YoloFaceBranch):
         self._stage_threads = int(os.getenv("PERSON_CAPTURE_AMD_STAGE_THREADS", "8"))
         self._arc = ArcFaceEngine(self._ectx, self._arc_params, self._arc_depth, precision=self.arc_precision,
                                   max_batch=self._arc_batch)
-        # HIP graphs for small net runs (unchanged callers' per-frame extract(): a SCRFD pass of one
-        # frame and an ArcFace pass of its faces are ~60 and ~100 small launches each): runs of at
-        # most this many images replay a captured graph (bit-identical, the same launches);
-        # PERSON_CAPTURE_AMD_GRAPH_BATCH=0 launches eagerly
-        self._graph_batch = int(os.getenv("PERSON_CAPTURE_AMD_GRAPH_BATCH", "8"))
+        # HIP graphs for net runs (unchanged callers' per-frame extract(): a SCRFD pass of one frame and
+        # an ArcFace pass of its faces are ~60 and ~100 small launches each; a C3 ArcFace quantum ~120):
+        # SCRFD runs of at most this many images and ArcFace runs of 4x as many rows replay a captured
+        # graph (bit-identical, the same launches). 128 (round 6; was 8): C3 1014 -> 1030 frames/s, C4 /
+        # C5 unchanged (profiles/r06aj_graph_batch_ab.txt). PERSON_CAPTURE_AMD_GRAPH_BATCH=0 launches eagerly
+        self._graph_batch = int(os.getenv("PERSON_CAPTURE_AMD_GRAPH_BATCH", "128"))
         if self._graph_batch > 0:
             self._arc.net.set_graph(True, max_batch=4 * self._graph_batch)
         self._arc_feat_dim = self._arc.dim

@@ -91,3 +91,31 @@ def test_scrfd_single_frame_bit_identical_to_batch(gpu_ctx, split):
                 assert np.array_equal(small[k].view(np.uint8), large[k][:N].view(np.uint8)), (N, k)
     finally:
         net.close()
+
+
+def test_graph_replay_of_a_full_arcface_quantum(gpu_ctx):
+    """FaceEmbedder replays captured HIP graphs for ArcFace runs up to 4 x PERSON_CAPTURE_AMD_GRAPH_BATCH
+    rows (default 512: a whole C3 quantum of 256 rows): the capture and its replays give the eager run's
+    bits, and a profiled run executes eagerly (its per-op events are the point)."""
+    P = models.compile_iresnet(models.synth_iresnet(100, seed=12), 100, split=True)
+    net = Net(gpu_ctx, P.serialize(), PC_PREC_F16, max_batch=256)
+    try:
+        x = _images(256, 112, 13) * 127.5
+        d = gpu_ctx.upload(x)
+        net.run(d.ptr, 256)
+        eager = net.read_output(0, 256).copy()
+        net.set_graph(True, max_batch=512)
+        outs = []
+        for _ in range(2):   # capture, then replay
+            net.run(d.ptr, 256)
+            outs.append(net.read_output(0, 256).copy())
+        net.profile(True)
+        net.run(d.ptr, 256)
+        nrec = len(net.profile_ops())
+        net.profile(False)
+        d.free()
+        for o in outs:
+            assert np.array_equal(o.view(np.uint8), eager.view(np.uint8))
+        assert nrec >= 90, nrec   # (one record per op of the run)
+    finally:
+        net.close()
