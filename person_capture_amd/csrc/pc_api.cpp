@@ -846,7 +846,10 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
             if (out_c8 && !conv_fast_valid_c8(k, rb)) continue;   // f16c8 output / residual: LDS epilogue
             if (!conv_fast_valid_sx(k, rb)) continue;
             const long long t = (M + bp - 1) / bp * (npad / bc);
-            const double est = (double)((t + 255) / 256) * bc * bp * sxcost(k);
+            // the 2-wave whole-width tiles (20, 21) need two workgroups per CU to keep their K loop fed:
+            // a grid under one per CU ran SCRFD-x3's 20x20x224 at b32 in 124 us against 76.5 on the 32x256
+            // tile (12), at b64 130 vs 162 (profiles/r06ap_tile_sweep.txt)
+            const double est = (double)((t + 255) / 256) * bc * bp * sxcost(k) * ((k == 20 || k == 21) && t < 256 ? 2.0 : 1.0);
             if (bsx < 0 || est < bsx_t) { bsx = k; bsx_t = est; bsx_rowb = rb; }
             break;
           }
