@@ -790,7 +790,13 @@ def main():
         det_nets = [e.net for e in fe._scrfd_engines.values()] if args.frames == "per-frame" else [fe._engine(640).net]
         net_names = tuple("scrfd" if k == 0 else f"scrfd{k}" for k in range(len(det_nets))) + ("arcface",)
     nets = det_nets + [fe._arc.net]
-    if not os.getenv("PC_BENCH_NOPROF"):
+    # the roofline's HIP events: over the timed region (a profiled run launches its ops eagerly, one event
+    # per op boundary). Per-frame mode replays each frame's small runs as HIP graphs (GRAPH_BATCH), which
+    # the events would turn into eager launches: its events come from one more, profiled, step after
+    # the timed region instead (prof_steps 1)
+    prof_timed = not os.getenv("PC_BENCH_NOPROF") and args.frames != "per-frame"
+    prof_steps = args.steps if prof_timed else 1
+    if prof_timed:
         for n in nets:
             n.profile(True)
     if fe.host_times is not None:
@@ -804,6 +810,11 @@ def main():
     t1 = time.perf_counter()
     _barrier(world)
     elapsed = _max_over_ranks(world, t1 - t0)
+    if not prof_timed and not os.getenv("PC_BENCH_NOPROF"):
+        for n in nets:
+            n.profile(True)
+        step()
+        ctx.sync()
     prof = [n.profile_read() for n in nets]
     if fe.detector_backend == "yolo":
         progs = [getattr(e, "program", None) for e in fe._yf_engines.values()] + [fe._arc.program]
@@ -867,12 +878,14 @@ def main():
                                      "traffic_mean_per_launch": traffic},
                      "launches": conv_launches, "avg_launch_us": round(conv_ms * 1e3 / max(1, conv_launches), 2),
                      "flops_per_launch": round(conv_flops / max(1, conv_launches)),
-                     "conv_share_of_step": round(conv_ms * 1e-3 / (t1 - t0), 4),
+                     "conv_share_of_step": round(conv_ms / prof_steps * 1e-3 / ((t1 - t0) / args.steps), 4),
                      "streams": 2 if fe._ectx is not fe._ctx else 1,
                      "streams_note": "ArcFace (embed stream) runs beside SCRFD (detection stream): the conv "
                                      "event spans of the two overlap, so conv_share_of_step can exceed 1 and a "
                                      "launch's duration includes the co-running kernels' share of the CUs",
-                     "per_net": {name: _net_roof(name, p_, args.steps, fe) for name, p_ in zip(net_names, prof)},
+                     "per_net": {name: _net_roof(name, p_, prof_steps, fe) for name, p_ in zip(net_names, prof)},
+                     "events": ("HIP events over the timed region" if prof_timed else
+                                "HIP events of one profiled step after the timed region (its timed steps replay HIP graphs)"),
                      "traffic_unit": "HBM bytes per launch of the dominant kernel (rocprofv3 FETCH_SIZE x2 + "
                                      "WRITE_SIZE, bench_traffic.json); conv_family.traffic_mean_per_launch: the mean "
                                      "over all conv launches",
