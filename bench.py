@@ -485,11 +485,11 @@ def _kernel_of(code: float, cfg: float) -> str:
     if c == 501:
         return "conv_hxg<96,96,5> (halo-staged f16x3 per 32-channel group, pc_conv_hx.hip)"
     if c == 502:
-        return "conv_hxi<14,16,14,256,256,8,1> (image-resident f16x3, one 14x14 image per workgroup, pc_conv_hxi.hip)"
+        return "conv_hxi<14,16,14,256,256,8,1> (image-resident, one 14x14 image per workgroup, pc_conv_hxi.hip)"
     if c == 503:
-        return "conv_hxi<28,32,7,128,128,4,2> (image-resident f16x3, 7 rows of a 28x28 image per workgroup, pc_conv_hxi.hip)"
+        return "conv_hxi<28,32,7,128,128,4,2> (image-resident, 7 rows of a 28x28 image per workgroup, pc_conv_hxi.hip)"
     if c == 505:
-        return "conv_hxi<7,9,7,512,512,8,1> (image-resident f16x3, one 7x7 image per workgroup at pitch 9, pc_conv_hxi.hip)"
+        return "conv_hxi<7,9,7,512,512,8,1> (image-resident, one 7x7 image per workgroup at pitch 9, pc_conv_hxi.hip)"
     if c >= 200:
         return f"conv_t2d (2-D block kernel, variant {c - 200})"
     if c >= 100:
