@@ -490,6 +490,9 @@ def _kernel_of(code: float, cfg: float) -> str:
         return "conv_hxi<28,32,7,128,128,4,2> (image-resident, 7 rows of a 28x28 image per workgroup, pc_conv_hxi.hip)"
     if c == 505:
         return "conv_hxi<7,9,7,512,512,8,1> (image-resident, one 7x7 image per workgroup at pitch 9, pc_conv_hxi.hip)"
+    if c in (506, 507, 508):
+        shape = {506: "14,16,7,256,32,2,1", 507: "28,32,7,128,32,2,2", 508: "7,9,7,512,32,2,1"}[c]
+        return f"conv_hxi<{shape}> (small-batch form: 32 channels of 7 rows per workgroup, pc_conv_hxi.hip)"
     if c >= 200:
         return f"conv_t2d (2-D block kernel, variant {c - 200})"
     if c >= 100:
@@ -642,8 +645,9 @@ def _traffic_for(dominant, code, prec="f16"):
     if not dominant or code is None:
         return None
     # the halo-staged kernels: one instantiation per code
-    hx_names = {500: "conv_hx64", 501: "conv_hxg<96, 96", 502: "conv_hxi<14, 16, 14", 503: "conv_hxi<28, 32, 7",
-                505: "conv_hxi<7, 9, 7"}
+    hx_names = {500: "conv_hx64", 501: "conv_hxg<96, 96", 502: "conv_hxi<14, 16, 14", 503: "conv_hxi<28, 32, 7, 128, 128",
+                505: "conv_hxi<7, 9, 7, 512, 512", 506: "conv_hxi<14, 16, 7", 507: "conv_hxi<28, 32, 7, 128, 32",
+                508: "conv_hxi<7, 9, 7, 512, 32"}
     if code in hx_names:
         return dominant.get("hbm_bytes_per_launch") if hx_names[code] in dominant.get("kernel", "") else None
     if not (100 <= code < 200 or 600 <= code < 700):

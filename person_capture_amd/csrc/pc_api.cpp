@@ -31,7 +31,7 @@ hipError_t conv_halo_launch(int f32, int cfg, const ConvParams& p, hipStream_t s
 hipError_t conv_fast_launch(int f32, int rowb, int cfg, const ConvParams& p, hipStream_t s);
 hipError_t conv_hx_launch(const ConvParams& p, hipStream_t s);
 hipError_t conv_hxg_launch(const ConvParams& p, hipStream_t s);
-hipError_t conv_hxi_launch(const ConvParams& p, hipStream_t s);
+hipError_t conv_hxi_launch(const ConvParams& p, int small, hipStream_t s);
 int conv_fast_num_cfgs();
 constexpr int kFastSmallCfg0 = 15, kFastSmallCfg1 = 19;   // conv_fast tiles 15..19: small-batch plans only
 int conv_fast_tile(int cfg, int* bc, int* bp);
@@ -930,13 +930,13 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
     // batches that give every CU a workgroup (plans for >= 192 / 64 images): bit-identical to the fused
     // tiles the smaller plan classes run (same K order, MFMA order and epilogue arithmetic).
     // PC_CONV_HXI is a mask of the shapes it takes: bit 0 14x14x256, bit 1 28x28x128 (f16x3), bits 2 / 3 the
-    // same shapes of plain f16 nets, bit 4 the f16x3 7x7x512 (default 27: all but plain 14x14x256, which the
+    // same shapes of plain f16 nets, bit 4 the f16x3 7x7x512, bit 5 the small-batch forms (default 59: all but plain 14x14x256, which the
     // resident chain beats). ArcFace-x3
     // b256 per layer, interleaved on one box: 28x28x128 187.5 vs 224.2 us on the 128x256 WG tile,
     // 14x14x256 149.3 vs 151.5 on the 256x224 one; C3 962 vs 930 frames/s with the embed quantum at 128
     // faces (256 rows = one round of one-image workgroups; at 383 rows, 1.5 rounds, 876: the quantum
     // follows, face_embedder.py), profiles/r06e_*
-    const int hxi_mask = getenv("PC_CONV_HXI") ? atoi(getenv("PC_CONV_HXI")) : 27;
+    const int hxi_mask = getenv("PC_CONV_HXI") ? atoi(getenv("PC_CONV_HXI")) : 59;
     // plain f16 nets (BASELINE C2's fp16 ArcFace): bits 2 / 3 = 14x14x256 / 28x28x128 (tap-major K: the
     // plain tiles' and the resident chain's order, bit-identical). f16 ArcFace b256, one box (r06m):
     // 28x28x128 72.8 us/launch vs 94.0 on tile cfg 14 (C2 f16 7.64 vs 8.17 ms); 14x14x256 65 us x 58 =
@@ -953,14 +953,19 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
     }
     const int hc = X.C / 2;
     // (bit 4: the f16x3 7x7x512 stage, one image per workgroup at pitch 9)
+    // (bit 5, default on: the small-batch forms, 32 channels of 7 rows per workgroup, in the plans for <= 32
+    // images - a per-frame extract()'s rows; the f16x3 shapes. ArcFace-x3 at 12 rows, one box: 14x14x256
+    // 29.9 vs 31.3 us on the 64x64 tile, 28x28x128 20.7 vs 27.6, 7x7x512 35.6 vs 56.6; profiles/r06bh_*)
+    const bool hxs_shape = (hxi_mask & 32) && plan_batch <= 32 &&
+                           ((hc == 256 && X.H == 14) || (hc == 128 && X.H == 28) || (hc == 512 && X.H == 7));
     const bool hxi_shape = ((hxi_mask & 1) && hc == 256 && X.H == 14 && plan_batch >= 192) ||
                            ((hxi_mask & 2) && hc == 128 && X.H == 28 && plan_batch >= 64) ||
-                           ((hxi_mask & 16) && hc == 512 && X.H == 7 && plan_batch >= 192);
+                           ((hxi_mask & 16) && hc == 512 && X.H == 7 && plan_batch >= 192) || hxs_shape;
     if (hxi_shape && X.split && !X.c8 && !Y.c8 && X.cs == X.C && Y.split && Y.C == X.C && Y.cs == Y.C && npad == hc &&
         w[4] == 3 && w[5] == 3 && w[6] == 1 && w[7] == 1 && X.W == X.H && Y.H == X.H && Y.W == X.W && w[15] == 27 * hc &&
         !(w[21] >= 0 && (w[22] == RES_UP2 || !n->tens[w[21]].split || n->tens[w[21]].c8)) &&
         (double)X.H * X.W * n->max_batch * X.cs * esz + kZeroTail < 4294967296.0) {
-      pl.hx = hc == 256 ? 3 : hc == 128 ? 4 : 6;   // (profile codes 502 / 503 / 505)
+      pl.hx = (hc == 256 ? 3 : hc == 128 ? 4 : 6) + (hxs_shape ? (hc == 512 ? 3 : 4) : 0);   // (profile codes 502 / 503 / 505, small 506-508)
       pl.fast = pl.halo = pl.t2d = -1;
       pl.sx = 0;
     }
@@ -1717,7 +1722,7 @@ static int run_ops(pc_net* n, int N, hipStream_t s) {
       p.zero = c->zero;
       if (const char* e = getenv("PC_CONV_DBG")) p.dbg = atoi(e);
       if (pl.hx >= 3) {
-        HIPCHK(c, conv_hxi_launch(p, s));
+        HIPCHK(c, conv_hxi_launch(p, pl.hx >= 7, s));
       } else if (pl.hx == 2) {
         HIPCHK(c, conv_hxg_launch(p, s));
       } else if (pl.hx) {
@@ -1931,7 +1936,7 @@ extern "C" int pc_net_profile_ops(pc_net* n, double* out, int max_recs) {
     o[0] = r.op; o[1] = r.kind; o[2] = ms; o[3] = r.flops;
     const ConvPlan* pl = conv ? (r.small >= 0 ? &n->plans_cls[r.small][r.op] : &n->plans[r.op]) : nullptr;
     o[4] = r.code >= 0 ? r.code
-                       : conv ? (pl->hx            ? 499 + pl->hx   // 500 conv_hx64, 501 conv_hxg, 502 / 503 / 505 conv_hxi 14x14 / 28x28 / 7x7
+                       : conv ? (pl->hx            ? 499 + pl->hx   // 500 conv_hx64, 501 conv_hxg, 502 / 503 / 505 conv_hxi 14x14 / 28x28 / 7x7, 506-508 their small-batch forms
                                  : pl->c8          ? 600 + pl->fast
                                  : pl->t2d >= 0    ? 200 + pl->t2d
                                  : pl->fast >= 0   ? 100 + pl->fast

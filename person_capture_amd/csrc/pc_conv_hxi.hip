@@ -43,8 +43,17 @@ struct HxiGeom {
   static constexpr int NW = WCH * WPX, NT = 64 * NW;
   static constexpr int NF = (ROWS * PITCH + 15) / 16;       // pixel fragments per workgroup (16 slots each)
   static constexpr int TP = NF / WPX, TC = COUT / WCH / 16;
-  // fragments per read group (two workgroups per CU: one at a time, their 4 waves per SIMD hide the reads)
-  static constexpr int TPG = OCC > 1 ? 1 : (TP > 7 ? (TP % 2 == 0 ? TP / 2 : TP) : TP);
+  static constexpr int CB = CIN / COUT;                      // channel blocks: workgroups per row block
+  static constexpr int WPS = (NW * OCC + 3) / 4;             // waves per SIMD
+  // fragments per read group (4 waves per SIMD - two 8-wave workgroups per CU: one at a time, the other
+  // waves hide the reads)
+  static constexpr int TPG = WPS > 2 ? 1 : (TP > 7 ? (TP % 2 == 0 ? TP / 2 : TP) : TP);
+  // one wave per SIMD (the small-batch forms): no other wave hides a latency - the weights come 5 k-steps
+  // ahead (not 1), and the pixel fragments of k-step k + 1 are read under k-step k's MFMAs (PF): 14x14 at
+  // 12 images 34.9 -> 29.9 us. (Loader waves of their own for the halo pieces, 1-4 per workgroup, did not
+  // beat the compute waves issuing them: 28.5-30.0 / 20.9-21.0 / 37-45 us, profiles/r06bh_hxs_phase.txt)
+  static constexpr int WD = WPS == 1 ? 6 : 2;                // weight register buffers
+  static constexpr bool PF = WPS == 1 && SPLIT && TPG == TP;
   static constexpr int SB = SPLIT ? 256 : CIN * 2;           // halo slot bytes
   static constexpr int NB = SPLIT ? 2 : CIN / 32;            // 32-channel blocks per staged group
   static constexpr int NG = SPLIT ? CIN / 64 : 1, KPG = 9 * NB, NKS = NG * KPG;
@@ -71,20 +80,22 @@ struct HxiGeom {
 };
 
 template <int HW, int PITCH, int ROWS, int CIN, int COUT, int WCH, int WPX, bool SPLIT = true, int OCC = 1>
-__global__ __launch_bounds__(512, 2 * OCC) void conv_hxi(ConvParams p) {
+__global__ __launch_bounds__(64 * WCH * WPX, (WCH * WPX * OCC + 3) / 4) void conv_hxi(ConvParams p) {
   using G = HxiGeom<HW, PITCH, ROWS, CIN, COUT, WCH, WPX, SPLIT, OCC>;
   constexpr int NW = G::NW, NT = G::NT, TC = G::TC, TP = G::TP, TPG = G::TPG, NG = G::NG, NKS = G::NKS;
   constexpr int STAGE = G::STAGE, PIECES = G::PIECES, SB = G::SB, NB = G::NB, KPG = G::KPG;
   static_assert(G::SMEM * OCC <= 163840, "LDS for OCC workgroups per CU");
-  static_assert(NW == 8, "8 waves");
+  static_assert(NW <= 16, "waves");
   __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
   const ConvSeg& S = p.seg[0];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wch = wave % WCH, wpx = wave / WCH;
-  constexpr int RB = HW / ROWS;                  // row blocks per image
-  const int b = xcd_remap(blockIdx.x, p.N * RB);
-  const int n = b / RB, r0 = (b - n * RB) * ROWS;
+  constexpr int RB = HW / ROWS, CB = G::CB;      // row blocks per image, channel blocks per row block
+  // (a row block's CB workgroups are consecutive: on one XCD after the remap, sharing its halo in the L2)
+  const int b = xcd_remap(blockIdx.x, p.N * RB * CB);
+  const int cb = b % CB, nb = b / CB;
+  const int n = nb / RB, r0 = (nb - n * RB) * ROWS;
   const int fr = lane & 15, kg = lane >> 4;
 
   auto rsrc = [](const void* base) __attribute__((always_inline)) {
@@ -126,14 +137,19 @@ __global__ __launch_bounds__(512, 2 * OCC) void conv_hxi(ConvParams p) {
   auto wload = [&](f16x8* wh, f16x8* wl, int s) __attribute__((always_inline)) {
 #pragma unroll
     for (int a = 0; a < TC; ++a) {
-      const int o = (TC * wch + a) * G::WTILE + lane * 16;
+      const int o = (cb * (COUT / 16) + TC * wch + a) * G::WTILE + lane * 16;
       wh[a] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, o, s * tile, 0));
       if constexpr (SPLIT) wl[a] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, o + 1024, s * tile, 0));
     }
   };
-  f16x8 wbh[2][TC], wbl[2][TC];
+  constexpr int WD = G::WD;
+  f16x8 wbh[WD][TC], wbl[WD][TC];
   stage(0, 0);
-  wload(wbh[0], wbl[0], 0);
+  static_for<WD - 1>([&](auto jc) __attribute__((always_inline)) {
+    constexpr int j = decltype(jc)::value;
+    if constexpr (j < NKS) wload(wbh[j], wbl[j], j);
+  });
+  f16x8 bhp[2][G::PF ? TP : 1];   // (PF: this and the next k-step's hi pixel fragments)
 
   f32x4 acc[TC][TP];
 #pragma unroll
@@ -163,21 +179,63 @@ __global__ __launch_bounds__(512, 2 * OCC) void conv_hxi(ConvParams p) {
       stage(g, 0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
-      // group g's halo: every VMEM op but the youngest (the next k-step's weights) has landed
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SPLIT ? 2 * TC : TC) : "memory");
+      // group g's halo: every VMEM op but the youngest (the next WD - 1 k-steps' weights) has landed
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((WD - 1) * (SPLIT ? 2 * TC : TC)) : "memory");
     }
     __syncthreads();   // every wave's pieces of group g; every wave done reading group g - 1's stage
     if constexpr (G::NSTAGE == 2 && g + 1 < NG) stage(g + 1, st ^ 1);
     const char* base = smem + st * STAGE;
     static_for<KPG>([&](auto kc) __attribute__((always_inline)) {
-      constexpr int k = decltype(kc)::value, tap = k / NB, blk = k % NB, s = g * KPG + k, q = s & 1;
+      constexpr int k = decltype(kc)::value, tap = k / NB, blk = k % NB, s = g * KPG + k, q = s % WD;
       constexpr int dy = tap / 3, dx = tap % 3;
-      if constexpr (s + 1 < NKS) wload(wbh[q ^ 1], wbl[q ^ 1], s + 1);
+      if constexpr (s + WD - 1 < NKS) wload(wbh[(s + WD - 1) % WD], wbl[(s + WD - 1) % WD], s + WD - 1);
       // (pitches that are multiples of 8 keep the row shift out of the swizzled offset: fewer live offsets -
       // folding it in spilled the two-workgroup 28x28 form)
       constexpr int sh = PITCH % 8 == 0 ? dx : dy * PITCH + dx, rsh = PITCH % 8 == 0 ? dy * PITCH : 0;
       const unsigned oh = boff(sh, blk * 4 + kg), ol = SPLIT ? boff(sh, 8 + blk * 4 + kg) : 0u;
       if (p.dbg & 2) return;   // tuning only: no MFMAs
+      if constexpr (G::PF) {
+        // the hi fragments were read at the previous k-step (the group's first: here), the lo ones at the top
+        // of this one; the next k-step's hi fragments are requested before the last MFMA pass (same passes,
+        // same order per accumulator)
+        constexpr int cur = k & 1;
+        if constexpr (k == 0) {
+#pragma unroll
+          for (int t = 0; t < TP; ++t) bhp[cur][t] = *reinterpret_cast<const f16x8*>(base + oh + (fslot(t) + rsh) * SB);
+        }
+        f16x8 bl[TP];
+#pragma unroll
+        for (int t = 0; t < TP; ++t) bl[t] = *reinterpret_cast<const f16x8*>(base + ol + (fslot(t) + rsh) * SB);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int a = 0; a < TC; ++a)
+#pragma unroll
+          for (int t = 0; t < TP; ++t)
+            acc[a][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wbl[q][a], bhp[cur][t], acc[a][t], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int a = 0; a < TC; ++a)
+#pragma unroll
+          for (int t = 0; t < TP; ++t)
+            acc[a][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wbh[q][a], bhp[cur][t], acc[a][t], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (k + 1 < KPG) {
+          constexpr int tap1 = (k + 1) / NB, blk1 = (k + 1) % NB, dy1 = tap1 / 3, dx1 = tap1 % 3;
+          constexpr int sh1 = PITCH % 8 == 0 ? dx1 : dy1 * PITCH + dx1, rsh1 = PITCH % 8 == 0 ? dy1 * PITCH : 0;
+          const unsigned oh1 = boff(sh1, blk1 * 4 + kg);
+#pragma unroll
+          for (int t = 0; t < TP; ++t)
+            bhp[cur ^ 1][t] = *reinterpret_cast<const f16x8*>(base + oh1 + (fslot(t) + rsh1) * SB);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int a = 0; a < TC; ++a)
+#pragma unroll
+          for (int t = 0; t < TP; ++t)
+            acc[a][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wbh[q][a], bl[t], acc[a][t], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        return;
+      }
       static_for<TP / TPG>([&](auto pc) __attribute__((always_inline)) {
         constexpr int t0 = decltype(pc)::value * TPG;
         f16x8 bh[TPG], bl[SPLIT ? TPG : 1];
@@ -237,7 +295,7 @@ __global__ __launch_bounds__(512, 2 * OCC) void conv_hxi(ConvParams p) {
   const int cg = threadIdx.x % CGN, pl0 = threadIdx.x / CGN;
 #pragma unroll
   for (int pass = 0; pass < NPASS; ++pass) {
-    const int ch = pass * PC + cg * 8;
+    const int ch = cb * COUT + pass * PC + cg * 8;
     // per-thread channel terms (one 8-channel group for all of the thread's pixels): channel bias (0
     // otherwise, as conv_epilogue_lds adds it), negative-side slope (PReLU / 0 for ReLU / 1)
     float bc[8], sl[8];
@@ -248,9 +306,9 @@ __global__ __launch_bounds__(512, 2 * OCC) void conv_hxi(ConvParams p) {
     }
     // the per-pixel term of each of the thread's items, requested before anything waits on it: the
     // residual hi + lo (its f32 value), or the border-class bias of a folded pre-BN conv
-    // (two workgroups per CU: loaded at the item instead - the other workgroup covers the latency, and
+    // (four waves per SIMD - two 8-wave workgroups per CU: loaded at the item instead - the other workgroup covers the latency, and
     // the registers are not there)
-    constexpr bool PREF = OCC == 1;
+    constexpr bool PREF = G::WPS <= 2;
     float pre[PREF ? IT : 1][8];
     auto load_pre = [&](int k, float* dst) __attribute__((always_inline)) {
       const int pl = pl0 + PSTEP * k;
@@ -365,6 +423,14 @@ __global__ __launch_bounds__(512, 2 * OCC) void conv_hxi(ConvParams p) {
 // 7x7x512 (the last stage, split only): one image per workgroup at pitch 9 - 63 slots in 4 fragments
 // (77 % kept; a pitch of 16 would keep 44 %), 8 x 1 waves of 64 channels x 4 fragments
 #define PC_HXI_7 7, 9, 7, 512, 512, 8, 1
+// small-batch forms (a per-frame extract()'s ~12 ArcFace rows: 12 one-image workgroups would idle 244
+// CUs, and conv_fast's 64x64 tile re-stages every pixel per tap and is bound by the LDS port): 32 output
+// channels of 7 rows per workgroup - 16 workgroups per image (2 or 4 waves of 16 or 32 channels x 7
+// fragments, or 4 at the 7x7 map), the rows' halo staged per 64-channel group as above. Same K order,
+// MFMA order and epilogue: the same bits as every other form (tests/test_gpu_arcface.py)
+#define PC_HXI_14S 14, 16, 7, 256, 32, 2, 1
+#define PC_HXI_28S 28, 32, 7, 128, 32, 2, 2
+#define PC_HXI_7S 7, 9, 7, 512, 32, 2, 1
 
 // can a conv run here: one segment of C channels (split: X.C 2 C = [hi | lo]; plain f16: X.C C), dense,
 // on an HW x HW map of an instantiated shape, C output channels written in the same form (dense), 3x3
@@ -381,10 +447,16 @@ int conv_hxi_ok(const ConvParams& p) {
          p.wfrag != nullptr && (!split || p.ysplit == C);
 }
 
-hipError_t conv_hxi_launch(const ConvParams& p, hipStream_t s) {
+hipError_t conv_hxi_launch(const ConvParams& p, int small, hipStream_t s) {
   if (!conv_hxi_ok(p)) return hipErrorInvalidValue;
   const bool split = p.ysplit != 0;
-  if (p.OH == 7) {
+  if (small) {   // (16 workgroups per image; split only)
+    if (!split) return hipErrorInvalidValue;
+    const dim3 grid(p.N * 16);
+    if (p.OH == 7) hipLaunchKernelGGL((conv_hxi<PC_HXI_7S, true, 2>), grid, dim3(128), 0, s, p);
+    else if (p.OH == 14) hipLaunchKernelGGL((conv_hxi<PC_HXI_14S, true, 2>), grid, dim3(128), 0, s, p);
+    else hipLaunchKernelGGL((conv_hxi<PC_HXI_28S, true, 1>), grid, dim3(256), 0, s, p);
+  } else if (p.OH == 7) {
     hipLaunchKernelGGL((conv_hxi<PC_HXI_7, true, 1>), dim3(p.N), dim3(512), 0, s, p);
   } else if (p.OH == 14) {
     // (half an image per workgroup at two per CU, 7 rows: 147.7 vs 145.3 us, profiles/r06t_hxi14_half_ab.txt)

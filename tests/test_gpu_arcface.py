@@ -210,6 +210,36 @@ def test_arcface_f16x3_hxi_bit_identical(gpu_ctx, monkeypatch, batch):
     assert np.array_equal(outs[0].view(np.uint8), outs[2].view(np.uint8))
 
 
+@pytest.mark.parametrize("batch", [1, 12, 30])
+def test_arcface_f16x3_hxi_small_bit_identical(gpu_ctx, monkeypatch, batch):
+    """conv_hxi's small-batch forms (PC_CONV_HXI bit 5; codes 506 / 507 / 508: 32 output channels of 7 rows
+    per workgroup, 16 workgroups per image) run the 14x14x256 / 28x28x128 / 7x7x512 layers of the plans for
+    <= 32 images - a per-frame extract()'s rows - and give the fused tiles' bits (PC_CONV_HXI=0)."""
+    from person_capture_amd.runtime import Net
+    P = models.compile_iresnet(models.synth_iresnet(100, seed=12), 100, split=True)
+    x = np.zeros((batch, 112, 112, 4), np.float16)
+    x[..., :3] = np.random.default_rng(13).uniform(-127.5, 127.5, (batch, 112, 112, 3))
+    d = gpu_ctx.upload(x)
+    outs, codes = [], []
+    try:
+        for hxi in ("59", "0"):
+            monkeypatch.setenv("PC_CONV_HXI", hxi)
+            net = Net(gpu_ctx, P.serialize(), PC_PREC_F16, max_batch=512)
+            try:
+                net.profile(True)
+                net.run(d.ptr, batch)
+                codes.append([int(r[4]) for r in net.profile_ops()])
+                net.profile(False)
+                outs.append(net.read_output(0, batch).copy())
+            finally:
+                net.close()
+    finally:
+        d.free()
+    assert [sum(1 for c in codes[0] if c == k) for k in (506, 507, 508)] == [58, 24, 4], codes[0]
+    assert not {502, 503, 505, 506, 507, 508} & set(codes[1])
+    assert np.array_equal(outs[0].view(np.uint8), outs[1].view(np.uint8))
+
+
 def test_arcface_f16_hxi_bit_identical(gpu_ctx, monkeypatch):
     """The plain f16 form of conv_hxi (BASELINE C2's fp16 net: the halo holds every input channel, K walks
     taps then 32-channel blocks - the plain tiles' and the resident chain's order) on the 14x14x256 and

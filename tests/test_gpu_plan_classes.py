@@ -52,11 +52,13 @@ def test_arcface_small_batches_bit_identical_to_large_batch(gpu_ctx, depth, mode
             d.free()
         large_forms, rows_differ = {}, 0
         (large,), _ = _run(gpu_ctx, net, x, 200, 1, large_forms)
-        ran_small = 0
+        ran_small = ran_hxs = 0
         for N in (1, 2, 5, 12, 30, 64):
             small_forms = {}
             (small,), codes = _run(gpu_ctx, net, x, N, 1, small_forms)
-            ran_small += sum(1 for c in codes if 115 <= c % 500 < 120)   # conv_fast small-batch tiles (C8: 615..)
+            # conv_fast small-batch tiles (C8: 615..), conv_hxi's small-batch forms (f16x3: 506-508)
+            ran_small += sum(1 for c in codes if 115 <= c % 500 < 120 or 506 <= c <= 508)
+            ran_hxs += sum(1 for c in codes if 506 <= c <= 508)
             # fused split tiles of one conv at different K-row widths in the two classes (the
             # channel-group K order makes them accumulate alike)
             rows_differ += sum(1 for op, (c, f) in small_forms.items() if 100 <= c < 200 and f & 1 and
@@ -67,6 +69,7 @@ def test_arcface_small_batches_bit_identical_to_large_batch(gpu_ctx, depth, mode
         assert ran_small >= 100, ran_small
         if mode == "f16x3":
             assert rows_differ > 0
+            assert ran_hxs == 5 * 86, ran_hxs   # (N = 1 .. 30: 58 + 24 + 4 layers each; 64 rows: the tiles)
     finally:
         net.close()
 
