@@ -490,6 +490,8 @@ def _kernel_of(code: float, cfg: float) -> str:
         return "conv_hxi<28,32,7,128,128,4,2> (image-resident, 7 rows of a 28x28 image per workgroup, pc_conv_hxi.hip)"
     if c == 505:
         return "conv_hxi<7,9,7,512,512,8,1> (image-resident, one 7x7 image per workgroup at pitch 9, pc_conv_hxi.hip)"
+    if c == 504:
+        return "conv_hxg<96,96,1,32,2> (small-batch form: 32 channels of a 16x4 block per workgroup, pc_conv_hx.hip)"
     if c in (506, 507, 508):
         shape = {506: "14,16,7,256,32,2,1", 507: "28,32,7,128,32,2,2", 508: "7,9,7,512,32,2,1"}[c]
         return f"conv_hxi<{shape}> (small-batch form: 32 channels of 7 rows per workgroup, pc_conv_hxi.hip)"
@@ -646,7 +648,7 @@ def _traffic_for(dominant, code, prec="f16"):
         return None
     # the halo-staged kernels: one instantiation per code
     hx_names = {500: "conv_hx64", 501: "conv_hxg<96, 96", 502: "conv_hxi<14, 16, 14", 503: "conv_hxi<28, 32, 7, 128, 128",
-                505: "conv_hxi<7, 9, 7, 512, 512", 506: "conv_hxi<14, 16, 7", 507: "conv_hxi<28, 32, 7, 128, 32",
+                505: "conv_hxi<7, 9, 7, 512, 512", 504: "conv_hxg<96, 96, 1, 32", 506: "conv_hxi<14, 16, 7", 507: "conv_hxi<28, 32, 7, 128, 32",
                 508: "conv_hxi<7, 9, 7, 512, 32"}
     if code in hx_names:
         return dominant.get("hbm_bytes_per_launch") if hx_names[code] in dominant.get("kernel", "") else None

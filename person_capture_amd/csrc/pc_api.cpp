@@ -30,7 +30,7 @@ hipError_t conv_launch(int f32, int rowb, int cfg, const ConvParams& p, hipStrea
 hipError_t conv_halo_launch(int f32, int cfg, const ConvParams& p, hipStream_t s);
 hipError_t conv_fast_launch(int f32, int rowb, int cfg, const ConvParams& p, hipStream_t s);
 hipError_t conv_hx_launch(const ConvParams& p, hipStream_t s);
-hipError_t conv_hxg_launch(const ConvParams& p, hipStream_t s);
+hipError_t conv_hxg_launch(const ConvParams& p, int small, hipStream_t s);
 hipError_t conv_hxi_launch(const ConvParams& p, int small, hipStream_t s);
 int conv_fast_num_cfgs();
 constexpr int kFastSmallCfg0 = 15, kFastSmallCfg1 = 19;   // conv_fast tiles 15..19: small-batch plans only
@@ -918,11 +918,16 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
         w[5] == 3 && w[6] == 1 && w[7] == 1 && X.H == Y.H && X.W == Y.W && w[15] == 9 * 288 &&
         !(w[21] >= 0 && (w[22] == RES_UP2 || !n->tens[w[21]].split || n->tens[w[21]].c8)) &&
         (double)X.H * X.W * n->max_batch * X.cs * esz + kZeroTail < 4294967296.0 &&
-        plan_batch * ((Y.H + 19) / 20) * ((Y.W + 15) / 16) >= 128 &&
         !(getenv("PC_CONV_HXG") && atoi(getenv("PC_CONV_HXG")) == 0)) {
-      // (one 16x20 block per CU; smaller grids - a single frame's 80x80 map is 20 blocks - keep the
-      // fused tiles, bit-identical: conv_hxg walks K and the MFMA passes in their order)
-      pl.hx = 2;
+      // (one 16x20 block per CU; smaller grids - a single frame's 80x80 map is 20 blocks - take the
+      // small-batch form, 16x4 blocks x 32 channels (PC_CONV_HXG bit 1; 80x80 / 40x40 maps, 20x20 in the plans
+      // for <= 16 frames; SCRFD-x3 at one frame 1.20 -> 0.98 ms, profiles/r06bm_*), or the fused
+      // tiles: bit-identical, conv_hxg walks K and the MFMA passes in their order)
+      const int hxg_mask = getenv("PC_CONV_HXG") ? atoi(getenv("PC_CONV_HXG")) : 3;
+      if (plan_batch * ((Y.H + 19) / 20) * ((Y.W + 15) / 16) >= 128 && (hxg_mask & 1)) pl.hx = 2;
+      else if ((hxg_mask & 2) && (Y.H >= 40 || plan_batch <= 16)) pl.hx = 5;   // (profile code 504)
+    }
+    if (pl.hx == 2 || pl.hx == 5) {
       pl.fast = pl.halo = pl.t2d = -1;
       pl.sx = 0;
     }
@@ -1721,10 +1726,10 @@ static int run_ops(pc_net* n, int N, hipStream_t s) {
       p.partial = n->partial;
       p.zero = c->zero;
       if (const char* e = getenv("PC_CONV_DBG")) p.dbg = atoi(e);
-      if (pl.hx >= 3) {
+      if (pl.hx >= 3 && pl.hx != 5) {
         HIPCHK(c, conv_hxi_launch(p, pl.hx >= 7, s));
-      } else if (pl.hx == 2) {
-        HIPCHK(c, conv_hxg_launch(p, s));
+      } else if (pl.hx == 2 || pl.hx == 5) {
+        HIPCHK(c, conv_hxg_launch(p, pl.hx == 5, s));
       } else if (pl.hx) {
         HIPCHK(c, conv_hx_launch(p, s));
       } else if (pl.t2d >= 0) {

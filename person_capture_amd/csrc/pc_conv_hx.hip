@@ -269,24 +269,30 @@ __global__ __launch_bounds__(256, 2) void conv_hx64(ConvParams p, int nby, int n
 //    per k-step and fragment the MFMAs are SX's: W_lo*x_hi, W_hi*x_hi, W_hi*x_lo (so a plan class may
 //    take the fused tiles instead: same accumulators);
 //  * epilogue: conv_hx64's (f32 image over the LDS, 16-byte hi and lo stores per pixel and 8 channels).
-template <int CIN, int COUT, int TP>
-__global__ __launch_bounds__(256, 1) void conv_hxg(ConvParams p, int nby, int nbx) {
-  constexpr int TC = COUT / 16, NG = CIN / 32, NKS = 9 * NG;
+// Small-batch form (CO < COUT, a single frame's 80x80 / 40x40 maps, whose 16x20 blocks are a few dozen):
+// a workgroup computes CO of the output channels of a 16 x 4 TP block - COUT / CO workgroups per block,
+// each staging the block's halo - at several workgroups per CU (WPE waves per SIMD). Same K order, MFMA
+// order and epilogue per output: the same bits.
+template <int CIN, int COUT, int TP, int CO = COUT, int WPE = 1>
+__global__ __launch_bounds__(256, WPE) void conv_hxg(ConvParams p, int nby, int nbx) {
+  constexpr int TC = CO / 16, NG = CIN / 32, NKS = 9 * NG, CB = COUT / CO;
   constexpr int BW = 16, BH = 4 * TP, PW = BW + 2, SLOTS = (BH + 2) * PW;
   constexpr int SB = 128;                                    // slot: 32 hi + 32 lo f16 channels
   constexpr int PIECES = ((SLOTS * SB + 1023) / 1024 + 3) / 4 * 4;   // 1 KiB DMA pieces per stage, 4 waves alike
   constexpr int STAGE = PIECES * 1024;
-  constexpr int RS = COUT + 4;                               // epilogue image row (floats)
+  constexpr int RS = CO + 4;                                 // epilogue image row (floats)
   constexpr int EPI = BH * BW * RS * 4;
   constexpr int SMEM = 2 * STAGE > EPI ? 2 * STAGE : EPI;
   static_assert(COUT % 16 == 0 && CIN % 32 == 0 && CIN % 64 != 0, "32-channel groups (pack_wfrag gt 1)");
+  static_assert(COUT % CO == 0 && CO % 16 == 0, "channel blocks");
   static_assert(SMEM <= 163840, "LDS");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
   const ConvSeg& S = p.seg[0];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nblk = p.N * nby * nbx;
-  const int b = xcd_remap(blockIdx.x, nblk);
+  const int nblk = p.N * nby * nbx * CB;
+  const int bq = xcd_remap(blockIdx.x, nblk);
+  const int cb = bq % CB, b = bq / CB;   // (a block's CB workgroups consecutive: one XCD, one halo in its L2)
   const int n = b / (nby * nbx), rem = b - n * (nby * nbx);
   const int oy0 = (rem / nbx) * BH, ox0 = (rem - (rem / nbx) * nbx) * BW;
   const int H = S.H, W = S.W;
@@ -326,12 +332,13 @@ __global__ __launch_bounds__(256, 1) void conv_hxg(ConvParams p, int nby, int nb
   };
   // weight fragments of k-step s = 32-channel group s / 9, tap s % 9 (packed K tile s): TC row blocks
   // x [W_hi, W_lo] x 1 KiB (lane l: row 16 a + (l & 15), channels 8 (l >> 4) .. +8)
-  constexpr int TILE = TC * 2 * 1024;
+  constexpr int TILE = COUT / 16 * 2 * 1024;
+  const int wo = lane * 16 + cb * TC * 2 * 1024;   // this workgroup's row blocks cb TC ..
   auto wload = [&](f16x8* wh, f16x8* wl, int s) __attribute__((always_inline)) {
 #pragma unroll
     for (int a = 0; a < TC; ++a) {
-      wh[a] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16 + (a * 2) * 1024, s * TILE, 0));
-      wl[a] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16 + (a * 2 + 1) * 1024, s * TILE, 0));
+      wh[a] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, wo + (a * 2) * 1024, s * TILE, 0));
+      wl[a] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, wo + (a * 2 + 1) * 1024, s * TILE, 0));
     }
   };
   f16x8 wbh[2][TC], wbl[2][TC];
@@ -402,10 +409,10 @@ __global__ __launch_bounds__(256, 1) void conv_hxg(ConvParams p, int nby, int nb
   const bool pre_act = !p.act_after_res;
   // a thread keeps one 8-channel group (threads past the last whole pixel lane idle), so the channel
   // terms load once; the pixels' residual rows are requested before the first store
-  constexpr int CGN = COUT / 8, PL = 256 / CGN, NPX = BH * BW, ITP = (NPX + PL - 1) / PL;
+  constexpr int CGN = CO / 8, PL = 256 / CGN, NPX = BH * BW, ITP = (NPX + PL - 1) / PL;
   const int cg = threadIdx.x % CGN, pl0 = threadIdx.x / CGN;
   if (pl0 >= PL) return;
-  const int ch = cg * 8;
+  const int ch = cb * CO + cg * 8;
   float bc[8], sl[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -434,8 +441,8 @@ __global__ __launch_bounds__(256, 1) void conv_hxg(ConvParams p, int nby, int nb
       const int oy = oy0 + pl / BW, ox = ox0 + (pl & (BW - 1));
       if (oy >= OH || ox >= OW) continue;
       const long long pix = ((long long)n * OH + oy) * OW + ox;
-      const f32x4 lo4 = *reinterpret_cast<const f32x4*>(im + pl * RS + ch);
-      const f32x4 hi4 = *reinterpret_cast<const f32x4*>(im + pl * RS + ch + 4);
+      const f32x4 lo4 = *reinterpret_cast<const f32x4*>(im + pl * RS + cg * 8);
+      const f32x4 hi4 = *reinterpret_cast<const f32x4*>(im + pl * RS + cg * 8 + 4);
       float v[8] = {lo4[0] + bc[0], lo4[1] + bc[1], lo4[2] + bc[2], lo4[3] + bc[3],
                     hi4[0] + bc[4], hi4[1] + bc[5], hi4[2] + bc[6], hi4[3] + bc[7]};
       if (p.bias_mode == BIAS_BORDER9) {
@@ -490,8 +497,13 @@ int conv_hxg_ok(const ConvParams& p) {
          p.ycs % 8 == 0 && p.cwrite == 96 && p.wfrag != nullptr;
 }
 
-hipError_t conv_hxg_launch(const ConvParams& p, hipStream_t s) {
+hipError_t conv_hxg_launch(const ConvParams& p, int small, hipStream_t s) {
   if (!conv_hxg_ok(p)) return hipErrorInvalidValue;
+  if (small) {   // 16x4 blocks x 32 of the 96 output channels, 3 workgroups per block
+    const int nby = (p.OH + 3) / 4, nbx = (p.OW + 15) / 16;
+    hipLaunchKernelGGL((conv_hxg<96, 96, 1, 32, 2>), dim3(p.N * nby * nbx * 3), dim3(256), 0, s, p, nby, nbx);
+    return hipGetLastError();
+  }
   const int nby = (p.OH + 4 * HXG_TP - 1) / (4 * HXG_TP), nbx = (p.OW + 15) / 16;
   hipLaunchKernelGGL((conv_hxg<96, 96, HXG_TP>), dim3(p.N * nby * nbx), dim3(256), 0, s, p, nby, nbx);
   return hipGetLastError();
