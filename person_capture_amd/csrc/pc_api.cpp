@@ -914,8 +914,10 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
     // 96 -> 96 channel layers (SCRFD's 80x80 / 40x40 / 20x20 x96 trunk) on conv_hxg<96, 96>: one
     // workgroup per CU, every output channel per wave, the halo staged per 32-channel group
     // (PC_CONV_HXG=0 disables, for A/B)
-    if (X.split && !X.c8 && !Y.c8 && X.C == 192 && X.cs == 192 && Y.split && Y.C == 192 && npad == 96 && w[4] == 3 &&
-        w[5] == 3 && w[6] == 1 && w[7] == 1 && X.H == Y.H && X.W == Y.W && w[15] == 9 * 288 &&
+    // (and SCRFD's 20x20x224 neck layers, small-batch form only)
+    const bool c224 = X.C == 448 && Y.H == 20 && plan_batch <= 16;
+    if (X.split && !X.c8 && !Y.c8 && (X.C == 192 || c224) && X.cs == X.C && Y.split && Y.C == X.C && npad == X.C / 2 &&
+        w[4] == 3 && w[5] == 3 && w[6] == 1 && w[7] == 1 && X.H == Y.H && X.W == Y.W && w[15] == 27 * npad &&
         !(w[21] >= 0 && (w[22] == RES_UP2 || !n->tens[w[21]].split || n->tens[w[21]].c8)) &&
         (double)X.H * X.W * n->max_batch * X.cs * esz + kZeroTail < 4294967296.0 &&
         !(getenv("PC_CONV_HXG") && atoi(getenv("PC_CONV_HXG")) == 0)) {
@@ -924,7 +926,7 @@ static int plan_conv(pc_net* n, const NetOp& op, ConvPlan& pl, long long plan_ba
       // for <= 16 frames; SCRFD-x3 at one frame 1.20 -> 0.98 ms, profiles/r06bm_*), or the fused
       // tiles: bit-identical, conv_hxg walks K and the MFMA passes in their order)
       const int hxg_mask = getenv("PC_CONV_HXG") ? atoi(getenv("PC_CONV_HXG")) : 3;
-      if (plan_batch * ((Y.H + 19) / 20) * ((Y.W + 15) / 16) >= 128 && (hxg_mask & 1)) pl.hx = 2;
+      if (plan_batch * ((Y.H + 19) / 20) * ((Y.W + 15) / 16) >= 128 && (hxg_mask & 1) && !c224) pl.hx = 2;
       else if ((hxg_mask & 2) && (Y.H >= 40 || plan_batch <= 16)) pl.hx = 5;   // (profile code 504)
     }
     if (pl.hx == 2 || pl.hx == 5) {

@@ -487,21 +487,26 @@ __global__ __launch_bounds__(256, WPE) void conv_hxg(ConvParams p, int nby, int 
 
 constexpr int HXG_TP = 5;   // 16 x 20 output blocks: 80 / 20 rows, no waste on the 80x80 maps
 
-// can a conv run on conv_hxg<96, 96>: split 96-channel input (X.C 192 = [hi | lo]), 96 output
-// channels written split, 3x3 stride 1 pad 1, same size, plain or same-size split residual
-int conv_hxg_ok(const ConvParams& p) {
+// can a conv run on conv_hxg<C, C>: split C-channel input (X.C 2 C = [hi | lo]), C output channels written
+// split, 3x3 stride 1 pad 1, same size, plain or same-size split residual; C = 96 (both forms) or 224 (SCRFD's
+// 20x20x224 neck, the small-batch form)
+int conv_hxg_ok(const ConvParams& p, int small) {
   const ConvSeg& S = p.seg[0];
-  return p.nseg == 1 && S.C == 192 && S.cs == 192 && S.KH == 3 && S.KW == 3 && S.stride == 1 && S.pad == 1 &&
-         S.H == p.OH && S.W == p.OW && p.npad == 96 && p.ysplit == 96 && p.splitk == 1 && !p.out_f32 &&
-         p.ktot == 9 * 288 && p.res_mode != RES_UP2 && (p.res_mode == RES_NONE || (p.rsplit == 96 && p.rcs % 8 == 0)) &&
-         p.ycs % 8 == 0 && p.cwrite == 96 && p.wfrag != nullptr;
+  const int C = S.C / 2;
+  return p.nseg == 1 && (C == 96 || (small && C == 224)) && S.cs == 2 * C && S.KH == 3 && S.KW == 3 && S.stride == 1 &&
+         S.pad == 1 && S.H == p.OH && S.W == p.OW && p.npad == C && p.ysplit == C && p.splitk == 1 && !p.out_f32 &&
+         p.ktot == 27 * C && p.res_mode != RES_UP2 && (p.res_mode == RES_NONE || (p.rsplit == C && p.rcs % 8 == 0)) &&
+         p.ycs % 8 == 0 && p.cwrite == C && p.wfrag != nullptr;
 }
 
 hipError_t conv_hxg_launch(const ConvParams& p, int small, hipStream_t s) {
-  if (!conv_hxg_ok(p)) return hipErrorInvalidValue;
-  if (small) {   // 16x4 blocks x 32 of the 96 output channels, 3 workgroups per block
+  if (!conv_hxg_ok(p, small)) return hipErrorInvalidValue;
+  if (small) {   // 16x4 blocks x 32 of the C output channels, C / 32 workgroups per block
     const int nby = (p.OH + 3) / 4, nbx = (p.OW + 15) / 16;
-    hipLaunchKernelGGL((conv_hxg<96, 96, 1, 32, 2>), dim3(p.N * nby * nbx * 3), dim3(256), 0, s, p, nby, nbx);
+    if (p.npad == 224)
+      hipLaunchKernelGGL((conv_hxg<224, 224, 1, 32, 2>), dim3(p.N * nby * nbx * 7), dim3(256), 0, s, p, nby, nbx);
+    else
+      hipLaunchKernelGGL((conv_hxg<96, 96, 1, 32, 2>), dim3(p.N * nby * nbx * 3), dim3(256), 0, s, p, nby, nbx);
     return hipGetLastError();
   }
   const int nby = (p.OH + 4 * HXG_TP - 1) / (4 * HXG_TP), nbx = (p.OW + 15) / 16;
